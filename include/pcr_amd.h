@@ -1,0 +1,208 @@
+/*
+ * pcr_amd.h -- C ABI of libpcr_amd.so, the MI355X (gfx950) implementation of
+ * the rotation-invariant-feature hot path of
+ * Gilgamesh666666/Point-cloud-registration-based-on-rotation-invariant-feature.
+ *
+ * Each entry point replaces one function of the reference's pybind11 module
+ * `_multi_shape_pvcnn_backend` (PVCNN/modules/functional/src/bindings.cpp) or
+ * one PyTorch block of the reference model; the citation above every
+ * declaration names the interface it replaces (paths relative to the
+ * reference's PVCNN/ directory).
+ *
+ * Conventions
+ *  - Plain device pointers (HIP device memory), sizes as int, layouts exactly
+ *    as the reference's tensors (channel-major [B, C, N] fp32, int32 indices).
+ *  - The caller owns every buffer.  Outputs are FULLY written by the library,
+ *    including the slots the reference leaves at their torch::zeros /
+ *    ones*10000 fill, so callers may pass uninitialised (torch.empty) memory.
+ *  - `stream` is a hipStream_t (NULL = legacy default stream).  Work is only
+ *    enqueued; nothing synchronises, allocates or frees, so every call is
+ *    hipGraph-capturable.  Calls needing scratch take a caller-provided
+ *    workspace whose size comes from the matching *_workspace_size().
+ *  - Return value: PCR_OK or a negative pcr_status; pcr_last_error() holds a
+ *    message (thread-local).  The reference instead exit(-1)s on a launch
+ *    failure (src/cuda_utils.cuh:28-37).
+ */
+#ifndef PCR_AMD_H
+#define PCR_AMD_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int pcr_status;
+#define PCR_OK 0
+#define PCR_ERR_INVALID (-1)
+#define PCR_ERR_LAUNCH (-2)
+#define PCR_ERR_UNSUPPORTED (-3)
+
+/* Last error message of the calling thread ("" when none). */
+const char *pcr_last_error(void);
+/* Library version string. */
+const char *pcr_version(void);
+
+/* ---------------------------------------------------------------- KNN ----
+ * knn_forward_cuda (modules/functional/src/knn/knn.cpp:6-25, kernel
+ * knn/knn.cu:5-49, both directions): xyz1 [b,c,n], xyz2 [b,c,m] ->
+ * dist1 [b,k,n], idx1 [b,k,n] (into xyz2), dist2 [b,k,m], idx2 [b,k,m].
+ * Squared L2, ascending, ties by lower index, unfilled slots (10000, 0). */
+pcr_status pcr_knn_forward(const float *xyz1, const float *xyz2, int b, int c, int n, int m,
+                           int k, float *dist1, float *dist2, int *idx1, int *idx2,
+                           void *stream);
+
+/* knn_backward_cuda (knn/knn.cpp:27-52, kernel knn/knn.cu:52-78, :88-98).
+ * gradxyz1 [b,c,n], gradxyz2 [b,c,m]; both directions accumulate into both. */
+pcr_status pcr_knn_backward(const float *xyz1, const float *xyz2, const float *graddist1,
+                            const float *graddist2, const int *idx1, const int *idx2, int b,
+                            int c, int n, int m, int k, float *gradxyz1, float *gradxyz2,
+                            void *stream);
+
+/* ---------------------------------------------------------------- PPF ----
+ * spherical_ppf_forward (modules/functional/src/spherical_ppf/ppf.cpp:17-36,
+ * kernel ppf.cu:19-92).  Argument order of the BACKEND (points first); the
+ * Python ppf() wrapper swaps (modules/functional/ppf.py:20).
+ * coords/center/normals/center_normal [b,3,n] -> feat [b,4,n]. */
+pcr_status pcr_spherical_ppf_forward(const float *coords, const float *center,
+                                     const float *normals, const float *center_normal, int b,
+                                     int n, float *feat, void *stream);
+
+/* Local k-neighbour PPF of the model (models/pvcnn_classify.py:252-269:
+ * BallQuery grouping of coords+normals, d = c - (p - c), three acos + |d|),
+ * fused with the grouping.  points/normals [b,3,n]; centers/center_normals
+ * [b,3,m]; idx either [b,m,u] (ball_query layout, idx_kmajor=0) or [b,u,m]
+ * (knn layout, idx_kmajor=1).  relative=1 reproduces the model (grouped
+ * coordinates are relative to the centre), relative=0 uses d = c - p.
+ * out [b,4,u,m] = (nr_d, ni_d, nr_ni, |d|). */
+pcr_status pcr_local_ppf_forward(const float *points, const float *normals, const float *centers,
+                                 const float *center_normals, const int *idx, int b, int n,
+                                 int m, int u, int idx_kmajor, int relative, float *out,
+                                 void *stream);
+
+/* Fused self-KNN + local PPF (the extractor's neighbour stage): for every
+ * point of xyz [b,3,n] its k nearest points (self included, knn semantics)
+ * -> idx [b,k,n] (may be NULL), dist [b,k,n] (may be NULL) and the local PPF
+ * [b,4,k,n] of (point, neighbour) with `relative` as above. */
+pcr_status pcr_knn_local_ppf(const float *xyz, const float *normals, int b, int n, int k,
+                             int relative, int *idx, float *dist, float *ppf, void *stream);
+
+/* ------------------------------------------------ ball query / grouping --
+ * ball_query (ball_query/ball_query.cpp:6-30, kernel ball_query.cu:19-50):
+ * centers [b,3,m], points [b,3,n] -> idx [b,m,u]. */
+pcr_status pcr_ball_query(const float *centers, const float *points, int b, int m, int n,
+                          float radius, int u, int *idx, void *stream);
+
+/* grouping_forward (grouping/grouping.cpp:6-24, grouping.cu:18-36):
+ * features [b,c,n], indices [b,m,u] -> out [b,c,m,u]. */
+pcr_status pcr_grouping_forward(const float *features, const int *indices, int b, int c, int n,
+                                int m, int u, float *out, void *stream);
+
+/* grouping_backward (grouping.cpp:26-44, grouping.cu:58-85):
+ * grad_y [b,c,m,u], indices [b,m,u] -> grad_x [b,c,n]. */
+pcr_status pcr_grouping_backward(const float *grad_y, const int *indices, int b, int c, int n,
+                                 int m, int u, float *grad_x, void *stream);
+
+/* ------------------------------------------------------- voxelization ----
+ * Scratch for the voxelizers: per-cloud sort permutation, occupied-voxel
+ * segments and an occupancy bitmap with word prefix counts. */
+size_t pcr_voxelize_workspace_size(int b, int n, int r);
+
+/* spherical_avg_voxelize_forward (spherical_voxelization/spherical_vox.cpp:17-46,
+ * kernels spherical_vox.cu:19-125): features [b,c,n], normalised coords
+ * [b,3,n] -> out [b,c,r^3] (voxel mean), ind [b,n] (-1 = dropped),
+ * cnt [b,r^3].  Means are accumulated in ascending point order. */
+pcr_status pcr_spherical_avg_voxelize_forward(const float *features, const float *coords, int b,
+                                              int c, int n, int r, float *out, int *ind, int *cnt,
+                                              void *workspace, size_t workspace_bytes,
+                                              void *stream);
+
+/* avg_voxelize_forward (voxelization/vox.cpp:17-46, vox.cu:18-73): cube
+ * variant on int voxel coords [b,3,n]. */
+pcr_status pcr_avg_voxelize_forward(const float *features, const int *coords, int b, int c,
+                                    int n, int r, float *out, int *ind, int *cnt,
+                                    void *workspace, size_t workspace_bytes, void *stream);
+
+/* spherical_avg_voxelize_backward (spherical_vox.cpp:57-79, spherical_vox.cu:139-163)
+ * and avg_voxelize_backward (vox.cpp:57-76, vox.cu:87-111): grad_y [b,c,r3],
+ * ind [b,n], cnt [b,r3] -> grad_x [b,c,n]. */
+pcr_status pcr_avg_voxelize_backward(const float *grad_y, const int *ind, const int *cnt, int b,
+                                     int c, int n, int r3, float *grad_x, void *stream);
+
+/* Spherical_Voxelization's coordinate normalisation
+ * (modules/spherical_vox.py:16-20) with a fixed reduction order:
+ * coords [b,3,n] -> norm_coords [b,3,n]. */
+pcr_status pcr_spherical_normalize(const float *coords, int b, int n, float *norm_coords,
+                                   void *stream);
+
+/* ----------------------------------------------------- devoxelization ----
+ * spherical_trilinear_devoxelize_forward
+ * (interpolate/spherical_trilinear_devox.cpp:19-56, .cu:23-136): coords
+ * [b,3,n], features [b,c,r^3], g_inds [b,n] -> outs [b,c,n], inds [b,8,n],
+ * wgts [b,8,n].  is_training is ignored, as in the reference. */
+pcr_status pcr_spherical_trilinear_devoxelize_forward(int r, int is_training, const float *coords,
+                                                      const float *features, const int *g_inds,
+                                                      int b, int c, int n, float *outs, int *inds,
+                                                      float *wgts, void *stream);
+
+/* trilinear_devoxelize_forward (interpolate/trilinear_devox.cpp:18-56,
+ * .cu:22-106): cube variant on continuous voxel coords [b,3,n]. */
+pcr_status pcr_trilinear_devoxelize_forward(int r, int is_training, const float *coords,
+                                            const float *features, int b, int c, int n,
+                                            float *outs, int *inds, float *wgts, void *stream);
+
+/* spherical_trilinear_devoxelize_backward (spherical_trilinear_devox.cpp:68-92,
+ * .cu:150-194; skip_neg=1: points with inds[0]==-1 are skipped) and
+ * trilinear_devoxelize_backward (trilinear_devox.cpp:58-91, .cu:120-163;
+ * skip_neg=0): grad_y [b,c,n] -> grad_x [b,c,r^3]. */
+pcr_status pcr_devoxelize_backward(const float *grad_y, const int *inds, const float *wgts, int b,
+                                   int c, int n, int r, int skip_neg, float *grad_x,
+                                   void *stream);
+
+/* PVConv dgcnn centre term (modules/pvconv.py:68-89): related[b,c,i] =
+ * features[b,c,i] - avg_grid[b,c,ind[b,i]], 0 where ind == -1. */
+pcr_status pcr_dgcnn_center_gather(const float *features, const float *avg_grid, const int *ind,
+                                   int b, int c, int n, int r3, float *related, void *stream);
+
+/* ---------------------------------------------------- fused extractor ----
+ * The spherical voxel stage of the sph-dg extractor forward, fused:
+ * normalise coords -> spherical voxel index -> voxel mean grid (written
+ * once, coalesced) -> spherical devoxelisation of that grid -> per-cloud
+ * max-pooled descriptor.  Outputs (any may be NULL except grid):
+ * norm_coords [b,3,n], ind [b,n], cnt [b,r^3], grid [b,c,r^3],
+ * devox [b,c,n], dinds [b,8,n], dwgts [b,8,n], desc [b,c] (max over points of
+ * devox).  Equivalent to pcr_spherical_normalize + ..._avg_voxelize_forward +
+ * ..._trilinear_devoxelize_forward on the produced grid. */
+size_t pcr_extractor_workspace_size(int b, int n, int c, int r);
+pcr_status pcr_extractor_voxel_stage(const float *xyz, const float *features, int b, int c,
+                                     int n, int r, float *norm_coords, int *ind, int *cnt,
+                                     float *grid, float *devox, int *dinds, float *dwgts,
+                                     float *desc, void *workspace, size_t workspace_bytes,
+                                     void *stream);
+
+/* The two launches of pcr_extractor_voxel_stage, separately (so a caller can
+ * time the grid kernel with events on its stream): prep = normalise + index
+ * + sort + corners; grid = means + dense grid/cnt + devox + descriptor.  The
+ * workspace carries the prep results to the grid launch. */
+pcr_status pcr_extractor_voxel_prep(const float *xyz, int b, int n, int r, float *norm_coords,
+                                    int *ind, int *dinds, float *dwgts, void *workspace,
+                                    size_t workspace_bytes, void *stream);
+pcr_status pcr_extractor_voxel_grid(const float *features, int b, int c, int n, int r, int *cnt,
+                                    float *grid, float *devox, const int *dinds,
+                                    const float *dwgts, float *desc, void *workspace,
+                                    size_t workspace_bytes, void *stream);
+
+/* ------------------------------------------------------ self tests ------
+ * Device evaluation of the shared bit-exact math (include/pcr_math.h) for
+ * host-vs-device parity tests.  op: 0 acosf, 1 atanf, 2 sqrtf, 3 x/y,
+ * 4 spherical index (x: [3,n] coords, y unused, out_i: index with r=aux). */
+pcr_status pcr_selftest_math(int op, const float *x, const float *y, int n, int aux, float *out_f,
+                             int *out_i, void *stream);
+pcr_status pcr_selftest_math_d(int op, const double *x, const double *y, int n, double *out,
+                               void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PCR_AMD_H */

@@ -1,0 +1,355 @@
+/*
+ * pcr_math.h -- bit-exact scalar math shared by the HIP kernels (device) and
+ * the CPU oracle (host C).  Every function here is a fixed sequence of IEEE-754
+ * operations that are correctly rounded on both x86-64 and gfx950 (add, mul,
+ * div, sqrt, fma, floor, conversions), so host and device produce identical
+ * bits for identical inputs.  Both sides MUST be compiled with
+ * -ffp-contract=off: every fused multiply-add the reference's nvcc build is
+ * assumed to contract is written out explicitly with fmaf()/fma().
+ *
+ * Why a private acos/atan: the reference calls CUDA's float acos/atan
+ * (spherical_vox.cu:46,54; spherical_trilinear_devox.cu:58,62) and double acos
+ * (ppf.cu:62-64).  glibc, OCML and CUDA libm disagree in the last ulp, and one
+ * ulp on a spherical angle can move a point across a voxel-bin edge.  We use a
+ * double-precision polynomial (max rel. error ~1e-17, fitted with mpmath; see
+ * oracle/fit_math.py) rounded once to float, i.e. a correctly rounded acosf /
+ * atanf except in ~1e-9 of double-rounding cases.  Against genuine sm_61
+ * output the voxel index can differ only for points whose pre-floor bin value
+ * sits within a few ulp of an integer (flagged by the oracle).
+ *
+ * The FMA-contraction convention ("nvcc-FMA") follows LLVM's DAG combine for
+ * (a*b + c*d) + e*f:  fma(e, f, fma(a, b, c*d)).
+ */
+#ifndef PCR_MATH_H
+#define PCR_MATH_H
+
+#if defined(__HIP__)
+#define PCR_HD static inline __host__ __device__
+#else
+#define PCR_HD static inline
+#endif
+
+/* acos(-1.0) in double: the reference's `#define PI acos(-1.0)`
+ * (spherical_vox.cu:5, spherical_trilinear_devox.cu:5). */
+#define PCR_PI 3.141592653589793115997963468544185161590576171875
+#define PCR_PIO2 1.5707963267948965579989817342720925807952880859375
+#define PCR_PIO4 0.78539816339744827899949086713604629039764404296875
+#define PCR_TAN_PI8 0.41421356237309503
+
+/* KNN "undefined" sentinel, knn.cuh:3 (UNDEFINE_VALUE 10000). */
+#define PCR_KNN_UNDEF 10000.0f
+
+/* ---- conversions with CUDA/AMD hardware semantics (cvt.rzi / v_cvt_i32):
+ * truncate toward zero, saturate, NaN -> 0.  Plain C (int) of NaN is UB. ---- */
+PCR_HD int pcr_f2i(float v) {
+  if (v != v) return 0;
+  if (v >= 2147483648.0f) return 2147483647;
+  if (v <= -2147483648.0f) return (-2147483647 - 1);
+  return (int)v;
+}
+PCR_HD int pcr_d2i(double v) {
+  if (v != v) return 0;
+  if (v >= 2147483648.0) return 2147483647;
+  if (v <= -2147483649.0) return (-2147483647 - 1);
+  return (int)v;
+}
+
+/* NaN-ignoring min/max with CUDA fmin/fmax semantics (used by ppf.cu:38,62). */
+PCR_HD double pcr_fmax_d(double a, double b) {
+  if (a != a) return b;
+  if (b != b) return a;
+  return a > b ? a : b;
+}
+PCR_HD double pcr_fmin_d(double a, double b) {
+  if (a != a) return b;
+  if (b != b) return a;
+  return a < b ? a : b;
+}
+
+/* ---- contracted sums of products (nvcc-FMA convention) ---- */
+/* x*x + y*y + z*z  -> fma(z, z, fma(x, x, y*y)) */
+PCR_HD float pcr_sumsq3f(float x, float y, float z) {
+  return __builtin_fmaf(z, z, __builtin_fmaf(x, x, y * y));
+}
+/* uncontracted variant, only used by the oracle to flag FMA-sensitive elements */
+PCR_HD float pcr_sumsq3f_nofma(float x, float y, float z) {
+  float a = x * x;
+  float b = y * y;
+  float c = z * z;
+  float s = a + b;
+  return s + c;
+}
+/* a0*b0 + a1*b1 + a2*b2 */
+PCR_HD float pcr_dot3f(float a0, float a1, float a2, float b0, float b1, float b2) {
+  return __builtin_fmaf(a2, b2, __builtin_fmaf(a0, b0, a1 * b1));
+}
+/* w0*f0 + w1*f1 + ... + w7*f7 (trilinear_devox.cu:73-77 as nvcc contracts it) */
+PCR_HD float pcr_wsum8(const float w[8], const float f[8]) {
+  float acc = w[1] * f[1];
+  acc = __builtin_fmaf(w[0], f[0], acc);
+  acc = __builtin_fmaf(w[2], f[2], acc);
+  acc = __builtin_fmaf(w[3], f[3], acc);
+  acc = __builtin_fmaf(w[4], f[4], acc);
+  acc = __builtin_fmaf(w[5], f[5], acc);
+  acc = __builtin_fmaf(w[6], f[6], acc);
+  acc = __builtin_fmaf(w[7], f[7], acc);
+  return acc;
+}
+
+/* ---- double-precision asin/acos/atan kernels (Horner, explicit fma) ---- */
+/* asin(s) = s + s*z*P(z), z = s*s, |s| <= 0.5; P fitted on z in [0, 0.25] */
+PCR_HD double pcr_asin_core(double s) {
+  double z = s * s;
+  double p = 0.03207412686712179;
+  p = __builtin_fma(p, z, -0.029288652492291928);
+  p = __builtin_fma(p, z, 0.026492027340877928);
+  p = __builtin_fma(p, z, -0.0027168811083041495);
+  p = __builtin_fma(p, z, 0.00874110307727393);
+  p = __builtin_fma(p, z, 0.006869444870499221);
+  p = __builtin_fma(p, z, 0.008452406065746546);
+  p = __builtin_fma(p, z, 0.009755275316163535);
+  p = __builtin_fma(p, z, 0.011552268573915126);
+  p = __builtin_fma(p, z, 0.013964819214172544);
+  p = __builtin_fma(p, z, 0.017352765309284954);
+  p = __builtin_fma(p, z, 0.022372159069960183);
+  p = __builtin_fma(p, z, 0.03038194444474315);
+  p = __builtin_fma(p, z, 0.04464285714285491);
+  p = __builtin_fma(p, z, 0.07500000000000001);
+  p = __builtin_fma(p, z, 0.16666666666666666);
+  return __builtin_fma(s * z, p, s);
+}
+
+/* atan(t) = t + t*z*Q(z), z = t*t, |t| <= tan(pi/8) */
+PCR_HD double pcr_atan_core(double t) {
+  double z = t * t;
+  double q = -0.01391822929102443;
+  q = __builtin_fma(q, z, 0.030635704112969498);
+  q = __builtin_fma(q, z, -0.04104436265755082);
+  q = __builtin_fma(q, z, 0.04719395030027433);
+  q = __builtin_fma(q, z, -0.05258041554297779);
+  q = __builtin_fma(q, z, 0.058819252531928636);
+  q = __builtin_fma(q, z, -0.06666642020055166);
+  q = __builtin_fma(q, z, 0.07692306736000173);
+  q = __builtin_fma(q, z, -0.0909090906700999);
+  q = __builtin_fma(q, z, 0.11111111110754729);
+  q = __builtin_fma(q, z, -0.14285714285711518);
+  q = __builtin_fma(q, z, 0.19999999999999993);
+  q = __builtin_fma(q, z, -0.3333333333333333);
+  return __builtin_fma(t * z, q, t);
+}
+
+PCR_HD double pcr_acos_d(double x) {
+  double ax = __builtin_fabs(x);
+  if (ax <= 0.5) return PCR_PIO2 - pcr_asin_core(x);
+  if (x > 0.0) {
+    double s = __builtin_sqrt((1.0 - x) * 0.5);
+    return 2.0 * pcr_asin_core(s);
+  }
+  {
+    double s = __builtin_sqrt((1.0 + x) * 0.5); /* also the NaN path */
+    return PCR_PI - 2.0 * pcr_asin_core(s);
+  }
+}
+
+PCR_HD double pcr_atan_d(double x) {
+  double a = __builtin_fabs(x);
+  int inv = 0;
+  double base = 0.0, t, r;
+  if (a > 1.0) {
+    a = 1.0 / a;
+    inv = 1;
+  }
+  if (a > PCR_TAN_PI8) {
+    t = (a - 1.0) / (a + 1.0);
+    base = PCR_PIO4;
+  } else {
+    t = a;
+  }
+  r = base + pcr_atan_core(t);
+  if (inv) r = PCR_PIO2 - r;
+  return (x < 0.0) ? -r : r;
+}
+
+/* float acos/atan of the reference (CUDA float overloads), rounded once */
+PCR_HD float pcr_acosf(float x) { return (float)pcr_acos_d((double)x); }
+PCR_HD float pcr_atanf(float x) { return (float)pcr_atan_d((double)x); }
+
+/* ---- spherical coordinates of a normalised point (spherical_vox.cu:34-56,
+ * spherical_trilinear_devox.cu:48-65).  Returns 0 when the reference drops
+ * the point (gama==0, gama>=1, |z/gama|>1, beta>=PI), else 1. ---- */
+PCR_HD int pcr_sph_coords(float x, float y, float z, int r, int use_fma,
+                          float *gama_o, float *alpha_o, float *beta_o) {
+  float g2 = use_fma ? pcr_sumsq3f(x, y, z) : pcr_sumsq3f_nofma(x, y, z);
+  float gama = __builtin_sqrtf(g2);
+  float beta, alpha;
+  if ((gama == 0.0f) || (gama >= 1.0f) || ((z / gama) > 1.0f) || ((z / gama) < -1.0f))
+    return 0;
+  beta = pcr_acosf(z / gama);
+  if ((double)beta >= PCR_PI) return 0;
+  if (x == 0.0f && y != 0.0f)
+    alpha = (float)((double)(y / __builtin_fabsf(y)) * PCR_PI * 0.5);
+  else if (x == 0.0f && y == 0.0f)
+    alpha = 0.0f;
+  else
+    alpha = (float)((double)pcr_atanf(y / x) +
+                    PCR_PI * (double)(1.0f - (x / __builtin_fabsf(x))) / 2.0);
+  alpha = (float)((double)alpha + PCR_PI / (double)r);
+  if (alpha < 0.0f) alpha = (float)((double)alpha + 2.0 * PCR_PI);
+  *gama_o = gama;
+  *alpha_o = alpha;
+  *beta_o = beta;
+  return 1;
+}
+
+/* voxel index of a normalised point, -1 when dropped (spherical_vox.cu:59-65) */
+PCR_HD int pcr_sph_index_v(float x, float y, float z, int r, int use_fma) {
+  float gama, alpha, beta;
+  int gx, gy, gz;
+  if (!pcr_sph_coords(x, y, z, r, use_fma, &gama, &alpha, &beta)) return -1;
+  gx = pcr_f2i(__builtin_floorf(gama * (float)r));
+  gy = pcr_d2i(__builtin_floor((double)((alpha * (float)r) / 2.0f) / PCR_PI));
+  gz = pcr_d2i(__builtin_floor((double)(beta * (float)r) / PCR_PI));
+  if (gx >= r) gx = r - 1;
+  if (gy >= r) gy = r - 1;
+  if (gz >= r) gz = r - 1;
+  return gx * r * r + gy * r + gz;
+}
+PCR_HD int pcr_sph_index(float x, float y, float z, int r) {
+  return pcr_sph_index_v(x, y, z, r, 1);
+}
+
+/* ---- spherical "trilinear" corners (spherical_trilinear_devox.cu:67-105),
+ * quirks preserved: integer division gama_lo = (pos/r2)/r == 0, radian-valued
+ * alpha/beta fractions, (int) of radian values.  Returns 0 when the point is
+ * dropped by the recomputed coordinates (the reference then writes nothing). */
+PCR_HD int pcr_sph_corners(float x, float y, float z, int pos, int r, int idx[8], float w[8]) {
+  float gama, alpha, beta;
+  int r2 = r * r;
+  int gg, ga, gb, glo, alo, blo, ghi, ahi, bhi;
+  float glo_f, alo_f, blo_f, gd1, ad1, bd1, gd0, ad0, bd0;
+  if (!pcr_sph_coords(x, y, z, r, 1, &gama, &alpha, &beta)) return 0;
+  gg = pos / r2;
+  ga = (pos - gg * r2) / r;
+  gb = pos - gg * r2 - ga * r;
+  glo_f = (float)(gg / r);
+  alo_f = (float)(PCR_PI * 2.0 * (double)ga / (double)r);
+  blo_f = (float)(PCR_PI * (double)gb / (double)r);
+  gd1 = gama - glo_f;
+  ad1 = alpha - alo_f;
+  bd1 = beta - blo_f;
+  gd0 = 1.0f - gd1;
+  ad0 = 1.0f - ad1;
+  bd0 = 1.0f - bd1;
+  w[0] = gd0 * ad0 * bd0;
+  w[1] = gd0 * ad0 * bd1;
+  w[2] = gd0 * ad1 * bd0;
+  w[3] = gd0 * ad1 * bd1;
+  w[4] = gd1 * ad0 * bd0;
+  w[5] = gd1 * ad0 * bd1;
+  w[6] = gd1 * ad1 * bd0;
+  w[7] = gd1 * ad1 * bd1;
+  glo = pcr_f2i(glo_f);
+  alo = pcr_f2i(alo_f);
+  blo = pcr_f2i(blo_f);
+  ghi = (gd1 > 0.0f) ? -1 : 0;
+  ahi = (ad1 > 0.0f) ? -1 : 0;
+  bhi = (bd1 > 0.0f) ? 1 : 0;
+  idx[0] = glo * r2 + alo * r + blo;
+  idx[1] = idx[0] + bhi;
+  idx[2] = idx[0] + (ahi & r);
+  idx[3] = idx[2] + bhi;
+  idx[4] = idx[0] + (ghi & r2);
+  idx[5] = idx[4] + bhi;
+  idx[6] = idx[4] + (ahi & r);
+  idx[7] = idx[6] + bhi;
+  return 1;
+}
+
+/* ---- cube trilinear corners (trilinear_devox.cu:45-80) on continuous
+ * voxel coordinates already clamped to [0, r-1] ---- */
+PCR_HD void pcr_cube_corners(float x, float y, float z, int r, int idx[8], float w[8]) {
+  int r2 = r * r;
+  float xl = __builtin_floorf(x), yl = __builtin_floorf(y), zl = __builtin_floorf(z);
+  float xd1 = x - xl, yd1 = y - yl, zd1 = z - zl;
+  float xd0 = 1.0f - xd1, yd0 = 1.0f - yd1, zd0 = 1.0f - zd1;
+  int xlo = pcr_f2i(xl), ylo = pcr_f2i(yl), zlo = pcr_f2i(zl);
+  int xhi = (xd1 > 0.0f) ? -1 : 0;
+  int yhi = (yd1 > 0.0f) ? -1 : 0;
+  int zhi = (zd1 > 0.0f) ? 1 : 0;
+  w[0] = xd0 * yd0 * zd0;
+  w[1] = xd0 * yd0 * zd1;
+  w[2] = xd0 * yd1 * zd0;
+  w[3] = xd0 * yd1 * zd1;
+  w[4] = xd1 * yd0 * zd0;
+  w[5] = xd1 * yd0 * zd1;
+  w[6] = xd1 * yd1 * zd0;
+  w[7] = xd1 * yd1 * zd1;
+  idx[0] = xlo * r2 + ylo * r + zlo;
+  idx[1] = idx[0] + zhi;
+  idx[2] = idx[0] + (yhi & r);
+  idx[3] = idx[2] + zhi;
+  idx[4] = idx[0] + (xhi & r2);
+  idx[5] = idx[4] + zhi;
+  idx[6] = idx[4] + (yhi & r);
+  idx[7] = idx[6] + zhi;
+}
+
+/* 1.0 / (float)cnt narrowed to float (spherical_vox.cu:112, vox.cu:67) */
+PCR_HD float pcr_inv_count(int cnt) { return (float)(1.0 / (double)(float)cnt); }
+
+/* ---- point-pair feature of one (point, centre) pair (ppf.cu:37-90).
+ * out = {a1, a2, a3, d_norm}; all zero when either normal is ~0. ---- */
+PCR_HD void pcr_global_ppf(float x, float y, float z, float cx, float cy, float cz,
+                           float nx, float ny, float nz, float cnx, float cny,
+                           float cnz, float out[4]) {
+  float dx = cx - x, dy = cy - y, dz = cz - z;
+  float s = __builtin_sqrtf(pcr_sumsq3f(dx, dy, dz));
+  float dn = (float)pcr_fmax_d((double)s, 1e-20);
+  float n1, n2;
+  dx /= dn;
+  dy /= dn;
+  dz /= dn;
+  n1 = __builtin_sqrtf(pcr_sumsq3f(cnx, cny, cnz));
+  n2 = __builtin_sqrtf(pcr_sumsq3f(nx, ny, nz));
+  if ((double)n2 <= 1e-10 || (double)n1 <= 1e-10) {
+    out[0] = out[1] = out[2] = out[3] = 0.0f;
+    return;
+  }
+  cnx /= n1;
+  cny /= n1;
+  cnz /= n1;
+  nx /= n2;
+  ny /= n2;
+  nz /= n2;
+  out[0] = (float)pcr_acos_d(pcr_fmax_d(pcr_fmin_d((double)pcr_dot3f(dx, dy, dz, cnx, cny, cnz), 1.0), -1.0));
+  out[1] = (float)pcr_acos_d(pcr_fmax_d(pcr_fmin_d((double)pcr_dot3f(dx, dy, dz, nx, ny, nz), 1.0), -1.0));
+  out[2] = (float)pcr_acos_d(pcr_fmax_d(pcr_fmin_d((double)pcr_dot3f(cnx, cny, cnz, nx, ny, nz), 1.0), -1.0));
+  out[3] = dn;
+}
+
+/* torch.clamp(v, -1, 1) on float: NaN propagates */
+PCR_HD float pcr_clamp1f(float v) {
+  if (v != v) return v;
+  return v < -1.0f ? -1.0f : (v > 1.0f ? 1.0f : v);
+}
+
+/* ---- local (k-neighbour) PPF of the model (pvcnn_classify.py:261-269).
+ * g = grouped neighbour minus centre as BallQuery returns it
+ * (modules/ball_query.py:24); d = c - g (the model's 2c - p quirk when
+ * relative != 0), else d = c - p.  out = {nr_d, ni_d, nr_ni, |d|}. ---- */
+PCR_HD void pcr_local_ppf(float cx, float cy, float cz, float cnx, float cny, float cnz,
+                          float px, float py, float pz, float pnx, float pny, float pnz,
+                          int relative, float out[4]) {
+  float gx = relative ? px - cx : px;
+  float gy = relative ? py - cy : py;
+  float gz = relative ? pz - cz : pz;
+  float dx = cx - gx, dy = cy - gy, dz = cz - gz;
+  float dn = __builtin_sqrtf(pcr_sumsq3f(dx, dy, dz));
+  float ux = dx / dn, uy = dy / dn, uz = dz / dn;
+  out[0] = pcr_acosf(pcr_clamp1f(pcr_dot3f(pnx, pny, pnz, ux, uy, uz)));
+  out[1] = pcr_acosf(pcr_clamp1f(pcr_dot3f(cnx, cny, cnz, ux, uy, uz)));
+  out[2] = pcr_acosf(pcr_clamp1f(pcr_dot3f(pnx, pny, pnz, cnx, cny, cnz)));
+  out[3] = dn;
+}
+
+#endif /* PCR_MATH_H */

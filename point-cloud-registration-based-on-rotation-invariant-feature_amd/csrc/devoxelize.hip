@@ -1,0 +1,257 @@
+// devoxelize.hip -- spherical / cube trilinear devoxelization (forward and
+// backward) and the PVConv dgcnn centre gather, for gfx950.
+//
+// Replaces (relative to the reference's PVCNN/modules/functional/src):
+//   interpolate/spherical_trilinear_devox.cu:23-136, :150-194
+//   interpolate/trilinear_devox.cu:22-106, :120-163
+// and the torch gather block of PVCNN/modules/pvconv.py:68-89.
+//
+// Forward: one thread per point, channel groups across workgroups so the
+// grid has >> 256 workgroups.  Corner indices/weights come from the shared
+// bit-exact helpers (pcr_sph_corners / pcr_cube_corners).  The spherical
+// quirk (integer-division gama_lo, radian fractions) confines every corner to
+// cells [0, r^2 + 8r + 5): those gathers are L2 hits.
+//
+// Backward: the reference memsets a dense [B, C, r^3] grad and scatters 8*C
+// float atomics per point onto <= 80 hot cells -- the worst contention case of
+// global atomics.  Here one workgroup owns a (cloud, channel-group) slab: it
+// accumulates the hot window [0, hw) in LDS, streams zeros over the rest of
+// its slab with 16-byte stores, then (after its own stores are complete)
+// adds the rare out-of-window corners with global atomics and finally stores
+// the window.  The dense gradient is written exactly once.
+#include "common.hpp"
+
+namespace pcr {
+
+template <bool SPH>
+__global__ __launch_bounds__(256) void devox_fwd_kernel(const float* __restrict__ coords,
+                                                        const float* __restrict__ feat,
+                                                        const int* __restrict__ g_inds, int c,
+                                                        int n, int r, int cg,
+                                                        float* __restrict__ outs,
+                                                        int* __restrict__ inds,
+                                                        float* __restrict__ wgts) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int j0 = blockIdx.y * cg;
+  const int b = blockIdx.z;
+  if (i >= n) return;
+  const int r3 = r * r * r;
+  const float* x = coords + (size_t)b * 3 * n;
+  int idx[8];
+  float w[8];
+  bool write_out = true;  // false -> outs stay 0 (reference: `continue`)
+  bool ok;
+  if (SPH) {
+    const int pos = g_inds[(size_t)b * n + i];
+    if (pos == -1) {
+      ok = false;
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        idx[q] = q == 0 ? -1 : 0;
+        w[q] = 0.0f;
+      }
+    } else {
+      ok = pcr_sph_corners(x[i], x[i + n], x[i + 2 * n], pos, r, idx, w) != 0;
+      if (!ok) {
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+          idx[q] = 0;
+          w[q] = 0.0f;
+        }
+      }
+    }
+    write_out = ok;
+  } else {
+    pcr_cube_corners(x[i], x[i + n], x[i + 2 * n], r, idx, w);
+    ok = true;
+  }
+  if (blockIdx.y == 0) {
+    int* I = inds + (size_t)b * 8 * n;
+    float* Wt = wgts + (size_t)b * 8 * n;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      I[i + (size_t)q * n] = idx[q];
+      Wt[i + (size_t)q * n] = w[q];
+    }
+  }
+  bool inb[8];
+#pragma unroll
+  for (int q = 0; q < 8; q++) inb[q] = idx[q] >= 0 && idx[q] < r3;
+  const int j1 = min(c, j0 + cg);
+  for (int j = j0; j < j1; j++) {
+    const float* f = feat + ((size_t)b * c + j) * r3;
+    float v = 0.0f;
+    if (write_out) {
+      float fv[8];
+#pragma unroll
+      for (int q = 0; q < 8; q++) fv[q] = inb[q] ? f[idx[q]] : 0.0f;
+      v = pcr_wsum8(w, fv);
+    }
+    outs[((size_t)b * c + j) * n + i] = v;
+  }
+}
+
+// Backward with the dense grad written once (see header comment).
+constexpr int kBwdThreads = 256;
+constexpr int kBwdMaxG = 4;
+
+__global__ __launch_bounds__(kBwdThreads) void devox_bwd_kernel(
+    const float* __restrict__ grad_y, const int* __restrict__ inds, const float* __restrict__ wgts,
+    int c, int n, int r3, int G, int hw, int skip_neg, float* __restrict__ grad_x) {
+  extern __shared__ __align__(16) float acc_s[];  // [G][hw]
+  const int grp = blockIdx.x;
+  const int b = blockIdx.y;
+  const int tid = threadIdx.x;
+  const int c0 = grp * G;
+  const int gcount = min(G, c - c0);
+  for (int t = tid; t < G * hw; t += kBwdThreads) acc_s[t] = 0.0f;
+  __syncthreads();
+  const int* I = inds + (size_t)b * 8 * n;
+  const float* Wt = wgts + (size_t)b * 8 * n;
+  const float* gy = grad_y + ((size_t)b * c + c0) * n;
+  float* gx = grad_x + ((size_t)b * c + c0) * r3;
+  // 1. accumulate the hot window in LDS; note whether any corner falls outside
+  int outside = 0;
+  for (int i = tid; i < n; i += kBwdThreads) {
+    if (skip_neg && I[i] == -1) continue;
+    int ci[8];
+    float cw[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      ci[q] = I[i + (size_t)q * n];
+      cw[q] = Wt[i + (size_t)q * n];
+      outside |= (ci[q] >= hw && ci[q] < r3);
+    }
+    for (int g = 0; g < gcount; g++) {
+      const float gv = gy[(size_t)g * n + i];
+#pragma unroll
+      for (int q = 0; q < 8; q++)
+        if (ci[q] >= 0 && ci[q] < hw) atomicAdd(&acc_s[g * hw + ci[q]], cw[q] * gv);
+    }
+  }
+  const int any_outside = __syncthreads_or(outside);
+  // 2. zero-stream the slab outside the window (written exactly once)
+  for (int g = 0; g < gcount; g++) {
+    float* row = gx + (size_t)g * r3;
+    int start = hw;
+    while (start < r3 && (start & 3)) {
+      if (tid == 0) row[start] = 0.0f;
+      start++;
+    }
+    const int nv = (r3 - start) >> 2;
+    float4* v4 = (float4*)(row + start);
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int t = tid; t < nv; t += kBwdThreads) v4[t] = z;
+    for (int t = start + nv * 4 + tid; t < r3; t += kBwdThreads) row[t] = 0.0f;
+  }
+  // 3. rare out-of-window corners (cube grids): global atomics after this
+  //    workgroup's own zero stores are released to the device
+  if (any_outside) {
+    __threadfence();
+    __syncthreads();
+    for (int i = tid; i < n; i += kBwdThreads) {
+      if (skip_neg && I[i] == -1) continue;
+      for (int q = 0; q < 8; q++) {
+        const int v = I[i + (size_t)q * n];
+        if (v < hw || v >= r3) continue;
+        const float w = Wt[i + (size_t)q * n];
+        for (int g = 0; g < gcount; g++) atomicAdd(gx + (size_t)g * r3 + v, w * gy[(size_t)g * n + i]);
+      }
+    }
+  }
+  __syncthreads();
+  // 3. store the window
+  for (int g = 0; g < gcount; g++)
+    for (int t = tid; t < hw; t += kBwdThreads) gx[(size_t)g * r3 + t] = acc_s[g * hw + t];
+}
+
+__global__ __launch_bounds__(256) void center_gather_kernel(const float* __restrict__ features,
+                                                            const float* __restrict__ grid,
+                                                            const int* __restrict__ ind, int c,
+                                                            int n, int r3, int cg,
+                                                            float* __restrict__ related) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int j0 = blockIdx.y * cg;
+  const int b = blockIdx.z;
+  if (i >= n) return;
+  const int pos = ind[(size_t)b * n + i];
+  const bool ok = pos >= 0 && pos < r3;
+  const int j1 = min(c, j0 + cg);
+  for (int j = j0; j < j1; j++) {
+    const size_t o = ((size_t)b * c + j) * n + i;
+    related[o] = ok ? features[o] - grid[((size_t)b * c + j) * r3 + pos] : 0.0f;
+  }
+}
+
+}  // namespace pcr
+
+using namespace pcr;
+
+static pcr_status devox_forward(bool sph, int r, const float* coords, const float* features,
+                                const int* g_inds, int b, int c, int n, float* outs, int* inds,
+                                float* wgts, void* stream, const char* name) {
+  PCR_REQUIRE(b >= 0 && c >= 0 && n >= 0 && r >= 1, "%s: invalid sizes", name);
+  PCR_REQUIRE((int64_t)r * r * r < (1ll << 31) / 64, "%s: resolution too large", name);
+  if (b == 0 || n == 0) return PCR_OK;
+  const int cg = 8;
+  dim3 grid(ceil_div(n, 256), c > 0 ? ceil_div(c, cg) : 1, b);
+  if (sph)
+    hipLaunchKernelGGL(devox_fwd_kernel<true>, grid, dim3(256), 0, as_stream(stream), coords,
+                       features, g_inds, c, n, r, cg, outs, inds, wgts);
+  else
+    hipLaunchKernelGGL(devox_fwd_kernel<false>, grid, dim3(256), 0, as_stream(stream), coords,
+                       features, g_inds, c, n, r, cg, outs, inds, wgts);
+  return launch_status(name);
+}
+
+extern "C" pcr_status pcr_spherical_trilinear_devoxelize_forward(int r, int is_training,
+                                                                 const float* coords,
+                                                                 const float* features,
+                                                                 const int* g_inds, int b, int c,
+                                                                 int n, float* outs, int* inds,
+                                                                 float* wgts, void* stream) {
+  (void)is_training;
+  return devox_forward(true, r, coords, features, g_inds, b, c, n, outs, inds, wgts, stream,
+                       "spherical_trilinear_devoxelize_forward");
+}
+
+extern "C" pcr_status pcr_trilinear_devoxelize_forward(int r, int is_training, const float* coords,
+                                                       const float* features, int b, int c, int n,
+                                                       float* outs, int* inds, float* wgts,
+                                                       void* stream) {
+  (void)is_training;
+  return devox_forward(false, r, coords, features, nullptr, b, c, n, outs, inds, wgts, stream,
+                       "trilinear_devoxelize_forward");
+}
+
+extern "C" pcr_status pcr_devoxelize_backward(const float* grad_y, const int* inds,
+                                              const float* wgts, int b, int c, int n, int r,
+                                              int skip_neg, float* grad_x, void* stream) {
+  PCR_REQUIRE(b >= 0 && c >= 0 && n >= 0 && r >= 1, "devoxelize_backward: invalid sizes");
+  const int64_t r3l = (int64_t)r * r * r;
+  PCR_REQUIRE(r3l < (1ll << 31) / 64, "devoxelize_backward: resolution too large");
+  if (b == 0 || c == 0) return PCR_OK;
+  const int r3 = (int)r3l;
+  // hot window: every spherical corner lies below r^2 + 8r + 5
+  int hw = skip_neg ? r * r + 8 * r + 8 : 2048;
+  if (hw > r3) hw = r3;
+  int G = kBwdMaxG;
+  while (G > 1 && (size_t)G * hw * 4 > 80 * 1024) G >>= 1;
+  if ((size_t)G * hw * 4 > 80 * 1024) hw = 80 * 1024 / 4;
+  if (hw > r3) hw = r3;
+  hipLaunchKernelGGL(devox_bwd_kernel, dim3(ceil_div(c, G), b), dim3(kBwdThreads),
+                     (size_t)G * hw * 4, as_stream(stream), grad_y, inds, wgts, c, n, r3, G, hw,
+                     skip_neg, grad_x);
+  return launch_status("devoxelize_backward");
+}
+
+extern "C" pcr_status pcr_dgcnn_center_gather(const float* features, const float* avg_grid,
+                                              const int* ind, int b, int c, int n, int r3,
+                                              float* related, void* stream) {
+  PCR_REQUIRE(b >= 0 && c >= 0 && n >= 0 && r3 >= 1, "dgcnn_center_gather: invalid sizes");
+  if (b == 0 || c == 0 || n == 0) return PCR_OK;
+  const int cg = 8;
+  hipLaunchKernelGGL(center_gather_kernel, dim3(ceil_div(n, 256), ceil_div(c, cg), b), dim3(256),
+                     0, as_stream(stream), features, avg_grid, ind, c, n, r3, cg, related);
+  return launch_status("dgcnn_center_gather");
+}

@@ -1,0 +1,517 @@
+// neighbors.hip -- neighbour search (KNN, ball query), grouping, point-pair
+// features (global and local) and the math self-test hooks, for gfx950.
+//
+// Replaces (relative to the reference's PVCNN/modules/functional/src):
+//   knn/knn.cu:5-98               KnnKernel / KnnGradKernel
+//   spherical_ppf/ppf.cu:19-99    spherical_ppf_kernel
+//   ball_query/ball_query.cu:19-59
+//   grouping/grouping.cu:18-85
+// and the PyTorch local-PPF block of PVCNN/models/pvcnn_classify.py:252-269.
+//
+// KNN: the reference keeps each query's top-k in GLOBAL memory and runs an
+// O(k) bubble pass per candidate with one workgroup per cloud.  Here each
+// thread owns one query and keeps its top-k in registers (a compile-time
+// sized, statically indexed sorted array, branch-free insertion), the
+// candidate cloud is staged through LDS in coalesced tiles shared by the
+// 256 queries of the workgroup, and the grid spans (query blocks x clouds).
+// Candidates are scanned in ascending index with a strict `<` test, which is
+// exactly the reference's tie rule (lower index first); slots that never fill
+// keep (10000, 0) as the reference's ones*10000 / zeros init.
+#include "common.hpp"
+
+namespace pcr {
+
+constexpr int kKnnThreads = 256;
+constexpr int kKnnTile = 1024;
+constexpr int kMaxC = 8;
+
+// Sorted ascending; valid region is the LAST k slots, the first KMAX-k slots
+// hold -inf and are never displaced.  Insert (d, j) if d < D[KMAX-1].
+template <int KMAX>
+struct TopK {
+  float d[KMAX];
+  int j[KMAX];
+  __device__ void init(int k) {
+#pragma unroll
+    for (int q = 0; q < KMAX; q++) {
+      d[q] = (q < KMAX - k) ? -__builtin_inff() : PCR_KNN_UNDEF;
+      j[q] = 0;
+    }
+  }
+  __device__ float thr() const { return d[KMAX - 1]; }
+  // Insertion as a compare-exchange carry chain: the carried element moves
+  // past every slot it is not strictly smaller than, so equal distances keep
+  // the earlier (lower) index first.  Each lane mask dies immediately (no
+  // SGPR pressure), and a non-qualifying x (>= D[KMAX-1], or NaN) falls off.
+  __device__ void insert(float x, int jx) {
+#pragma unroll
+    for (int q = 0; q < KMAX; q++) {
+      const bool lt = x < d[q];
+      const float nd = lt ? x : d[q];
+      const int nj = lt ? jx : j[q];
+      x = lt ? d[q] : x;
+      jx = lt ? j[q] : jx;
+      d[q] = nd;
+      j[q] = nj;
+    }
+  }
+};
+
+// Distance with the reference's contraction: d = t0*t0, d = fma(tp, tp, d)
+// (knn.cu:20-24 under nvcc --fmad=true).
+template <int KMAX, bool PPF, int CC>
+__global__ __launch_bounds__(kKnnThreads) void knn_kernel(
+    const float* __restrict__ xyz1, const float* __restrict__ xyz2, int c, int n, int m, int k,
+    float* __restrict__ dist, int* __restrict__ idx,
+    // fused local PPF (self KNN): normals of xyz1 (== xyz2), output [b,4,k,n]
+    const float* __restrict__ normals, int relative, float* __restrict__ ppf) {
+  __shared__ float tile_s[kMaxC * kKnnTile];
+  const int b = blockIdx.y;
+  const int i = blockIdx.x * kKnnThreads + threadIdx.x;
+  const bool active = i < n;
+  const float* x1 = xyz1 + (size_t)b * c * n;
+  const float* x2 = xyz2 + (size_t)b * c * m;
+  // CC == 3: the xyz specialisation; CC == kMaxC: generic c <= kMaxC
+  float q[CC];
+#pragma unroll
+  for (int p = 0; p < CC; p++) q[p] = (p < c && active) ? x1[i + (size_t)p * n] : 0.0f;
+  TopK<KMAX> top;
+  top.init(k);
+  for (int t0 = 0; t0 < m; t0 += kKnnTile) {
+    const int tl = min(kKnnTile, m - t0);
+    __syncthreads();
+    for (int p = 0; p < c; p++)
+      for (int t = threadIdx.x; t < tl; t += kKnnThreads)
+        tile_s[p * kKnnTile + t] = x2[(size_t)p * m + t0 + t];
+    __syncthreads();
+    if (active) {
+      if (CC == 3) {
+#pragma unroll 1
+        for (int t = 0; t < tl; t++) {
+          const float a = q[0] - tile_s[t];
+          const float bb = q[1] - tile_s[kKnnTile + t];
+          const float cc = q[2] - tile_s[2 * kKnnTile + t];
+          float d = a * a;
+          d = __builtin_fmaf(bb, bb, d);
+          d = __builtin_fmaf(cc, cc, d);
+          if (__any(d < top.thr())) top.insert(d, t0 + t);  // no-op for d >= thr
+        }
+      } else {
+#pragma unroll 1
+        for (int t = 0; t < tl; t++) {
+          float d = 0.0f;
+#pragma unroll
+          for (int p = 0; p < CC; p++) {
+            if (p < c) {
+              const float a = q[p] - tile_s[p * kKnnTile + t];
+              d = (p == 0) ? a * a : __builtin_fmaf(a, a, d);
+            }
+          }
+          if (__any(d < top.thr())) top.insert(d, t0 + t);  // no-op for d >= thr
+        }
+      }
+    }
+  }
+  if (!active) return;
+  const int base = KMAX - k;
+#pragma unroll
+  for (int s = 0; s < KMAX; s++) {
+    if (s >= base) {
+      const size_t o = ((size_t)b * k + (s - base)) * n + i;
+      if (dist) dist[o] = top.d[s];
+      if (idx) idx[o] = top.j[s];
+    }
+  }
+  if (PPF) {
+    // neighbour ids re-read from the rows this thread just wrote (idx is
+    // required for the fused variant) to keep the slot loop rolled
+    const float* nb = normals + (size_t)b * 3 * n;
+    const float cnx = nb[i], cny = nb[i + n], cnz = nb[i + 2 * n];
+#pragma unroll 1
+    for (int slot = 0; slot < k; slot++) {
+      const int jn = idx[((size_t)b * k + slot) * n + i];
+      float o[4];
+      pcr_local_ppf(q[0], q[1], q[2], cnx, cny, cnz, x2[jn], x2[jn + m], x2[jn + 2 * m], nb[jn],
+                    nb[jn + n], nb[jn + 2 * n], relative, o);
+#pragma unroll
+      for (int ch = 0; ch < 4; ch++) ppf[(((size_t)b * 4 + ch) * k + slot) * n + i] = o[ch];
+    }
+  }
+}
+
+// k > 128: the reference algorithm itself (top-k in the output buffers).
+__global__ __launch_bounds__(256) void knn_generic_kernel(const float* __restrict__ xyz1,
+                                                          const float* __restrict__ xyz2, int c,
+                                                          int n, int m, int k,
+                                                          float* __restrict__ dist,
+                                                          int* __restrict__ idx) {
+  const int b = blockIdx.y;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float* x1 = xyz1 + (size_t)b * c * n;
+  const float* x2 = xyz2 + (size_t)b * c * m;
+  float* D = dist + (size_t)b * k * n;
+  int* I = idx + (size_t)b * k * n;
+  for (int q = 0; q < k; q++) {
+    D[i + (size_t)q * n] = PCR_KNN_UNDEF;
+    I[i + (size_t)q * n] = 0;
+  }
+  for (int j = 0; j < m; j++) {
+    float d = 0.0f;
+    for (int p = 0; p < c; p++) {
+      const float a = x1[i + (size_t)p * n] - x2[j + (size_t)p * m];
+      d = (p == 0) ? a * a : __builtin_fmaf(a, a, d);
+    }
+    if (d < D[i + (size_t)(k - 1) * n]) {
+      int q = k - 1;
+      while (q > 0 && d < D[i + (size_t)(q - 1) * n]) {
+        D[i + (size_t)q * n] = D[i + (size_t)(q - 1) * n];
+        I[i + (size_t)q * n] = I[i + (size_t)(q - 1) * n];
+        q--;
+      }
+      D[i + (size_t)q * n] = d;
+      I[i + (size_t)q * n] = j;
+    }
+  }
+}
+
+// knn.cu:52-78: one direction, atomically accumulated into both grads.
+__global__ __launch_bounds__(256) void knn_grad_kernel(const float* __restrict__ x1,
+                                                       const float* __restrict__ x2, int c, int n,
+                                                       int m, int k, const float* __restrict__ gd,
+                                                       const int* __restrict__ id,
+                                                       float* __restrict__ g1,
+                                                       float* __restrict__ g2) {
+  const int b = blockIdx.y;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  x1 += (size_t)b * c * n;
+  x2 += (size_t)b * c * m;
+  gd += (size_t)b * k * n;
+  id += (size_t)b * k * n;
+  g1 += (size_t)b * c * n;
+  g2 += (size_t)b * c * m;
+  for (int q = 0; q < k; q++) {
+    const float g = gd[i + (size_t)q * n] * 2.0f;
+    if (g >= 20000.0f) continue;
+    const int j = id[i + (size_t)q * n];
+    if (j < 0 || j >= m) continue;
+    for (int p = 0; p < c; p++) {
+      const float t = g * (x1[i + (size_t)p * n] - x2[j + (size_t)p * m]);
+      atomicAdd(g1 + i + (size_t)p * n, t);
+      atomicAdd(g2 + j + (size_t)p * m, -t);
+    }
+  }
+}
+
+// ppf.cu:28-90
+__global__ __launch_bounds__(256) void global_ppf_kernel(const float* __restrict__ coords,
+                                                         const float* __restrict__ center,
+                                                         const float* __restrict__ normals,
+                                                         const float* __restrict__ cnormals, int n,
+                                                         float* __restrict__ feat) {
+  const int b = blockIdx.y;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const size_t o3 = (size_t)b * 3 * n, o4 = (size_t)b * 4 * n;
+  float out[4];
+  pcr_global_ppf(coords[o3 + i], coords[o3 + i + n], coords[o3 + i + 2 * n], center[o3 + i],
+                 center[o3 + i + n], center[o3 + i + 2 * n], normals[o3 + i],
+                 normals[o3 + i + n], normals[o3 + i + 2 * n], cnormals[o3 + i],
+                 cnormals[o3 + i + n], cnormals[o3 + i + 2 * n], out);
+#pragma unroll
+  for (int ch = 0; ch < 4; ch++) feat[o4 + i + (size_t)ch * n] = out[ch];
+}
+
+// pvcnn_classify.py:258-269 with explicit neighbour indices; out [b,4,u,m]
+__global__ __launch_bounds__(256) void local_ppf_kernel(
+    const float* __restrict__ pts, const float* __restrict__ nrm, const float* __restrict__ ctr,
+    const float* __restrict__ cnrm, const int* __restrict__ idx, int n, int m, int u, int kmajor,
+    int relative, float* __restrict__ out) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  const int q = blockIdx.y;
+  const int b = blockIdx.z;
+  if (j >= m) return;
+  const float* P = pts + (size_t)b * 3 * n;
+  const float* Nn = nrm + (size_t)b * 3 * n;
+  const float* C = ctr + (size_t)b * 3 * m;
+  const float* Cn = cnrm + (size_t)b * 3 * m;
+  const int* I = idx + (size_t)b * m * u;
+  int s = kmajor ? I[(size_t)q * m + j] : I[(size_t)j * u + q];
+  if (s < 0 || s >= n) s = 0;
+  float o[4];
+  pcr_local_ppf(C[j], C[j + m], C[j + 2 * m], Cn[j], Cn[j + m], Cn[j + 2 * m], P[s], P[s + n],
+                P[s + 2 * n], Nn[s], Nn[s + n], Nn[s + 2 * n], relative, o);
+#pragma unroll
+  for (int ch = 0; ch < 4; ch++) out[(((size_t)b * 4 + ch) * u + q) * m + j] = o[ch];
+}
+
+// ball_query.cu:30-49: points staged through LDS tiles; per-centre early exit
+constexpr int kBqTile = 1024;
+__global__ __launch_bounds__(256) void ball_query_kernel(const float* __restrict__ centers,
+                                                         const float* __restrict__ points, int m,
+                                                         int n, float r2, int u,
+                                                         int* __restrict__ idx) {
+  __shared__ float tile_s[3 * kBqTile];
+  const int b = blockIdx.y;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = j < m;
+  const float* C = centers + (size_t)b * 3 * m;
+  const float* P = points + (size_t)b * 3 * n;
+  int* I = idx + (size_t)b * m * u + (size_t)j * u;
+  float cx = 0.f, cy = 0.f, cz = 0.f;
+  if (active) {
+    cx = C[j];
+    cy = C[j + m];
+    cz = C[j + 2 * m];
+  }
+  int cnt = 0, first = 0;
+  bool done = !active;
+  for (int t0 = 0; t0 < n; t0 += kBqTile) {
+    if (!__syncthreads_or(!done)) break;
+    const int tl = min(kBqTile, n - t0);
+    for (int t = threadIdx.x; t < tl; t += blockDim.x) {
+      tile_s[t] = P[t0 + t];
+      tile_s[kBqTile + t] = P[n + t0 + t];
+      tile_s[2 * kBqTile + t] = P[2 * n + t0 + t];
+    }
+    __syncthreads();
+    if (!done) {
+      for (int t = 0; t < tl && cnt < u; t++) {
+        const float dx = cx - tile_s[t], dy = cy - tile_s[kBqTile + t],
+                    dz = cz - tile_s[2 * kBqTile + t];
+        const float d2 = pcr_sumsq3f(dx, dy, dz);
+        if (d2 < r2 && (double)d2 > 1e-5) {
+          if (cnt == 0) first = t0 + t;
+          I[cnt] = t0 + t;
+          ++cnt;
+        }
+      }
+      if (cnt >= u) done = true;
+    }
+    __syncthreads();
+  }
+  if (active)
+    for (int v = cnt; v < u; v++) I[v] = first;
+}
+
+// grouping.cu:29-35: one thread per output element, coalesced stores
+__global__ __launch_bounds__(256) void grouping_kernel(const float* __restrict__ feat,
+                                                       const int* __restrict__ idx, int c, int n,
+                                                       int m, int u, float* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // over m*u
+  const int l = blockIdx.y;
+  const int b = blockIdx.z;
+  const int64_t mu = (int64_t)m * u;
+  if (e >= mu) return;
+  const int s = idx[(size_t)b * mu + e];
+  const float v = (s >= 0 && s < n) ? feat[((size_t)b * c + l) * n + s] : 0.0f;
+  out[((size_t)b * c + l) * mu + e] = v;
+}
+
+// grouping.cu:69-76
+__global__ __launch_bounds__(256) void grouping_grad_kernel(const float* __restrict__ grad_y,
+                                                            const int* __restrict__ idx, int c,
+                                                            int n, int m, int u,
+                                                            float* __restrict__ grad_x) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int l = blockIdx.y;
+  const int b = blockIdx.z;
+  const int64_t mu = (int64_t)m * u;
+  if (e >= mu) return;
+  const int s = idx[(size_t)b * mu + e];
+  if (s < 0 || s >= n) return;
+  atomicAdd(grad_x + ((size_t)b * c + l) * n + s, grad_y[((size_t)b * c + l) * mu + e]);
+}
+
+// ---------------------------------------------------------- self tests
+__global__ void selftest_f_kernel(int op, const float* x, const float* y, int n, int aux,
+                                  float* of, int* oi) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  switch (op) {
+    case 0: of[i] = pcr_acosf(x[i]); break;
+    case 1: of[i] = pcr_atanf(x[i]); break;
+    case 2: of[i] = __builtin_sqrtf(x[i]); break;
+    case 3: of[i] = x[i] / y[i]; break;
+    case 4: oi[i] = pcr_sph_index(x[i], x[i + n], x[i + 2 * n], aux); break;
+    default: break;
+  }
+}
+__global__ void selftest_d_kernel(int op, const double* x, const double* y, int n, double* o) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  switch (op) {
+    case 0: o[i] = pcr_acos_d(x[i]); break;
+    case 1: o[i] = pcr_atan_d(x[i]); break;
+    case 2: o[i] = __builtin_sqrt(x[i]); break;
+    case 3: o[i] = x[i] / y[i]; break;
+    case 4: o[i] = __builtin_fma(x[i], y[i], x[i]); break;
+    default: break;
+  }
+}
+
+template <bool PPF, int CC>
+static pcr_status launch_knn_c(const float* xyz1, const float* xyz2, int b, int c, int n, int m,
+                               int k, float* dist, int* idx, const float* normals, int relative,
+                               float* ppf, hipStream_t st) {
+  dim3 grid(ceil_div(n, kKnnThreads), b);
+  if (k <= 16)
+    hipLaunchKernelGGL((knn_kernel<16, PPF, CC>), grid, dim3(kKnnThreads), 0, st, xyz1, xyz2, c,
+                       n, m, k, dist, idx, normals, relative, ppf);
+  else if (k <= 32)
+    hipLaunchKernelGGL((knn_kernel<32, PPF, CC>), grid, dim3(kKnnThreads), 0, st, xyz1, xyz2, c,
+                       n, m, k, dist, idx, normals, relative, ppf);
+  else if (k <= 64)
+    hipLaunchKernelGGL((knn_kernel<64, PPF, CC>), grid, dim3(kKnnThreads), 0, st, xyz1, xyz2, c,
+                       n, m, k, dist, idx, normals, relative, ppf);
+  else if (k <= 128)
+    hipLaunchKernelGGL((knn_kernel<128, PPF, CC>), grid, dim3(kKnnThreads), 0, st, xyz1, xyz2, c,
+                       n, m, k, dist, idx, normals, relative, ppf);
+  else
+    return PCR_ERR_UNSUPPORTED;
+  return PCR_OK;
+}
+
+template <bool PPF>
+static pcr_status launch_knn(const float* xyz1, const float* xyz2, int b, int c, int n, int m,
+                             int k, float* dist, int* idx, const float* normals, int relative,
+                             float* ppf, hipStream_t st) {
+  if (c == 3)
+    return launch_knn_c<PPF, 3>(xyz1, xyz2, b, c, n, m, k, dist, idx, normals, relative, ppf, st);
+  if (PPF) return PCR_ERR_UNSUPPORTED;
+  return launch_knn_c<false, kMaxC>(xyz1, xyz2, b, c, n, m, k, dist, idx, normals, relative, ppf,
+                                    st);
+}
+
+}  // namespace pcr
+
+using namespace pcr;
+
+extern "C" pcr_status pcr_knn_forward(const float* xyz1, const float* xyz2, int b, int c, int n,
+                                      int m, int k, float* dist1, float* dist2, int* idx1,
+                                      int* idx2, void* stream) {
+  PCR_REQUIRE(b >= 0 && c >= 1 && n >= 0 && m >= 0 && k >= 1, "knn_forward: invalid sizes");
+  if (b == 0) return PCR_OK;
+  hipStream_t st = as_stream(stream);
+  if (c <= kMaxC && k <= 128) {
+    if (n > 0) launch_knn<false>(xyz1, xyz2, b, c, n, m, k, dist1, idx1, nullptr, 0, nullptr, st);
+    if (m > 0) launch_knn<false>(xyz2, xyz1, b, c, m, n, k, dist2, idx2, nullptr, 0, nullptr, st);
+  } else {
+    if (n > 0)
+      hipLaunchKernelGGL(knn_generic_kernel, dim3(ceil_div(n, 256), b), dim3(256), 0, st, xyz1,
+                         xyz2, c, n, m, k, dist1, idx1);
+    if (m > 0)
+      hipLaunchKernelGGL(knn_generic_kernel, dim3(ceil_div(m, 256), b), dim3(256), 0, st, xyz2,
+                         xyz1, c, m, n, k, dist2, idx2);
+  }
+  return launch_status("knn_forward");
+}
+
+extern "C" pcr_status pcr_knn_backward(const float* xyz1, const float* xyz2,
+                                       const float* graddist1, const float* graddist2,
+                                       const int* idx1, const int* idx2, int b, int c, int n,
+                                       int m, int k, float* gradxyz1, float* gradxyz2,
+                                       void* stream) {
+  PCR_REQUIRE(b >= 0 && c >= 1 && n >= 0 && m >= 0 && k >= 1, "knn_backward: invalid sizes");
+  if (b == 0) return PCR_OK;
+  hipStream_t st = as_stream(stream);
+  if (hipMemsetAsync(gradxyz1, 0, sizeof(float) * (size_t)b * c * n, st) != hipSuccess ||
+      hipMemsetAsync(gradxyz2, 0, sizeof(float) * (size_t)b * c * m, st) != hipSuccess)
+    return launch_status("knn_backward memset");
+  if (n > 0)
+    hipLaunchKernelGGL(knn_grad_kernel, dim3(ceil_div(n, 256), b), dim3(256), 0, st, xyz1, xyz2,
+                       c, n, m, k, graddist1, idx1, gradxyz1, gradxyz2);
+  if (m > 0)
+    hipLaunchKernelGGL(knn_grad_kernel, dim3(ceil_div(m, 256), b), dim3(256), 0, st, xyz2, xyz1,
+                       c, m, n, k, graddist2, idx2, gradxyz2, gradxyz1);
+  return launch_status("knn_backward");
+}
+
+extern "C" pcr_status pcr_knn_local_ppf(const float* xyz, const float* normals, int b, int n,
+                                        int k, int relative, int* idx, float* dist, float* ppf,
+                                        void* stream) {
+  PCR_REQUIRE(b >= 0 && n >= 1 && k >= 1 && k <= 128, "knn_local_ppf: invalid sizes (k<=128)");
+  PCR_REQUIRE(ppf != nullptr && idx != nullptr, "knn_local_ppf: idx and ppf outputs required");
+  if (b == 0) return PCR_OK;
+  launch_knn<true>(xyz, xyz, b, 3, n, n, k, dist, idx, normals, relative, ppf, as_stream(stream));
+  return launch_status("knn_local_ppf");
+}
+
+extern "C" pcr_status pcr_spherical_ppf_forward(const float* coords, const float* center,
+                                                const float* normals, const float* center_normal,
+                                                int b, int n, float* feat, void* stream) {
+  PCR_REQUIRE(b >= 0 && n >= 0, "spherical_ppf_forward: invalid sizes");
+  if (b == 0 || n == 0) return PCR_OK;
+  hipLaunchKernelGGL(global_ppf_kernel, dim3(ceil_div(n, 256), b), dim3(256), 0,
+                     as_stream(stream), coords, center, normals, center_normal, n, feat);
+  return launch_status("spherical_ppf_forward");
+}
+
+extern "C" pcr_status pcr_local_ppf_forward(const float* points, const float* normals,
+                                            const float* centers, const float* center_normals,
+                                            const int* idx, int b, int n, int m, int u,
+                                            int idx_kmajor, int relative, float* out,
+                                            void* stream) {
+  PCR_REQUIRE(b >= 0 && n >= 1 && m >= 0 && u >= 0, "local_ppf_forward: invalid sizes");
+  PCR_REQUIRE(u <= 65535, "local_ppf_forward: u too large");
+  if (b == 0 || m == 0 || u == 0) return PCR_OK;
+  hipLaunchKernelGGL(local_ppf_kernel, dim3(ceil_div(m, 256), u, b), dim3(256), 0,
+                     as_stream(stream), points, normals, centers, center_normals, idx, n, m, u,
+                     idx_kmajor, relative, out);
+  return launch_status("local_ppf_forward");
+}
+
+extern "C" pcr_status pcr_ball_query(const float* centers, const float* points, int b, int m,
+                                     int n, float radius, int u, int* idx, void* stream) {
+  PCR_REQUIRE(b >= 0 && m >= 0 && n >= 0 && u >= 1, "ball_query: invalid sizes");
+  if (b == 0 || m == 0) return PCR_OK;
+  const float r2 = radius * radius;  // ball_query.cpp:24 (float * float)
+  hipLaunchKernelGGL(ball_query_kernel, dim3(ceil_div(m, 256), b), dim3(256), 0,
+                     as_stream(stream), centers, points, m, n, r2, u, idx);
+  return launch_status("ball_query");
+}
+
+extern "C" pcr_status pcr_grouping_forward(const float* features, const int* indices, int b, int c,
+                                           int n, int m, int u, float* out, void* stream) {
+  PCR_REQUIRE(b >= 0 && c >= 0 && n >= 0 && m >= 0 && u >= 0, "grouping_forward: invalid sizes");
+  PCR_REQUIRE(c <= 65535, "grouping_forward: c too large");
+  const int64_t mu = (int64_t)m * u;
+  if (b == 0 || c == 0 || mu == 0) return PCR_OK;
+  hipLaunchKernelGGL(grouping_kernel, dim3((unsigned)ceil_div64(mu, 256), c, b), dim3(256), 0,
+                     as_stream(stream), features, indices, c, n, m, u, out);
+  return launch_status("grouping_forward");
+}
+
+extern "C" pcr_status pcr_grouping_backward(const float* grad_y, const int* indices, int b, int c,
+                                            int n, int m, int u, float* grad_x, void* stream) {
+  PCR_REQUIRE(b >= 0 && c >= 0 && n >= 0 && m >= 0 && u >= 0, "grouping_backward: invalid sizes");
+  PCR_REQUIRE(c <= 65535, "grouping_backward: c too large");
+  if (b == 0 || c == 0) return PCR_OK;
+  hipStream_t st = as_stream(stream);
+  if (hipMemsetAsync(grad_x, 0, sizeof(float) * (size_t)b * c * n, st) != hipSuccess)
+    return launch_status("grouping_backward memset");
+  const int64_t mu = (int64_t)m * u;
+  if (mu == 0) return PCR_OK;
+  hipLaunchKernelGGL(grouping_grad_kernel, dim3((unsigned)ceil_div64(mu, 256), c, b), dim3(256),
+                     0, st, grad_y, indices, c, n, m, u, grad_x);
+  return launch_status("grouping_backward");
+}
+
+extern "C" pcr_status pcr_selftest_math(int op, const float* x, const float* y, int n, int aux,
+                                        float* out_f, int* out_i, void* stream) {
+  PCR_REQUIRE(n >= 0 && op >= 0 && op <= 4, "selftest_math: invalid args");
+  if (n == 0) return PCR_OK;
+  hipLaunchKernelGGL(selftest_f_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, as_stream(stream),
+                     op, x, y, n, aux, out_f, out_i);
+  return launch_status("selftest_math");
+}
+
+extern "C" pcr_status pcr_selftest_math_d(int op, const double* x, const double* y, int n,
+                                          double* out, void* stream) {
+  PCR_REQUIRE(n >= 0 && op >= 0 && op <= 4, "selftest_math_d: invalid args");
+  if (n == 0) return PCR_OK;
+  hipLaunchKernelGGL(selftest_d_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, as_stream(stream),
+                     op, x, y, n, out);
+  return launch_status("selftest_math_d");
+}

@@ -1,0 +1,78 @@
+"""ctypes binding of libpcr_amd.so (the C ABI declared in include/pcr_amd.h).
+
+This is the reference-side binding a maintainer adds to call the MI355X
+library: every symbol of the header with its exact C signature.  There is no
+CPU fallback anywhere in the product path -- if the shared library is missing
+or a call fails, a RuntimeError is raised.
+"""
+import ctypes
+import os
+
+_PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("PCR_AMD_LIB", os.path.join(_PKG_ROOT, "lib", "libpcr_amd.so"))
+CSRC_DIR = os.path.join(_PKG_ROOT, "csrc")
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+F = ctypes.c_float
+SZ = ctypes.c_size_t
+ST = ctypes.c_int
+
+# name -> (restype, argtypes); mirrors include/pcr_amd.h one to one
+SIGNATURES = {
+    "pcr_last_error": (ctypes.c_char_p, []),
+    "pcr_version": (ctypes.c_char_p, []),
+    "pcr_knn_forward": (ST, [P, P, I, I, I, I, I, P, P, P, P, P]),
+    "pcr_knn_backward": (ST, [P, P, P, P, P, P, I, I, I, I, I, P, P, P]),
+    "pcr_spherical_ppf_forward": (ST, [P, P, P, P, I, I, P, P]),
+    "pcr_local_ppf_forward": (ST, [P, P, P, P, P, I, I, I, I, I, I, P, P]),
+    "pcr_knn_local_ppf": (ST, [P, P, I, I, I, I, P, P, P, P]),
+    "pcr_ball_query": (ST, [P, P, I, I, I, F, I, P, P]),
+    "pcr_grouping_forward": (ST, [P, P, I, I, I, I, I, P, P]),
+    "pcr_grouping_backward": (ST, [P, P, I, I, I, I, I, P, P]),
+    "pcr_voxelize_workspace_size": (SZ, [I, I, I]),
+    "pcr_spherical_avg_voxelize_forward": (ST, [P, P, I, I, I, I, P, P, P, P, SZ, P]),
+    "pcr_avg_voxelize_forward": (ST, [P, P, I, I, I, I, P, P, P, P, SZ, P]),
+    "pcr_avg_voxelize_backward": (ST, [P, P, P, I, I, I, I, P, P]),
+    "pcr_spherical_normalize": (ST, [P, I, I, P, P]),
+    "pcr_spherical_trilinear_devoxelize_forward": (ST, [I, I, P, P, P, I, I, I, P, P, P, P]),
+    "pcr_trilinear_devoxelize_forward": (ST, [I, I, P, P, I, I, I, P, P, P, P]),
+    "pcr_devoxelize_backward": (ST, [P, P, P, I, I, I, I, I, P, P]),
+    "pcr_dgcnn_center_gather": (ST, [P, P, P, I, I, I, I, P, P]),
+    "pcr_extractor_workspace_size": (SZ, [I, I, I, I]),
+    "pcr_extractor_voxel_stage": (ST, [P, P, I, I, I, I, P, P, P, P, P, P, P, P, P, SZ, P]),
+    "pcr_extractor_voxel_prep": (ST, [P, I, I, I, P, P, P, P, P, SZ, P]),
+    "pcr_extractor_voxel_grid": (ST, [P, I, I, I, I, P, P, P, P, P, P, P, SZ, P]),
+    "pcr_selftest_math": (ST, [I, P, P, I, I, P, P, P]),
+    "pcr_selftest_math_d": (ST, [I, P, P, I, P, P]),
+}
+
+_lib = None
+
+
+def load():
+    """Load libpcr_amd.so once; raise loudly if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            "libpcr_amd.so not found at %s -- build it with `make -C %s` "
+            "(or __graft_entry__.build()); there is no CPU fallback" % (LIB_PATH, CSRC_DIR))
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(status, what):
+    if status != 0:
+        msg = load().pcr_last_error()
+        raise RuntimeError("%s failed (status %d): %s" % (what, status, msg.decode() if msg else ""))
+
+
+def version():
+    return load().pcr_version().decode()

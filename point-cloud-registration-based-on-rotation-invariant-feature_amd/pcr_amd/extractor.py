@@ -1,0 +1,144 @@
+"""Fused sph-dg extractor forward: the north-star hot path as one step.
+
+One step over a batch of clouds (xyz [B,3,N], normals [B,3,N], point
+features [B,C,N], all resident on the GPU):
+
+  neighbour stage (stream A): self-KNN (k) -> local PPF [B,4,k,N]
+      = knn_forward_cuda + the model's local-PPF block
+        (PVCNN/models/pvcnn_classify.py:252-269), fused in one kernel
+  voxel stage (stream B): Spherical_Voxelization normalisation
+      (PVCNN/modules/spherical_vox.py:16-20) -> spherical_avg_voxelize
+      (grid [B,C,r^3], ind, cnt) -> spherical_trilinear_devoxelize of that grid
+      ([B,C,N] + inds/wgts) -> per-cloud descriptor (max over points) [B,C]
+
+The two stages are independent, so they run on two HIP streams forked from
+and joined back to the caller's stream; the whole step is capturable into a
+hipGraph (``capture()`` / ``replay()``) so a step costs one graph launch.
+"""
+import torch
+
+from . import _lib
+from .ops import _ptr
+
+
+class SphExtractor:
+    def __init__(self, batch, npoints, channels, k, resolution, device="cuda", relative=True,
+                 with_dist=False):
+        self.b, self.n, self.c, self.k, self.r = batch, npoints, channels, k, resolution
+        self.relative = relative
+        self.device = torch.device(device)
+        b, n, c, r = batch, npoints, channels, resolution
+        r3 = r * r * r
+        dev = self.device
+        e = torch.empty
+        self.knn_idx = e((b, k, n), dtype=torch.int32, device=dev)
+        self.knn_dist = e((b, k, n), dtype=torch.float32, device=dev) if with_dist else None
+        self.local_ppf = e((b, 4, k, n), dtype=torch.float32, device=dev)
+        self.norm_coords = e((b, 3, n), dtype=torch.float32, device=dev)
+        self.ind = e((b, n), dtype=torch.int32, device=dev)
+        self.cnt = e((b, r3), dtype=torch.int32, device=dev)
+        self.grid = e((b, c, r3), dtype=torch.float32, device=dev)
+        self.devox = e((b, c, n), dtype=torch.float32, device=dev)
+        self.dinds = e((b, 8, n), dtype=torch.int32, device=dev)
+        self.dwgts = e((b, 8, n), dtype=torch.float32, device=dev)
+        self.desc = e((b, c), dtype=torch.float32, device=dev)
+        lib = _lib.load()
+        self.ws = e(max(256, lib.pcr_extractor_workspace_size(b, n, c, r)), dtype=torch.uint8,
+                    device=dev)
+        self.s_nbr = torch.cuda.Stream(device=dev)
+        self.s_vox = torch.cuda.Stream(device=dev)
+        self.graph = None
+        self._static_in = None
+
+    # ---------------------------------------------------------------- stages
+    def neighbor_stage(self, xyz, normals, stream):
+        _lib.check(_lib.load().pcr_knn_local_ppf(
+            _ptr(xyz), _ptr(normals), self.b, self.n, self.k, int(self.relative),
+            _ptr(self.knn_idx), _ptr(self.knn_dist), _ptr(self.local_ppf), stream),
+            "knn_local_ppf")
+
+    def voxel_stage(self, xyz, features, stream):
+        _lib.check(_lib.load().pcr_extractor_voxel_stage(
+            _ptr(xyz), _ptr(features), self.b, self.c, self.n, self.r, _ptr(self.norm_coords),
+            _ptr(self.ind), _ptr(self.cnt), _ptr(self.grid), _ptr(self.devox), _ptr(self.dinds),
+            _ptr(self.dwgts), _ptr(self.desc), _ptr(self.ws), self.ws.numel(), stream),
+            "extractor_voxel_stage")
+
+    def voxel_prep(self, xyz, stream):
+        _lib.check(_lib.load().pcr_extractor_voxel_prep(
+            _ptr(xyz), self.b, self.n, self.r, _ptr(self.norm_coords), _ptr(self.ind),
+            _ptr(self.dinds), _ptr(self.dwgts), _ptr(self.ws), self.ws.numel(), stream),
+            "extractor_voxel_prep")
+
+    def voxel_grid(self, features, stream):
+        """The dominant kernel (vox_grid_kernel<true>) on its own."""
+        _lib.check(_lib.load().pcr_extractor_voxel_grid(
+            _ptr(features), self.b, self.c, self.n, self.r, _ptr(self.cnt), _ptr(self.grid),
+            _ptr(self.devox), _ptr(self.dinds), _ptr(self.dwgts), _ptr(self.desc), _ptr(self.ws),
+            self.ws.numel(), stream), "extractor_voxel_grid")
+
+    def forward(self, xyz, normals, features):
+        """Enqueue one step on the current stream (fork/join over two streams)."""
+        for t, name in ((xyz, "xyz"), (normals, "normals"), (features, "features")):
+            if not (t.is_cuda and t.is_contiguous() and t.dtype == torch.float32):
+                raise RuntimeError("%s must be a contiguous float CUDA tensor" % name)
+        if tuple(xyz.shape) != (self.b, 3, self.n) or tuple(features.shape) != (self.b, self.c,
+                                                                                  self.n):
+            raise RuntimeError("input shape does not match the extractor configuration")
+        cur = torch.cuda.current_stream(self.device)
+        self.s_nbr.wait_stream(cur)
+        self.s_vox.wait_stream(cur)
+        self.neighbor_stage(xyz, normals, self.s_nbr.cuda_stream)
+        self.voxel_stage(xyz, features, self.s_vox.cuda_stream)
+        cur.wait_stream(self.s_nbr)
+        cur.wait_stream(self.s_vox)
+        return self.outputs()
+
+    def outputs(self):
+        return {
+            "knn_idx": self.knn_idx, "local_ppf": self.local_ppf, "norm_coords": self.norm_coords,
+            "ind": self.ind, "cnt": self.cnt, "grid": self.grid, "devox": self.devox,
+            "dinds": self.dinds, "dwgts": self.dwgts, "desc": self.desc,
+        }
+
+    # ---------------------------------------------------------------- graphs
+    def capture(self, xyz, normals, features):
+        """Capture one step into a hipGraph bound to these input tensors."""
+        self._static_in = (xyz, normals, features)
+        side = torch.cuda.Stream(device=self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):
+            self.forward(xyz, normals, features)  # warm-up outside capture
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.forward(xyz, normals, features)
+        self.graph = g
+        return g
+
+    def replay(self):
+        self.graph.replay()
+        return self.outputs()
+
+
+def grid_kernel_bytes_per_cloud(n, r, c):
+    """Algorithmic HBM bytes of the dominant kernel (fused vox grid + devox +
+    descriptor) per cloud: features read 4CN, grid written 4C r^3, cnt
+    written 4 r^3, devox written 4CN, corner inds+wgts read 64N, descriptor
+    4C.  (The <= 80 hot grid cells devox reads come from LDS, not HBM.)"""
+    r3 = r ** 3
+    return 4 * c * n + 4 * c * r3 + 4 * r3 + 4 * c * n + 64 * n + 4 * c
+
+
+def algorithmic_bytes_per_cloud(n, k, r, c):
+    """SURVEY.md 8d per-cloud byte model (the roofline.achieved numerator):
+    KNN 12N + 4kN; local PPF 24N + 16kN; sph-vox 12N + 4CN + 4N + 4r^3 + 4C r^3;
+    sph-devox 12N + 4N + 320C + 4CN + 64N."""
+    r3 = r ** 3
+    knn = 12 * n + 4 * k * n
+    lppf = 24 * n + 16 * k * n
+    vox = 12 * n + 4 * c * n + 4 * n + 4 * r3 + 4 * c * r3
+    devox = 12 * n + 4 * n + 4 * 80 * c + 4 * c * n + 64 * n
+    return {"knn": knn, "local_ppf": lppf, "sph_vox": vox, "sph_devox": devox,
+            "total": knn + lppf + vox + devox}

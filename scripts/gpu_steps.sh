@@ -1,0 +1,33 @@
+#!/bin/bash
+# Runs GPU steps in order on the gpurun box.  Each step has its own time
+# limit; a test failure (exit 1) lets the next step run, but a crash, abort,
+# signal or timeout (anything else non-zero) stops the script: nothing more
+# touches the GPU after a fault.
+#   usage: scripts/gpu_steps.sh <step> [<step> ...]
+#   steps: smoke tests bench prof pmc
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+run() {  # name limit cmd...
+  local name=$1 limit=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$limit" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  tail -n 25 "gpurun_out/$name.log"
+  echo "=== $name exit $rc"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+for step in "$@"; do
+  case $step in
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) run pytest_gpu 1200 python -m pytest tests -x -q -m gpu -p no:cacheprovider ;;
+    tests_all) run pytest_gpu 1200 python -m pytest tests -q -m gpu -p no:cacheprovider ;;
+    bench) run bench 600 python bench.py ;;
+    prof) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+          run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline ;;
+    pmc)  run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --kernel-iters 5 --no-cpu-baseline --no-graph
+          run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --kernel-iters 5 --no-cpu-baseline --no-graph ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done

@@ -1,0 +1,147 @@
+"""GPU parity of the fused extractor step (bench.py's workload) and of the
+shared bit-exact math, plus full-size property tests."""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from clouds import gaussian_clouds
+
+pytestmark = pytest.mark.gpu
+
+
+def T(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def N(t):
+    return t.detach().cpu().numpy()
+
+
+def expected_step(xyz, nrm, feat, k, r):
+    """Composition of oracle ops = what one extractor step must produce."""
+    ki_d, ki = oracle.knn_dir(xyz, xyz, k)
+    lppf = oracle.local_ppf(xyz, nrm, xyz, nrm, ki, kmajor=True, relative=True)
+    nc = oracle.normalize_sph(xyz)
+    grid, ind, cnt = oracle.spherical_avg_voxelize_forward(feat, nc, r)
+    devox, dinds, dwgts = oracle.spherical_trilinear_devoxelize_forward(r, nc, grid, ind)
+    desc = devox.max(axis=2)
+    return dict(knn_idx=ki, local_ppf=lppf, norm_coords=nc, ind=ind, cnt=cnt, grid=grid,
+                devox=devox, dinds=dinds, dwgts=dwgts, desc=desc)
+
+
+@pytest.mark.parametrize("b,n,c,k,r", [(1, 1024, 64, 16, 16), (4, 1024, 64, 32, 32),
+                                       (2, 2048, 32, 32, 32), (2, 500, 7, 8, 9)])
+def test_extractor_matches_oracle(dev, b, n, c, k, r):
+    from pcr_amd.extractor import SphExtractor
+    xyz, nrm, feat = gaussian_clouds(b, n, seed=n + b, c=c)
+    ex = SphExtractor(b, n, c, k, r, device=dev)
+    out = ex.forward(T(xyz, dev), T(nrm, dev), T(feat, dev))
+    torch.cuda.synchronize()
+    exp = expected_step(xyz, nrm, feat, k, r)
+    for key in ("knn_idx", "ind", "cnt", "dinds"):
+        assert np.array_equal(N(out[key]), exp[key]), key
+    for key in ("norm_coords", "grid", "dwgts", "devox", "desc"):
+        assert np.array_equal(N(out[key]), exp[key]), key
+    assert np.array_equal(N(out["local_ppf"]), exp["local_ppf"], equal_nan=True)
+
+
+def test_extractor_graph_replay(dev):
+    from pcr_amd.extractor import SphExtractor
+    b, n, c, k, r = 8, 1024, 64, 32, 32
+    xyz, nrm, feat = gaussian_clouds(b, n, seed=1, c=c)
+    tx, tn, tf = T(xyz, dev), T(nrm, dev), T(feat, dev)
+    ex = SphExtractor(b, n, c, k, r, device=dev)
+    ref = {kk: v.clone() for kk, v in ex.forward(tx, tn, tf).items()}
+    ex.capture(tx, tn, tf)
+    for _ in range(3):
+        out = ex.replay()
+    torch.cuda.synchronize()
+    for key, v in ref.items():
+        assert torch.equal(out[key], v) or torch.allclose(out[key], v, equal_nan=True), key
+
+
+def test_extractor_full_size_properties(dev):
+    """BASELINE c2 shape: 32 x 1024, k=32, r=32, C=64 -- size-independent
+    properties: ind consistent with cnt, grid empty where cnt == 0, the grid
+    mean reproduces the per-voxel mean, knn slot 0 is at distance 0."""
+    from pcr_amd.extractor import SphExtractor
+    b, n, c, k, r = 32, 1024, 64, 32, 32
+    xyz, nrm, feat = gaussian_clouds(b, n, seed=7, c=c)
+    ex = SphExtractor(b, n, c, k, r, device=dev, with_dist=True)
+    out = ex.forward(T(xyz, dev), T(nrm, dev), T(feat, dev))
+    torch.cuda.synchronize()
+    ind, cnt, grid = out["ind"].long(), out["cnt"], out["grid"]
+    valid = ind >= 0
+    hist = torch.zeros_like(cnt)
+    for bi in range(b):
+        hist[bi].index_add_(0, ind[bi][valid[bi]], torch.ones_like(ind[bi][valid[bi]],
+                                                                   dtype=cnt.dtype))
+    assert torch.equal(hist, cnt)
+    empty = (cnt == 0).unsqueeze(1).expand_as(grid)
+    assert (grid[empty] == 0).all()
+    sums = torch.zeros_like(grid)
+    tf = T(feat, dev)
+    for bi in range(b):
+        sums[bi].index_add_(1, ind[bi][valid[bi]], tf[bi][:, valid[bi]])
+    mean = sums / cnt.clamp(min=1).unsqueeze(1)
+    assert torch.allclose(mean, grid, atol=1e-5)
+    assert (ex.knn_dist[:, 0, :] == 0).all()
+    # full-size bit-exact check on two clouds against the oracle
+    exp = expected_step(xyz[:2], nrm[:2], feat[:2], k, r)
+    for key in ("knn_idx", "ind", "cnt", "grid", "devox"):
+        assert np.array_equal(N(out[key][:2]), exp[key]), key
+
+
+def test_device_math_bit_exact(dev):
+    """pcr_math.h evaluated on gfx950 == the same code on the host."""
+    import ctypes
+    from pcr_amd import _lib
+    lib = _lib.load()
+    rng = np.random.default_rng(0)
+    n = 1 << 20
+    x = np.concatenate([rng.uniform(-1, 1, n - 8),
+                        [-1, 1, 0, -0.0, 0.5, -0.5, 1e-30, np.nextafter(1, 0)]]).astype(np.float32)
+    tx = T(x, dev)
+    out = torch.empty_like(tx)
+    s = torch.cuda.current_stream().cuda_stream
+    for op, ref in ((0, oracle.acosf), (1, oracle.atanf)):
+        _lib.check(lib.pcr_selftest_math(op, tx.data_ptr(), None, n, 0, out.data_ptr(), None, s),
+                   "selftest")
+        assert np.array_equal(N(out), ref(x)), op
+    t = (rng.standard_normal(n) * 10).astype(np.float32)
+    tt = T(t, dev)
+    _lib.check(lib.pcr_selftest_math(1, tt.data_ptr(), None, n, 0, out.data_ptr(), None, s), "st")
+    assert np.array_equal(N(out), oracle.atanf(t))
+    pos = np.abs(t).astype(np.float32)
+    tp = T(pos, dev)
+    _lib.check(lib.pcr_selftest_math(2, tp.data_ptr(), None, n, 0, out.data_ptr(), None, s), "st")
+    assert np.array_equal(N(out), np.sqrt(pos))
+    y = rng.standard_normal(n).astype(np.float32)
+    ty = T(y, dev)
+    _lib.check(lib.pcr_selftest_math(3, tt.data_ptr(), ty.data_ptr(), n, 0, out.data_ptr(), None,
+                                     s), "st")
+    assert np.array_equal(N(out), (t / y).astype(np.float32))
+    # double sqrt / div / fma / acos
+    xd = rng.uniform(0, 4, n)
+    yd = rng.uniform(0.1, 4, n)
+    txd, tyd = T(xd, dev), T(yd, dev)
+    od = torch.empty_like(txd)
+    _lib.check(lib.pcr_selftest_math_d(2, txd.data_ptr(), None, n, od.data_ptr(), s), "st")
+    assert np.array_equal(N(od), np.sqrt(xd))
+    _lib.check(lib.pcr_selftest_math_d(3, txd.data_ptr(), tyd.data_ptr(), n, od.data_ptr(), s),
+               "st")
+    assert np.array_equal(N(od), xd / yd)
+    xa = rng.uniform(-1, 1, n)
+    txa = T(xa, dev)
+    _lib.check(lib.pcr_selftest_math_d(0, txa.data_ptr(), None, n, od.data_ptr(), s), "st")
+    assert np.array_equal(N(od), oracle.acos_d(xa))
+    # spherical voxel index over many points, r = 32
+    xyz, _, _ = gaussian_clouds(1, 1 << 18, seed=3)
+    nc = oracle.normalize_sph(xyz)[0]
+    ti = torch.empty(nc.shape[1], dtype=torch.int32, device=dev)
+    tnc = T(nc, dev)
+    _lib.check(lib.pcr_selftest_math(4, tnc.data_ptr(), None, nc.shape[1], 32, None,
+                                     ti.data_ptr(), s), "st")
+    assert np.array_equal(N(ti), oracle.sph_index(nc, 32))
+    del ctypes

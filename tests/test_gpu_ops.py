@@ -1,0 +1,265 @@
+"""GPU parity: every hot-path op through the C ABI vs the golden fixtures and the
+CPU oracle.  Indices must match bit for bit; floats within the north-star
+tolerance (1e-5 abs) -- most are in fact bit-identical because the kernels
+and the oracle share include/pcr_math.h and the same accumulation order."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from clouds import gaussian_clouds, edge_norm_coords
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = np.load(os.path.join(os.path.dirname(__file__), "golden", "golden.npz"))
+TOL = 1e-5  # north_star: PPF angles and devoxelised features within 1e-5 fp32
+
+
+def T(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def N(t):
+    return t.detach().cpu().numpy()
+
+
+def close(a, b, tol=TOL):
+    a, b = np.asarray(a), np.asarray(b)
+    assert a.shape == b.shape, (a.shape, b.shape)
+    both_nan = np.isnan(a) & np.isnan(b)
+    diff = np.abs(np.where(both_nan, 0, a - b))
+    assert not np.isnan(diff).any(), "NaN mismatch"
+    assert diff.max(initial=0) <= tol, diff.max()
+
+
+# --------------------------------------------------------------- voxelize
+def test_sph_vox_golden(dev):
+    from pcr_amd import ops
+    g = GOLDEN
+    out, ind, cnt = ops.spherical_avg_voxelize_forward(T(g["svox_feat"], dev),
+                                                       T(g["svox_coords"], dev), int(g["svox_r"]))
+    assert np.array_equal(N(ind), g["svox_ind"])
+    assert np.array_equal(N(cnt), g["svox_cnt"])
+    assert np.array_equal(N(out), g["svox_out"])  # same summation order -> bit-exact
+    assert N(ind)[0, 0] == 2056
+
+
+@pytest.mark.parametrize("b,n,c,r", [(1, 1024, 64, 16), (32, 1024, 64, 32), (3, 2048, 67, 32),
+                                     (2, 777, 5, 7), (2, 4096, 3, 64)])
+def test_sph_vox_random(dev, b, n, c, r):
+    from pcr_amd import ops
+    xyz, _, feat = gaussian_clouds(b, n, seed=b * 7 + n, c=c)
+    nc = oracle.normalize_sph(xyz)
+    out, ind, cnt = ops.spherical_avg_voxelize_forward(T(feat, dev), T(nc, dev), r)
+    eo, ei, ec = oracle.spherical_avg_voxelize_forward(feat, nc, r)
+    assert np.array_equal(N(ind), ei)
+    assert np.array_equal(N(cnt), ec)
+    assert np.array_equal(N(out), eo)
+
+
+def test_sph_vox_backward(dev):
+    from pcr_amd import ops
+    g = GOLDEN
+    gx = ops.spherical_avg_voxelize_backward(T(g["svox_grad_y"], dev), T(g["svox_ind"], dev),
+                                             T(g["svox_cnt"], dev))
+    assert np.array_equal(N(gx), g["svox_grad_x"])
+
+
+def test_cube_vox_golden(dev):
+    from pcr_amd import ops
+    g = GOLDEN
+    out, ind, cnt = ops.avg_voxelize_forward(T(g["cvox_feat"], dev), T(g["cvox_vc"], dev),
+                                             int(g["cvox_r"]))
+    assert np.array_equal(N(ind), g["cvox_ind"])
+    assert np.array_equal(N(cnt), g["cvox_cnt"])
+    assert np.array_equal(N(out), g["cvox_out"])
+
+
+def test_normalize(dev):
+    from pcr_amd import ops
+    out = ops.spherical_normalize(T(GOLDEN["norm_in"], dev))
+    assert np.array_equal(N(out), GOLDEN["norm_out"])
+
+
+# ------------------------------------------------------------- devoxelize
+def test_sph_devox_golden(dev):
+    from pcr_amd import ops
+    g = GOLDEN
+    r = int(g["svox_r"])
+    outs, inds, wgts = ops.spherical_trilinear_devoxelize_forward(
+        r, True, T(g["svox_coords"], dev), T(g["sdevox_grid"], dev), T(g["svox_ind"], dev))
+    assert np.array_equal(N(inds), g["sdevox_inds"])
+    assert np.array_equal(N(wgts), g["sdevox_wgts"])
+    close(N(outs), g["sdevox_outs"])
+    assert np.array_equal(N(outs), g["sdevox_outs"])
+
+
+def test_sph_devox_backward(dev):
+    from pcr_amd import ops
+    g = GOLDEN
+    gx = ops.spherical_trilinear_devoxelize_backward(
+        T(g["sdevox_grad_y"], dev), T(g["sdevox_inds"], dev), T(g["sdevox_wgts"], dev),
+        int(g["svox_r"]))
+    close(N(gx), g["sdevox_grad_x"], 1e-4)
+
+
+def test_cube_devox_golden(dev):
+    from pcr_amd import ops
+    g = GOLDEN
+    rc = int(g["cvox_r"])
+    outs, inds, wgts = ops.trilinear_devoxelize_forward(rc, True, T(g["cvox_cc"], dev),
+                                                        T(g["cdevox_grid"], dev))
+    assert np.array_equal(N(inds), g["cdevox_inds"])
+    assert np.array_equal(N(wgts), g["cdevox_wgts"])
+    close(N(outs), g["cdevox_outs"])
+    gx = ops.trilinear_devoxelize_backward(T(g["cdevox_grad_y"], dev), inds, wgts, rc)
+    close(N(gx), g["cdevox_grad_x"], 1e-4)
+
+
+@pytest.mark.parametrize("b,n,c,r", [(4, 1024, 64, 32), (2, 2048, 16, 16)])
+def test_sph_devox_random(dev, b, n, c, r):
+    from pcr_amd import ops
+    xyz, _, feat = gaussian_clouds(b, n, seed=5, c=c)
+    nc = oracle.normalize_sph(xyz)
+    _, ind, _ = oracle.spherical_avg_voxelize_forward(feat, nc, r)
+    grid = np.random.default_rng(9).standard_normal((b, c, r ** 3)).astype(np.float32)
+    outs, inds, wgts = ops.spherical_trilinear_devoxelize_forward(r, False, T(nc, dev),
+                                                                  T(grid, dev), T(ind, dev))
+    eo, ei, ew = oracle.spherical_trilinear_devoxelize_forward(r, nc, grid, ind)
+    assert np.array_equal(N(inds), ei)
+    assert np.array_equal(N(wgts), ew)
+    assert np.array_equal(N(outs), eo)
+    gy = np.random.default_rng(3).standard_normal((b, c, n)).astype(np.float32)
+    gx = ops.spherical_trilinear_devoxelize_backward(T(gy, dev), inds, wgts, r)
+    close(N(gx), oracle.devoxelize_backward(gy, ei, ew, r, spherical=True), 1e-3)
+
+
+# -------------------------------------------------------------------- KNN
+def test_knn_golden(dev):
+    from pcr_amd import ops
+    g = GOLDEN
+    d1, d2, i1, i2 = ops.knn_forward_cuda(T(g["knn_x1"], dev), T(g["knn_x2"], dev),
+                                          int(g["knn_k"]))
+    assert np.array_equal(N(i1), g["knn_i1"])
+    assert np.array_equal(N(i2), g["knn_i2"])
+    assert np.array_equal(N(d1), g["knn_d1"])
+    assert np.array_equal(N(d2), g["knn_d2"])
+
+
+def test_knn_unfilled_slots(dev):
+    from pcr_amd import ops
+    g = GOLDEN
+    xs = g["knn_small_x"]
+    d1, d2, i1, i2 = ops.knn_forward_cuda(T(xs, dev), T(xs[:, :, :7], dev), 12)
+    assert np.array_equal(N(d1), g["knn_small_d1"]) and np.array_equal(N(i1), g["knn_small_i1"])
+    assert np.array_equal(N(d2), g["knn_small_d2"]) and np.array_equal(N(i2), g["knn_small_i2"])
+
+
+@pytest.mark.parametrize("b,n,m,k", [(2, 1024, 1024, 32), (1, 1000, 513, 16), (1, 300, 300, 64),
+                                     (1, 200, 220, 100), (1, 64, 70, 130)])
+def test_knn_random(dev, b, n, m, k):
+    from pcr_amd import ops
+    rng = np.random.default_rng(n + k)
+    x1 = rng.standard_normal((b, 3, n)).astype(np.float32)
+    x2 = rng.standard_normal((b, 3, m)).astype(np.float32)
+    d1, d2, i1, i2 = ops.knn_forward_cuda(T(x1, dev), T(x2, dev), k)
+    e = oracle.knn_forward(x1, x2, k)
+    for got, exp in zip((d1, d2, i1, i2), e):
+        assert np.array_equal(N(got), exp)
+
+
+def test_knn_general_c(dev):
+    from pcr_amd import ops
+    rng = np.random.default_rng(1)
+    x1 = rng.standard_normal((2, 5, 300)).astype(np.float32)
+    x2 = rng.standard_normal((2, 5, 250)).astype(np.float32)
+    got = ops.knn_forward_cuda(T(x1, dev), T(x2, dev), 20)
+    for a, b in zip(got, oracle.knn_forward(x1, x2, 20)):
+        assert np.array_equal(N(a), b)
+
+
+def test_knn_backward(dev):
+    from pcr_amd import ops
+    g = GOLDEN
+    g1, g2 = ops.knn_backward_cuda(T(g["knn_x1"], dev), T(g["knn_x2"], dev), T(g["knn_gd1"], dev),
+                                   T(g["knn_gd2"], dev), T(g["knn_i1"], dev), T(g["knn_i2"], dev))
+    close(N(g1), g["knn_g1"], 1e-4)
+    close(N(g2), g["knn_g2"], 1e-4)
+
+
+# ------------------------------------------------ ball query / grouping / PPF
+def test_ball_query_grouping(dev):
+    from pcr_amd import ops
+    g = GOLDEN
+    pts = T(g["bq_pts"], dev)
+    idx = ops.ball_query(pts, pts, 0.3, 32)
+    assert np.array_equal(N(idx), g["bq_idx"])
+    grp = ops.grouping_forward(pts, idx)
+    assert np.array_equal(N(grp), g["bq_grouped"])
+    gx = ops.grouping_backward(T(g["grp_grad_y"], dev), idx, pts.shape[2])
+    close(N(gx), g["grp_grad_x"], 1e-4)
+
+
+def test_ball_query_large(dev):
+    from pcr_amd import ops
+    xyz, _, _ = gaussian_clouds(2, 3000, seed=4)
+    xyz = xyz * np.float32(0.4)
+    idx = ops.ball_query(T(xyz, dev), T(xyz, dev), 0.3, 128)
+    assert np.array_equal(N(idx), oracle.ball_query(xyz, xyz, 0.3, 128))
+
+
+def test_local_ppf(dev):
+    from pcr_amd import ops
+    g = GOLDEN
+    pts, nrm = T(g["bq_pts"], dev), T(g["bq_nrm"], dev)
+    lp = ops.local_ppf_forward(pts, nrm, pts, nrm, T(g["bq_idx"], dev), kmajor=False)
+    assert np.array_equal(N(lp), g["lppf_ball"], equal_nan=True)
+    lk = ops.local_ppf_forward(pts, nrm, pts, nrm, T(g["lppf_knn_idx"], dev), kmajor=True)
+    assert np.array_equal(N(lk), g["lppf_knn"], equal_nan=True)
+
+
+def test_knn_local_ppf_fused(dev):
+    from pcr_amd import ops
+    xyz, nrm, _ = gaussian_clouds(3, 1024, seed=12)
+    idx, ppf, dist = ops.knn_local_ppf(T(xyz, dev), T(nrm, dev), 32, want_dist=True)
+    ed, ei = oracle.knn_dir(xyz, xyz, 32)
+    assert np.array_equal(N(idx), ei)
+    assert np.array_equal(N(dist), ed)
+    ep = oracle.local_ppf(xyz, nrm, xyz, nrm, ei, kmajor=True, relative=True)
+    assert np.array_equal(N(ppf), ep, equal_nan=True)
+
+
+def test_global_ppf(dev):
+    from pcr_amd import ops
+    g = GOLDEN
+    out = ops.spherical_ppf_forward(T(g["gppf_pts"], dev), T(g["gppf_cen"], dev),
+                                    T(g["gppf_nrm"], dev), T(g["gppf_cnrm"], dev))
+    assert np.array_equal(N(out), g["gppf_out"])
+    assert (N(out)[:, :, 3] == 0).all()  # zero normal -> all-zero row
+
+
+def test_center_gather(dev):
+    from pcr_amd import ops
+    rng = np.random.default_rng(0)
+    feat = rng.standard_normal((2, 6, 100)).astype(np.float32)
+    grid = rng.standard_normal((2, 6, 512)).astype(np.float32)
+    ind = rng.integers(-1, 512, (2, 100)).astype(np.int32)
+    rel = N(ops.dgcnn_center_gather(T(feat, dev), T(grid, dev), T(ind, dev)))
+    exp = feat - np.take_along_axis(grid, np.broadcast_to(np.maximum(ind, 0)[:, None, :],
+                                                          feat.shape), axis=2)
+    exp[np.broadcast_to((ind == -1)[:, None, :], feat.shape)] = 0
+    assert np.array_equal(rel, exp)
+
+
+def test_errors_are_raised(dev):
+    from pcr_amd import ops
+    x = torch.zeros((1, 3, 10), device=dev)
+    with pytest.raises(RuntimeError, match="must be a float tensor"):
+        ops.spherical_avg_voxelize_forward(x.double(), x, 8)
+    with pytest.raises(RuntimeError, match="contiguous"):
+        ops.knn_forward_cuda(x.transpose(1, 2), x, 4)
+    with pytest.raises(RuntimeError, match="unsupported"):
+        big = torch.zeros((1, 3, 5000), device=dev)
+        ops.spherical_avg_voxelize_forward(big, big, 8)
