@@ -32,6 +32,15 @@ pcr_status launch_status(const char* what);
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// Allows a kernel to take more than the default 64 KB of dynamic LDS (gfx950
+// has 160 KB per CU).  Idempotent; cheap after the first call.
+template <typename K>
+inline void allow_big_lds(K kernel, size_t bytes) {
+  if (bytes > 48 * 1024)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
 inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
 inline int64_t ceil_div64(int64_t a, int64_t b) { return (a + b - 1) / b; }
 

@@ -239,6 +239,7 @@ extern "C" pcr_status pcr_devoxelize_backward(const float* grad_y, const int* in
   while (G > 1 && (size_t)G * hw * 4 > 80 * 1024) G >>= 1;
   if ((size_t)G * hw * 4 > 80 * 1024) hw = 80 * 1024 / 4;
   if (hw > r3) hw = r3;
+  allow_big_lds(devox_bwd_kernel, (size_t)G * hw * 4);
   hipLaunchKernelGGL(devox_bwd_kernel, dim3(ceil_div(c, G), b), dim3(kBwdThreads),
                      (size_t)G * hw * 4, as_stream(stream), grad_y, inds, wgts, c, n, r3, G, hw,
                      skip_neg, grad_x);

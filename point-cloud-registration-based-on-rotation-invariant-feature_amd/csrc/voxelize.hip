@@ -551,7 +551,8 @@ static pcr_status run_voxelize(const float* features, const float* coords_f, con
   if (what & 1) {
     const int npad = next_pow2(n < 2 ? 2 : n);
     size_t prep_smem = (size_t)npad * 8 + (size_t)ws.W * 4;
-    PCR_REQUIRE(prep_smem <= 160 * 1024, "%s: prep LDS %zu too large", name, prep_smem);
+    PCR_REQUIRE(prep_smem <= 150 * 1024, "%s: prep LDS %zu too large", name, prep_smem);
+    allow_big_lds(vox_prep_kernel<MODE>, prep_smem);
     hipLaunchKernelGGL(vox_prep_kernel<MODE>, dim3(b), dim3(kPrepThreads), prep_smem, stream,
                        coords_f, coords_i, n, r, npad, norm_out, ind, ws, dinds, dwgts);
   }
@@ -563,7 +564,9 @@ static pcr_status run_voxelize(const float* features, const float* coords_f, con
     const int ntiles = ceil_div(r3, tile);
     const int nw = (tile + 31) / 32 + 1;
     size_t smem = grid_smem_bytes(G, n, nw);
-    PCR_REQUIRE(smem <= 160 * 1024, "%s: grid LDS %zu too large", name, smem);
+    PCR_REQUIRE(smem <= 150 * 1024, "%s: grid LDS %zu too large", name, smem);
+    allow_big_lds(vox_grid_kernel<true>, smem);
+    allow_big_lds(vox_grid_kernel<false>, smem);
     if (devox) {
       PCR_REQUIRE(ntiles == 1, "%s: fused devoxelisation needs r^3 <= 65536", name);
       PCR_REQUIRE(c > 0, "%s: fused devoxelisation needs c > 0", name);
