@@ -50,7 +50,11 @@ const char *pcr_version(void);
  * Squared L2, ascending, ties by lower index, unfilled slots (10000, 0). */
 pcr_status pcr_knn_forward(const float *xyz1, const float *xyz2, int b, int c, int n, int m,
                            int k, float *dist1, float *dist2, int *idx1, int *idx2,
-                           void *stream);
+                           void *workspace, size_t workspace_bytes, void *stream);
+/* Scratch of the spatially pruned KNN (Morton-sorted copies + block boxes of
+ * both point sets).  With workspace == NULL (or c != 3, or more than 4096
+ * points per cloud) a brute-force kernel is used instead, same results. */
+size_t pcr_knn_workspace_size(int b, int n, int m);
 
 /* knn_backward_cuda (knn/knn.cpp:27-52, kernel knn/knn.cu:52-78, :88-98).
  * gradxyz1 [b,c,n], gradxyz2 [b,c,m]; both directions accumulate into both. */
@@ -82,10 +86,12 @@ pcr_status pcr_local_ppf_forward(const float *points, const float *normals, cons
 
 /* Fused self-KNN + local PPF (the extractor's neighbour stage): for every
  * point of xyz [b,3,n] its k nearest points (self included, knn semantics)
- * -> idx [b,k,n] (may be NULL), dist [b,k,n] (may be NULL) and the local PPF
- * [b,4,k,n] of (point, neighbour) with `relative` as above. */
+ * -> idx [b,k,n], dist [b,k,n] (may be NULL) and the local PPF
+ * [b,4,k,n] of (point, neighbour) with `relative` as above.  Workspace:
+ * pcr_knn_workspace_size(b, n, n). */
 pcr_status pcr_knn_local_ppf(const float *xyz, const float *normals, int b, int n, int k,
-                             int relative, int *idx, float *dist, float *ppf, void *stream);
+                             int relative, int *idx, float *dist, float *ppf, void *workspace,
+                             size_t workspace_bytes, void *stream);
 
 /* ------------------------------------------------ ball query / grouping --
  * ball_query (ball_query/ball_query.cpp:6-30, kernel ball_query.cu:19-50):

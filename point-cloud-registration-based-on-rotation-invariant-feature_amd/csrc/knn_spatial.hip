@@ -1,0 +1,392 @@
+// knn_spatial.hip -- exact k-nearest-neighbour search with spatial pruning,
+// for gfx950.  Same results as knn/knn.cu:5-49 of the reference (k
+// lexicographically smallest (squared distance, index) pairs with distance
+// < 10000, squared distance with the reference's FMA contraction, unfilled
+// slots (10000, 0)), but sub-quadratic in practice:
+//
+//  1. knn_sort_kernel -- one workgroup per (cloud, point set): 30-bit Morton
+//     code of every point in the cloud's bounding box, LDS bitonic sort of
+//     (code, index), then the sorted SoA coordinates + original indices and
+//     the axis-aligned box of every 64-point block.
+//  2. knn_block_kernel -- one wave per 64 consecutive (Morton-sorted) queries,
+//     top-k per lane in registers as a lexicographically sorted array.
+//     Candidate blocks are visited outward from the wave's own block; a block
+//     is skipped when, for every lane, the squared distance to its box
+//     (computed with the same rounding chain, hence a true lower bound of
+//     every candidate distance inside) exceeds the lane's current k-th
+//     distance.  Candidates of a processed block are loaded once (coalesced,
+//     one per lane) and broadcast with v_readlane.  Because the array is kept
+//     in (d, index) order, the visiting order cannot change the result.
+#include "common.hpp"
+
+namespace pcr {
+
+constexpr int kSortThreads = 512;
+constexpr int kKnnMaxSortN = 4096;
+constexpr int kBlk = 64;
+
+struct KnnSet {
+  float* x;   // [b][npad] sorted coordinates (NaN padding)
+  float* y;
+  float* z;
+  int* j;     // [b][npad] original index (-1 padding)
+  float* box; // [b][nblk][8] min xyz, max xyz, -, -
+  int n, npad, nblk;
+};
+
+static inline size_t al256(size_t v) { return (v + 255) / 256 * 256; }
+
+static size_t knn_set_layout(int b, int n, KnnSet* s, char* base, size_t off) {
+  const int nblk = (n + kBlk - 1) / kBlk;
+  const int npad = nblk * kBlk;
+  auto take = [&](size_t bytes) {
+    char* q = base ? base + off : nullptr;
+    off = al256(off + bytes);
+    return q;
+  };
+  float* x = (float*)take((size_t)b * npad * 4);
+  float* y = (float*)take((size_t)b * npad * 4);
+  float* z = (float*)take((size_t)b * npad * 4);
+  int* j = (int*)take((size_t)b * npad * 4);
+  float* box = (float*)take((size_t)b * nblk * 8 * 4);
+  if (s) {
+    s->x = x;
+    s->y = y;
+    s->z = z;
+    s->j = j;
+    s->box = box;
+    s->n = n;
+    s->npad = npad;
+    s->nblk = nblk;
+  }
+  return off;
+}
+
+__device__ inline unsigned spread10(unsigned v) {
+  v &= 0x3FFu;
+  v = (v | (v << 16)) & 0x030000FFu;
+  v = (v | (v << 8)) & 0x0300F00Fu;
+  v = (v | (v << 4)) & 0x030C30C3u;
+  v = (v | (v << 2)) & 0x09249249u;
+  return v;
+}
+
+__device__ inline unsigned quant10(float v, float lo, float scale) {
+  float t = (v - lo) * scale;
+  if (!(t > 0.0f)) return 0u;  // also NaN
+  if (t >= 1023.0f) return 1023u;
+  return (unsigned)t;
+}
+
+__global__ __launch_bounds__(kSortThreads) void knn_sort_kernel(const float* __restrict__ pts,
+                                                                int n, int npad_sort, KnnSet s) {
+  extern __shared__ __align__(16) unsigned long long keys[];  // [npad_sort]
+  __shared__ float red[6][kSortThreads / kWave];
+  __shared__ float frame[6];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const float* P = pts + (size_t)b * 3 * n;
+  // bounding box (NaN-ignoring)
+  float mn[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
+  float mx[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
+  for (int i = tid; i < n; i += kSortThreads) {
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+      const float v = P[(size_t)a * n + i];
+      mn[a] = fminf(mn[a], v);
+      mx[a] = fmaxf(mx[a], v);
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < 3; a++) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      mn[a] = fminf(mn[a], __shfl_xor(mn[a], off, kWave));
+      mx[a] = fmaxf(mx[a], __shfl_xor(mx[a], off, kWave));
+    }
+  }
+  if ((tid & 63) == 0) {
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+      red[a][tid >> 6] = mn[a];
+      red[3 + a][tid >> 6] = mx[a];
+    }
+  }
+  __syncthreads();
+  if (tid < 6) {
+    float v = red[tid][0];
+    for (int w = 1; w < kSortThreads / kWave; w++)
+      v = tid < 3 ? fminf(v, red[tid][w]) : fmaxf(v, red[tid][w]);
+    frame[tid] = v;
+  }
+  __syncthreads();
+  float lo[3], sc[3];
+#pragma unroll
+  for (int a = 0; a < 3; a++) {
+    lo[a] = frame[a];
+    const float ext = frame[3 + a] - frame[a];
+    sc[a] = (ext > 0.0f && ext < __builtin_inff()) ? 1023.0f / ext : 0.0f;
+  }
+  for (int i = tid; i < npad_sort; i += kSortThreads) {
+    unsigned long long key = ~0ull;
+    if (i < n) {
+      const unsigned code = spread10(quant10(P[i], lo[0], sc[0])) |
+                            (spread10(quant10(P[n + i], lo[1], sc[1])) << 1) |
+                            (spread10(quant10(P[2 * n + i], lo[2], sc[2])) << 2);
+      key = ((unsigned long long)code << 32) | (unsigned)i;
+    }
+    keys[i] = key;
+  }
+  __syncthreads();
+  for (int k = 2; k <= npad_sort; k <<= 1) {
+    for (int jj = k >> 1; jj > 0; jj >>= 1) {
+      for (int t = tid; t < (npad_sort >> 1); t += kSortThreads) {
+        const int i = 2 * jj * (t / jj) + (t % jj);
+        const int l = i + jj;
+        const unsigned long long a = keys[i], c = keys[l];
+        if ((a > c) == ((i & k) == 0)) {
+          keys[i] = c;
+          keys[l] = a;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // sorted SoA + per-block boxes (one wave per block)
+  const size_t base = (size_t)b * s.npad;
+  const int lane = tid & 63;
+  for (int blk = tid >> 6; blk < s.nblk; blk += kSortThreads / kWave) {
+    const int p = blk * kBlk + lane;
+    float x = __builtin_nanf(""), y = x, z = x;
+    int j = -1;
+    if (p < n) {
+      j = (int)(unsigned)(keys[p] & 0xFFFFFFFFull);
+      x = P[j];
+      y = P[n + j];
+      z = P[2 * n + j];
+    }
+    s.x[base + p] = x;
+    s.y[base + p] = y;
+    s.z[base + p] = z;
+    s.j[base + p] = j;
+    float bmn[3] = {x, y, z}, bmx[3] = {x, y, z};
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+      if (p >= n || bmn[a] != bmn[a]) {
+        bmn[a] = __builtin_inff();
+        bmx[a] = -__builtin_inff();
+      }
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        bmn[a] = fminf(bmn[a], __shfl_xor(bmn[a], off, kWave));
+        bmx[a] = fmaxf(bmx[a], __shfl_xor(bmx[a], off, kWave));
+      }
+    }
+    if (lane < 8) {
+      float v = 0.0f;
+      if (lane < 3) v = bmn[lane == 0 ? 0 : (lane == 1 ? 1 : 2)];
+      else if (lane < 6) v = bmx[lane == 3 ? 0 : (lane == 4 ? 1 : 2)];
+      s.box[((size_t)b * s.nblk + blk) * 8 + lane] = v;
+    }
+  }
+}
+
+// Lexicographic top-k in registers; valid region is the last k slots (the
+// first KMAX-k hold -inf and are never displaced).
+template <int KMAX>
+struct TopKLex {
+  float d[KMAX];
+  int j[KMAX];
+  __device__ void init(int k) {
+#pragma unroll
+    for (int q = 0; q < KMAX; q++) {
+      d[q] = (q < KMAX - k) ? -__builtin_inff() : PCR_KNN_UNDEF;
+      j[q] = 0;
+    }
+  }
+  __device__ bool qualifies(float x, int jx) const {
+    return (x < d[KMAX - 1]) || (x == d[KMAX - 1] && jx < j[KMAX - 1]);
+  }
+  // carry-chain insertion; from the insertion slot on every element shifts
+  __device__ void insert(float x, int jx) {
+    bool ins = false;
+#pragma unroll
+    for (int q = 0; q < KMAX; q++) {
+      const bool lt = ins || (x < d[q]) || (x == d[q] && jx < j[q]);
+      const float nd = lt ? x : d[q];
+      const int nj = lt ? jx : j[q];
+      x = lt ? d[q] : x;
+      jx = lt ? j[q] : jx;
+      d[q] = nd;
+      j[q] = nj;
+      ins = lt;
+    }
+  }
+};
+
+__device__ inline float readlane_f(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+// Lower bound of the FMA-chain squared distance from q to any point of box.
+__device__ inline float box_lb(float qx, float qy, float qz, const float* bx) {
+  const float gx = qx < bx[0] ? bx[0] - qx : (qx > bx[3] ? qx - bx[3] : 0.0f);
+  const float gy = qy < bx[1] ? bx[1] - qy : (qy > bx[4] ? qy - bx[4] : 0.0f);
+  const float gz = qz < bx[2] ? bx[2] - qz : (qz > bx[5] ? qz - bx[5] : 0.0f);
+  float d = gx * gx;
+  d = __builtin_fmaf(gy, gy, d);
+  d = __builtin_fmaf(gz, gz, d);
+  return d;
+}
+
+template <int KMAX, bool PPF>
+__global__ __launch_bounds__(256) void knn_block_kernel(
+    KnnSet qs, KnnSet cs, int k, float* __restrict__ dist, int* __restrict__ idx,
+    // fused local PPF: original candidate coords/normals and query normals
+    const float* __restrict__ qxyz, const float* __restrict__ qnrm,
+    const float* __restrict__ cxyz, const float* __restrict__ cnrm, int relative,
+    float* __restrict__ ppf) {
+  const int b = blockIdx.y;
+  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (wave >= qs.nblk) return;  // wave-uniform
+  const size_t qb = (size_t)b * qs.npad + (size_t)wave * kBlk + lane;
+  const float qx = qs.x[qb], qy = qs.y[qb], qz = qs.z[qb];
+  const int qj = qs.j[qb];
+  TopKLex<KMAX> top;
+  top.init(k);
+  const float* boxes = cs.box + (size_t)b * cs.nblk * 8;
+  const size_t cbase = (size_t)b * cs.npad;
+  // home block: same relative position in the candidate Morton order
+  int home = (int)(((long long)wave * cs.nblk) / qs.nblk);
+  if (home >= cs.nblk) home = cs.nblk - 1;
+  for (int step = 0; step < 2 * cs.nblk; step++) {
+    const int off = (step + 1) >> 1;
+    const int blk = (step & 1) ? home + off : home - off;
+    if (blk < 0 || blk >= cs.nblk) {
+      if (home - off < 0 && home + off >= cs.nblk) break;
+      continue;
+    }
+    const float* bx = boxes + (size_t)blk * 8;
+    const float lb = box_lb(qx, qy, qz, bx);
+    const float thr = top.d[KMAX - 1];
+    if (!__any(lb <= thr)) continue;  // no lane can gain from this block
+    const size_t cp = cbase + (size_t)blk * kBlk + lane;
+    const float cx = cs.x[cp], cy = cs.y[cp], cz = cs.z[cp];
+    const int cj = cs.j[cp];
+#pragma unroll 2
+    for (int t = 0; t < kBlk; t++) {
+      const float sx = readlane_f(cx, t), sy = readlane_f(cy, t), sz = readlane_f(cz, t);
+      const int sj = __builtin_amdgcn_readlane(cj, t);
+      const float a = qx - sx, bb = qy - sy, cc = qz - sz;
+      float d = a * a;
+      d = __builtin_fmaf(bb, bb, d);
+      d = __builtin_fmaf(cc, cc, d);
+      if (__any(top.qualifies(d, sj))) top.insert(d, sj);
+    }
+  }
+  if (qj < 0) return;
+  const int n = qs.n;
+  const int base = KMAX - k;
+#pragma unroll
+  for (int s = 0; s < KMAX; s++) {
+    if (s >= base) {
+      const size_t o = ((size_t)b * k + (s - base)) * n + qj;
+      if (dist) dist[o] = top.d[s];
+      idx[o] = top.j[s];
+    }
+  }
+  if (PPF) {
+    const int m = cs.n;
+    const float* cb = cxyz + (size_t)b * 3 * m;
+    const float* nb = cnrm + (size_t)b * 3 * m;
+    const float* qn = qnrm + (size_t)b * 3 * n;
+    const float* qo = qxyz + (size_t)b * 3 * n;
+    const float ox = qo[qj], oy = qo[qj + n], oz = qo[qj + 2 * n];
+    const float cnx = qn[qj], cny = qn[qj + n], cnz = qn[qj + 2 * n];
+#pragma unroll 1
+    for (int slot = 0; slot < k; slot++) {
+      const int jn = idx[((size_t)b * k + slot) * n + qj];
+      float o[4];
+      pcr_local_ppf(ox, oy, oz, cnx, cny, cnz, cb[jn], cb[jn + m], cb[jn + 2 * m], nb[jn],
+                    nb[jn + m], nb[jn + 2 * m], relative, o);
+#pragma unroll
+      for (int ch = 0; ch < 4; ch++) ppf[(((size_t)b * 4 + ch) * k + slot) * n + qj] = o[ch];
+    }
+  }
+}
+
+size_t knn_ws_size(int b, int n, int m) {
+  size_t off = knn_set_layout(b, n, nullptr, nullptr, 0);
+  return knn_set_layout(b, m, nullptr, nullptr, off);
+}
+
+static int next_pow2i(int v) {
+  int p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+
+static void launch_sort(const float* pts, int b, int n, const KnnSet& s, hipStream_t st) {
+  const int npad_sort = next_pow2i(n < 2 ? 2 : n);
+  const size_t smem = (size_t)npad_sort * 8;
+  allow_big_lds(knn_sort_kernel, smem);
+  hipLaunchKernelGGL(knn_sort_kernel, dim3(b), dim3(kSortThreads), smem, st, pts, n, npad_sort,
+                     s);
+}
+
+template <bool PPF>
+static pcr_status launch_block(const KnnSet& qs, const KnnSet& cs, int b, int k, float* dist,
+                               int* idx, const float* qxyz, const float* qnrm, const float* cxyz,
+                               const float* cnrm, int relative, float* ppf, hipStream_t st) {
+  dim3 grid(ceil_div(qs.nblk, 4), b);
+#define PCR_KB(KM)                                                                        \
+  hipLaunchKernelGGL((knn_block_kernel<KM, PPF>), grid, dim3(256), 0, st, qs, cs, k, dist, idx, \
+                     qxyz, qnrm, cxyz, cnrm, relative, ppf)
+  if (k <= 16)
+    PCR_KB(16);
+  else if (k <= 32)
+    PCR_KB(32);
+  else if (k <= 64)
+    PCR_KB(64);
+  else if (k <= 128)
+    PCR_KB(128);
+  else
+    return PCR_ERR_UNSUPPORTED;
+#undef PCR_KB
+  return PCR_OK;
+}
+
+// Returns PCR_ERR_UNSUPPORTED (nothing launched) when the spatial path does
+// not apply; the caller then uses the brute-force kernels.
+pcr_status knn_spatial(const float* xyz1, const float* xyz2, int b, int n, int m, int k,
+                       float* dist1, int* idx1, float* dist2, int* idx2, const float* nrm1,
+                       const float* nrm2, int relative, float* ppf1, void* ws, size_t ws_bytes,
+                       bool self, hipStream_t st) {
+  if (ws == nullptr || n > kKnnMaxSortN || m > kKnnMaxSortN || n < 1 || m < 1 || k > 128)
+    return PCR_ERR_UNSUPPORTED;
+  if (ws_bytes < knn_ws_size(b, n, m)) return PCR_ERR_UNSUPPORTED;
+  KnnSet s1, s2;
+  size_t off = knn_set_layout(b, n, &s1, (char*)ws, 0);
+  knn_set_layout(b, m, &s2, (char*)ws, off);
+  launch_sort(xyz1, b, n, s1, st);
+  if (!self) launch_sort(xyz2, b, m, s2, st);
+  const KnnSet& c1 = self ? s1 : s2;
+  pcr_status rc;
+  if (ppf1)
+    rc = launch_block<true>(s1, c1, b, k, dist1, idx1, xyz1, nrm1, xyz2, nrm2, relative, ppf1, st);
+  else
+    rc = launch_block<false>(s1, c1, b, k, dist1, idx1, nullptr, nullptr, nullptr, nullptr, 0,
+                             nullptr, st);
+  if (rc != PCR_OK) return rc;
+  if (idx2) rc = launch_block<false>(c1, s1, b, k, dist2, idx2, nullptr, nullptr, nullptr, nullptr,
+                                     0, nullptr, st);
+  return rc;
+}
+
+}  // namespace pcr
+
+extern "C" size_t pcr_knn_workspace_size(int b, int n, int m) {
+  if (b <= 0 || n <= 0 || m <= 0) return 256;
+  return pcr::knn_ws_size(b, n, m);
+}

@@ -39,20 +39,24 @@ struct TopK {
     }
   }
   __device__ float thr() const { return d[KMAX - 1]; }
-  // Insertion as a compare-exchange carry chain: the carried element moves
-  // past every slot it is not strictly smaller than, so equal distances keep
-  // the earlier (lower) index first.  Each lane mask dies immediately (no
-  // SGPR pressure), and a non-qualifying x (>= D[KMAX-1], or NaN) falls off.
+  // Insertion as a compare-exchange carry chain: the new element passes every
+  // slot it is not strictly smaller than (equal distances keep the earlier,
+  // lower index first); from its slot on, every element shifts by one
+  // (`ins`), so equal displaced elements keep their order.  A non-qualifying
+  // x (>= D[KMAX-1], or NaN) falls off the end unchanged.  Lane masks are
+  // short-lived (no SGPR pressure, unlike a hoisted compare-all form).
   __device__ void insert(float x, int jx) {
+    bool ins = false;
 #pragma unroll
     for (int q = 0; q < KMAX; q++) {
-      const bool lt = x < d[q];
+      const bool lt = ins || (x < d[q]);
       const float nd = lt ? x : d[q];
       const int nj = lt ? jx : j[q];
       x = lt ? d[q] : x;
       jx = lt ? j[q] : jx;
       d[q] = nd;
       j[q] = nj;
+      ins = lt;
     }
   }
 };
@@ -390,10 +394,16 @@ using namespace pcr;
 
 extern "C" pcr_status pcr_knn_forward(const float* xyz1, const float* xyz2, int b, int c, int n,
                                       int m, int k, float* dist1, float* dist2, int* idx1,
-                                      int* idx2, void* stream) {
+                                      int* idx2, void* workspace, size_t workspace_bytes,
+                                      void* stream) {
   PCR_REQUIRE(b >= 0 && c >= 1 && n >= 0 && m >= 0 && k >= 1, "knn_forward: invalid sizes");
+  PCR_REQUIRE(dist1 && dist2 && idx1 && idx2, "knn_forward: all four outputs required");
   if (b == 0) return PCR_OK;
   hipStream_t st = as_stream(stream);
+  if (c == 3 && n > 0 && m > 0 &&
+      knn_spatial(xyz1, xyz2, b, n, m, k, dist1, idx1, dist2, idx2, nullptr, nullptr, 0, nullptr,
+                  workspace, workspace_bytes, xyz1 == xyz2 && n == m, st) == PCR_OK)
+    return launch_status("knn_forward");
   if (c <= kMaxC && k <= 128) {
     if (n > 0) launch_knn<false>(xyz1, xyz2, b, c, n, m, k, dist1, idx1, nullptr, 0, nullptr, st);
     if (m > 0) launch_knn<false>(xyz2, xyz1, b, c, m, n, k, dist2, idx2, nullptr, 0, nullptr, st);
@@ -430,10 +440,13 @@ extern "C" pcr_status pcr_knn_backward(const float* xyz1, const float* xyz2,
 
 extern "C" pcr_status pcr_knn_local_ppf(const float* xyz, const float* normals, int b, int n,
                                         int k, int relative, int* idx, float* dist, float* ppf,
-                                        void* stream) {
+                                        void* workspace, size_t workspace_bytes, void* stream) {
   PCR_REQUIRE(b >= 0 && n >= 1 && k >= 1 && k <= 128, "knn_local_ppf: invalid sizes (k<=128)");
   PCR_REQUIRE(ppf != nullptr && idx != nullptr, "knn_local_ppf: idx and ppf outputs required");
   if (b == 0) return PCR_OK;
+  if (knn_spatial(xyz, xyz, b, n, n, k, dist, idx, nullptr, nullptr, normals, normals, relative,
+                  ppf, workspace, workspace_bytes, true, as_stream(stream)) == PCR_OK)
+    return launch_status("knn_local_ppf");
   launch_knn<true>(xyz, xyz, b, 3, n, n, k, dist, idx, normals, relative, ppf, as_stream(stream));
   return launch_status("knn_local_ppf");
 }

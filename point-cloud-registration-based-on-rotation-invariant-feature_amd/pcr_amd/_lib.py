@@ -22,11 +22,12 @@ ST = ctypes.c_int
 SIGNATURES = {
     "pcr_last_error": (ctypes.c_char_p, []),
     "pcr_version": (ctypes.c_char_p, []),
-    "pcr_knn_forward": (ST, [P, P, I, I, I, I, I, P, P, P, P, P]),
+    "pcr_knn_forward": (ST, [P, P, I, I, I, I, I, P, P, P, P, P, SZ, P]),
+    "pcr_knn_workspace_size": (SZ, [I, I, I]),
     "pcr_knn_backward": (ST, [P, P, P, P, P, P, I, I, I, I, I, P, P, P]),
     "pcr_spherical_ppf_forward": (ST, [P, P, P, P, I, I, P, P]),
     "pcr_local_ppf_forward": (ST, [P, P, P, P, P, I, I, I, I, I, I, P, P]),
-    "pcr_knn_local_ppf": (ST, [P, P, I, I, I, I, P, P, P, P]),
+    "pcr_knn_local_ppf": (ST, [P, P, I, I, I, I, P, P, P, P, SZ, P]),
     "pcr_ball_query": (ST, [P, P, I, I, I, F, I, P, P]),
     "pcr_grouping_forward": (ST, [P, P, I, I, I, I, I, P, P]),
     "pcr_grouping_backward": (ST, [P, P, I, I, I, I, I, P, P]),

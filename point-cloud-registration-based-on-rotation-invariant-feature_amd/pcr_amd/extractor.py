@@ -45,6 +45,8 @@ class SphExtractor:
         lib = _lib.load()
         self.ws = e(max(256, lib.pcr_extractor_workspace_size(b, n, c, r)), dtype=torch.uint8,
                     device=dev)
+        self.knn_ws = e(max(256, lib.pcr_knn_workspace_size(b, n, n)), dtype=torch.uint8,
+                        device=dev)
         self.s_nbr = torch.cuda.Stream(device=dev)
         self.s_vox = torch.cuda.Stream(device=dev)
         self.graph = None
@@ -54,8 +56,8 @@ class SphExtractor:
     def neighbor_stage(self, xyz, normals, stream):
         _lib.check(_lib.load().pcr_knn_local_ppf(
             _ptr(xyz), _ptr(normals), self.b, self.n, self.k, int(self.relative),
-            _ptr(self.knn_idx), _ptr(self.knn_dist), _ptr(self.local_ppf), stream),
-            "knn_local_ppf")
+            _ptr(self.knn_idx), _ptr(self.knn_dist), _ptr(self.local_ppf), _ptr(self.knn_ws),
+            self.knn_ws.numel(), stream), "knn_local_ppf")
 
     def voxel_stage(self, xyz, features, stream):
         _lib.check(_lib.load().pcr_extractor_voxel_stage(

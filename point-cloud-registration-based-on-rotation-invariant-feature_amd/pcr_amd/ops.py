@@ -69,9 +69,11 @@ def knn_forward_cuda(xyz1, xyz2, k):
     dist2 = torch.empty((b, k, m), dtype=torch.float32, device=dev)
     idx1 = torch.empty((b, k, n), dtype=torch.int32, device=dev)
     idx2 = torch.empty((b, k, m), dtype=torch.int32, device=dev)
-    _lib.check(_lib.load().pcr_knn_forward(
+    lib = _lib.load()
+    ws = _workspace(lib.pcr_knn_workspace_size(b, n, m), dev)
+    _lib.check(lib.pcr_knn_forward(
         _ptr(xyz1), _ptr(xyz2), b, c, n, m, k, _ptr(dist1), _ptr(dist2), _ptr(idx1), _ptr(idx2),
-        _stream()), "knn_forward_cuda")
+        _ptr(ws), ws.numel(), _stream()), "knn_forward_cuda")
     return [dist1, dist2, idx1, idx2]
 
 
@@ -135,9 +137,11 @@ def knn_local_ppf(xyz, normals, k, relative=True, want_dist=False):
     idx = torch.empty((b, k, n), dtype=torch.int32, device=dev)
     ppf = torch.empty((b, 4, k, n), dtype=torch.float32, device=dev)
     dist = torch.empty((b, k, n), dtype=torch.float32, device=dev) if want_dist else None
-    _lib.check(_lib.load().pcr_knn_local_ppf(
+    lib = _lib.load()
+    ws = _workspace(lib.pcr_knn_workspace_size(b, n, n), dev)
+    _lib.check(lib.pcr_knn_local_ppf(
         _ptr(xyz), _ptr(normals), b, n, int(k), int(bool(relative)), _ptr(idx), _ptr(dist),
-        _ptr(ppf), _stream()), "knn_local_ppf")
+        _ptr(ppf), _ptr(ws), ws.numel(), _stream()), "knn_local_ppf")
     return idx, ppf, dist
 
 
