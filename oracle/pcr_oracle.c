@@ -428,29 +428,41 @@ void orc_local_ppf(int b, int n, int m, int u, const float *pts, const float *nr
 
 /* ------------------------------------------- deterministic normalisation */
 /* Spherical_Voxelization.forward (modules/spherical_vox.py:16-20) restated
- * with a fixed reduction order, the order the fused GPU extractor uses: the
- * per-axis mean is accumulated in double, 256 strided partial sums then a
- * halving tree; max of per-point fp32 norms; nc / (max + 1e-20f). */
-#define PCR_NORM_LANES 256
+ * with a fixed reduction order, the order the GPU prep kernel uses: the
+ * per-axis mean is accumulated in double -- lane t of 1024 sums points
+ * t, t+1024, ... ascending; each group of 64 lanes is halved
+ * (l += l+s for s = 32..1); the 16 group sums are halved the same way --
+ * then max of per-point fp32 norms, then nc / (max + 1e-20f). */
+#define PCR_NORM_LANES 1024
+static float cloud_mean_axis(const float *x, int n) {
+  double part[PCR_NORM_LANES], grp[PCR_NORM_LANES / 64];
+  int t, s, g;
+  for (t = 0; t < PCR_NORM_LANES; t++) {
+    double acc = 0.0;
+    int i;
+    for (i = t; i < n; i += PCR_NORM_LANES) acc += (double)x[i];
+    part[t] = acc;
+  }
+  for (g = 0; g < PCR_NORM_LANES / 64; g++) {
+    double *w = part + 64 * g;
+    for (s = 32; s > 0; s >>= 1)
+      for (t = 0; t < s; t++) w[t] += w[t + s];
+    grp[g] = w[0];
+  }
+  for (s = 8; s > 0; s >>= 1)
+    for (t = 0; t < s; t++) grp[t] += grp[t + s];
+  return (float)(grp[0] / (double)n);
+}
+
 void orc_normalize_sph(int b, int n, const float *coords, float *norm_coords) {
   int bi;
 #pragma omp parallel for
   for (bi = 0; bi < b; bi++) {
     const float *x = coords + (size_t)bi * 3 * n;
     float *o = norm_coords + (size_t)bi * 3 * n;
-    double part[PCR_NORM_LANES];
     float mean[3], maxn = 0.0f, denom;
-    int a, t, s, i;
-    for (a = 0; a < 3; a++) {
-      for (t = 0; t < PCR_NORM_LANES; t++) {
-        double acc = 0.0;
-        for (i = t; i < n; i += PCR_NORM_LANES) acc += (double)x[(size_t)a * n + i];
-        part[t] = acc;
-      }
-      for (s = PCR_NORM_LANES / 2; s > 0; s >>= 1)
-        for (t = 0; t < s; t++) part[t] += part[t + s];
-      mean[a] = (float)(part[0] / (double)n);
-    }
+    int a, i;
+    for (a = 0; a < 3; a++) mean[a] = cloud_mean_axis(x + (size_t)a * n, n);
     for (i = 0; i < n; i++) {
       float cx = x[i] - mean[0], cy = x[i + n] - mean[1], cz = x[i + 2 * n] - mean[2];
       float nn = __builtin_sqrtf(pcr_sumsq3f(cx, cy, cz));

@@ -191,38 +191,81 @@ __global__ __launch_bounds__(kSortThreads) void knn_sort_kernel(const float* __r
   }
 }
 
-// Lexicographic top-k in registers; valid region is the last k slots (the
-// first KMAX-k hold -inf and are never displaced).
+// Top-k in registers as packed keys (float bits of the squared distance << 32
+// | index).  Squared distances are >= +0 or NaN, so unsigned key order is the
+// lexicographic (distance, index) order and NaN sorts above the 10000
+// sentinel (never kept, as in the reference).  Valid region = the last k
+// slots; the first KMAX-k hold key 0 and are never displaced.
 template <int KMAX>
-struct TopKLex {
-  float d[KMAX];
-  int j[KMAX];
+struct TopKKey {
+  unsigned long long key[KMAX];
   __device__ void init(int k) {
+    const unsigned long long undef = (unsigned long long)__float_as_uint(PCR_KNN_UNDEF) << 32;
 #pragma unroll
-    for (int q = 0; q < KMAX; q++) {
-      d[q] = (q < KMAX - k) ? -__builtin_inff() : PCR_KNN_UNDEF;
-      j[q] = 0;
-    }
+    for (int q = 0; q < KMAX; q++) key[q] = (q < KMAX - k) ? 0ull : undef;
   }
-  __device__ bool qualifies(float x, int jx) const {
-    return (x < d[KMAX - 1]) || (x == d[KMAX - 1] && jx < j[KMAX - 1]);
-  }
-  // carry-chain insertion; from the insertion slot on every element shifts
-  __device__ void insert(float x, int jx) {
-    bool ins = false;
+  __device__ bool qualifies(unsigned long long x) const { return x < key[KMAX - 1]; }
+  __device__ float kth() const { return __uint_as_float((unsigned)(key[KMAX - 1] >> 32)); }
+  // Insert x into the sorted array, dropping the largest:
+  // new[q] = min(old[q], max(old[q-1], x)).  Every slot depends only on the
+  // old array, so the update has full instruction-level parallelism (the
+  // carry-chain form is a 32-deep dependent chain) and each lane mask dies
+  // right after its select.  A non-qualifying x leaves the array unchanged.
+  __device__ void insert(unsigned long long x) {
 #pragma unroll
-    for (int q = 0; q < KMAX; q++) {
-      const bool lt = ins || (x < d[q]) || (x == d[q] && jx < j[q]);
-      const float nd = lt ? x : d[q];
-      const int nj = lt ? jx : j[q];
-      x = lt ? d[q] : x;
-      jx = lt ? j[q] : jx;
-      d[q] = nd;
-      j[q] = nj;
-      ins = lt;
+    for (int q = KMAX - 1; q > 0; q--) {
+      const unsigned long long hi = key[q - 1] > x ? key[q - 1] : x;
+      key[q] = key[q] < hi ? key[q] : hi;
     }
+    key[0] = key[0] < x ? key[0] : x;
   }
 };
+
+__device__ inline unsigned long long make_key(float d, int j) {
+  return ((unsigned long long)__float_as_uint(d) << 32) | (unsigned)j;
+}
+
+__device__ inline void cex_up(unsigned long long& a, unsigned long long& b) {
+  const unsigned long long lo = a < b ? a : b;
+  const unsigned long long hi = a < b ? b : a;
+  a = lo;
+  b = hi;
+}
+
+// Merge a batch of kQ (unsorted) keys into the sorted top-k array: bitonic
+// sort of the batch, C[i] = min(A[i], Q[K-1-i]) (the K smallest of A u Q as
+// a bitonic sequence), then a bitonic merge.  kQ*log2(kQ)^2/4 + kQ +
+// (K/2)*log2(K) compare-exchanges for kQ keys instead of kQ*K selects.
+constexpr int kQ = 16;
+template <int KMAX>
+__device__ inline void merge_batch(unsigned long long (&key)[KMAX], unsigned long long (&q)[kQ]) {
+#pragma unroll
+  for (int kk = 2; kk <= kQ; kk <<= 1) {
+#pragma unroll
+    for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+#pragma unroll
+      for (int i = 0; i < kQ; i++) {
+        const int l = i ^ jj;
+        if (l > i) {
+          if ((i & kk) == 0)
+            cex_up(q[i], q[l]);
+          else
+            cex_up(q[l], q[i]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = KMAX - kQ; i < KMAX; i++) key[i] = key[i] < q[KMAX - 1 - i] ? key[i] : q[KMAX - 1 - i];
+#pragma unroll
+  for (int jj = KMAX >> 1; jj > 0; jj >>= 1) {
+#pragma unroll
+    for (int i = 0; i < KMAX; i++) {
+      const int l = i ^ jj;
+      if (l > i) cex_up(key[i], key[l]);
+    }
+  }
+}
 
 __device__ inline float readlane_f(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
@@ -253,8 +296,19 @@ __global__ __launch_bounds__(256) void knn_block_kernel(
   const size_t qb = (size_t)b * qs.npad + (size_t)wave * kBlk + lane;
   const float qx = qs.x[qb], qy = qs.y[qb], qz = qs.z[qb];
   const int qj = qs.j[qb];
-  TopKLex<KMAX> top;
+  TopKKey<KMAX> top;
   top.init(k);
+  // per-lane batch of qualifying keys, LDS [wave][slot][lane] (conflict-free)
+  __shared__ unsigned long long qbuf[4 * kQ * kBlk];
+  unsigned long long* myq = qbuf + (threadIdx.x >> 6) * kQ * kBlk + lane;
+  int qn = 0;
+  auto flush = [&]() {
+    unsigned long long qv[kQ];
+#pragma unroll
+    for (int s = 0; s < kQ; s++) qv[s] = s < qn ? myq[s * kBlk] : ~0ull;
+    merge_batch<KMAX>(top.key, qv);
+    qn = 0;
+  };
   const float* boxes = cs.box + (size_t)b * cs.nblk * 8;
   const size_t cbase = (size_t)b * cs.npad;
   // home block: same relative position in the candidate Morton order
@@ -269,7 +323,7 @@ __global__ __launch_bounds__(256) void knn_block_kernel(
     }
     const float* bx = boxes + (size_t)blk * 8;
     const float lb = box_lb(qx, qy, qz, bx);
-    const float thr = top.d[KMAX - 1];
+    const float thr = top.kth();
     if (!__any(lb <= thr)) continue;  // no lane can gain from this block
     const size_t cp = cbase + (size_t)blk * kBlk + lane;
     const float cx = cs.x[cp], cy = cs.y[cp], cz = cs.z[cp];
@@ -282,9 +336,17 @@ __global__ __launch_bounds__(256) void knn_block_kernel(
       float d = a * a;
       d = __builtin_fmaf(bb, bb, d);
       d = __builtin_fmaf(cc, cc, d);
-      if (__any(top.qualifies(d, sj))) top.insert(d, sj);
+      const unsigned long long key = make_key(d, sj);
+      // batch against the (stale, hence conservative) k-th key; merge when
+      // any lane's batch is full
+      if (top.qualifies(key)) {
+        myq[qn * kBlk] = key;
+        qn++;
+      }
+      if (__any(qn == kQ)) flush();
     }
   }
+  if (__any(qn > 0)) flush();
   if (qj < 0) return;
   const int n = qs.n;
   const int base = KMAX - k;
@@ -292,8 +354,8 @@ __global__ __launch_bounds__(256) void knn_block_kernel(
   for (int s = 0; s < KMAX; s++) {
     if (s >= base) {
       const size_t o = ((size_t)b * k + (s - base)) * n + qj;
-      if (dist) dist[o] = top.d[s];
-      idx[o] = top.j[s];
+      if (dist) dist[o] = __uint_as_float((unsigned)(top.key[s] >> 32));
+      idx[o] = (int)(unsigned)(top.key[s] & 0xFFFFFFFFull);
     }
   }
   if (PPF) {

@@ -28,7 +28,7 @@
 
 namespace pcr {
 
-constexpr int kPrepThreads = 512;
+constexpr int kPrepThreads = 1024;
 constexpr int kMaxSortN = 4096;
 constexpr int kGridThreads = 256;
 constexpr int kMaxG = 8;
@@ -82,6 +82,128 @@ static inline int next_pow2(int v) {
 }
 
 // ------------------------------------------------------------ prep kernel
+// One workgroup of 1024 threads per cloud; thread t owns points t + e*1024.
+// Everything after the initial coalesced loads stays in registers / LDS:
+// fixed-order fp64 mean (cloud_mean), fp32 max norm, voxel index and
+// devox corners, then a bitonic sort of the 64-bit (voxel, point) keys whose
+// stages run in registers (partner in the same thread), with DPP/shuffles
+// (partner in the same wave) or through LDS (other waves) -- 10 barriers for
+// 1024 keys instead of 55.
+constexpr int kMaxE = kMaxSortN / kPrepThreads;
+
+// Fixed-order per-axis mean of a cloud in double, the order the oracle
+// restates (orc_cloud_mean): thread t sums points t, t+1024, ... ascending;
+// each wave halves 64 partials (l += l+s for s = 32..1); the 16 wave sums
+// are halved the same way.  Returns the three means on every thread.
+__device__ inline void cloud_mean(const float (&px)[kMaxE], const float (&py)[kMaxE],
+                                  const float (&pz)[kMaxE], int E, int n, double* red,
+                                  float* mean_out) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  double s[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+  for (int e = 0; e < kMaxE; e++) {
+    if (e < E && e * kPrepThreads + tid < n) {
+      s[0] += (double)px[e];
+      s[1] += (double)py[e];
+      s[2] += (double)pz[e];
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < 3; a++) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const double o = __shfl_down(s[a], off, kWave);
+      if (lane < off) s[a] += o;
+    }
+    if (lane == 0) red[a * 16 + w] = s[a];
+  }
+  __syncthreads();
+  if (tid < 3) {
+    double v[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) v[i] = red[tid * 16 + i];
+#pragma unroll
+    for (int off = 8; off > 0; off >>= 1)
+#pragma unroll
+      for (int i = 0; i < off; i++) v[i] += v[i + off];
+    mean_out[tid] = (float)(v[0] / (double)n);
+  }
+  __syncthreads();
+}
+
+__device__ inline unsigned long long shfl_xor_u64(unsigned long long v, int m) {
+  const int lo = __shfl_xor((int)(unsigned)(v & 0xFFFFFFFFull), m, kWave);
+  const int hi = __shfl_xor((int)(unsigned)(v >> 32), m, kWave);
+  return ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
+}
+
+// Ascending bitonic sort of E*1024 keys, element (e, tid) at index e*1024+tid.
+__device__ inline void block_bitonic(unsigned long long (&v)[kMaxE], int E,
+                                     unsigned long long* lds) {
+  const int tid = threadIdx.x;
+  const int npad = E * kPrepThreads;
+  for (int kk = 2; kk <= npad; kk <<= 1) {
+    int j = kk >> 1;
+    // partner in another register of this thread
+    for (; j >= kPrepThreads; j >>= 1) {
+      const int je = j / kPrepThreads;
+#pragma unroll
+      for (int e = 0; e < kMaxE; e++) {
+        const int pe = e ^ je;
+        if (e < E && pe > e) {
+          const int i = e * kPrepThreads + tid;
+          const bool up = (i & kk) == 0;
+          const unsigned long long a = v[e], b = v[pe];
+          if ((a > b) == up) {
+            v[e] = b;
+            v[pe] = a;
+          }
+        }
+      }
+    }
+    // partner in another wave: through LDS
+    if (j >= kWave) {
+#pragma unroll
+      for (int e = 0; e < kMaxE; e++)
+        if (e < E) lds[e * kPrepThreads + tid] = v[e];
+      __syncthreads();
+      for (; j >= kWave; j >>= 1) {
+        for (int t = tid; t < (npad >> 1); t += kPrepThreads) {
+          const int i = 2 * j * (t / j) + (t % j);
+          const int l = i + j;
+          const unsigned long long a = lds[i], b = lds[l];
+          if ((a > b) == ((i & kk) == 0)) {
+            lds[i] = b;
+            lds[l] = a;
+          }
+        }
+        __syncthreads();
+      }
+#pragma unroll
+      for (int e = 0; e < kMaxE; e++)
+        if (e < E) v[e] = lds[e * kPrepThreads + tid];
+      __syncthreads();
+    }
+    // partner in the same wave: cross-lane exchange
+    for (; j > 0; j >>= 1) {
+#pragma unroll
+      for (int e = 0; e < kMaxE; e++) {
+        if (e < E) {
+          const int i = e * kPrepThreads + tid;
+          const unsigned long long o = shfl_xor_u64(v[e], j);
+          const bool lower = (i & j) == 0;
+          const bool up = (i & kk) == 0;
+          // lower element keeps min when ascending, max when descending
+          const bool take_min = (lower == up);
+          const unsigned long long mn = v[e] < o ? v[e] : o;
+          const unsigned long long mx = v[e] < o ? o : v[e];
+          v[e] = take_min ? mn : mx;
+        }
+      }
+    }
+  }
+}
+
 template <int MODE>
 __global__ __launch_bounds__(kPrepThreads) void vox_prep_kernel(
     const float* __restrict__ coords_f, const int* __restrict__ coords_i, int n, int r, int npad,
@@ -91,41 +213,53 @@ __global__ __launch_bounds__(kPrepThreads) void vox_prep_kernel(
   unsigned long long* keys = (unsigned long long*)smem_raw;  // [npad]
   unsigned* bm = (unsigned*)(keys + npad);                     // [W]
   __shared__ int scan_s[kPrepThreads / kWave + 1];
-  __shared__ double part[256];
+  __shared__ double red[48];
   __shared__ float s_stat[4];
 
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
-  const int nt = blockDim.x;
+  const int nt = kPrepThreads;
   const int r3 = r * r * r;
   const int W = ws.W;
+  const int E = npad / kPrepThreads;
 
-  float mean0 = 0.f, mean1 = 0.f, mean2 = 0.f, denom = 1.f;
-  if (MODE == kSphNormalize) {
-    const float* x = coords_f + (size_t)b * 3 * n;
-    // per-axis mean in double, fixed order (oracle orc_normalize_sph)
-    for (int a = 0; a < 3; a++) {
-      if (tid < 256) {
-        double acc = 0.0;
-        for (int i = tid; i < n; i += 256) acc += (double)x[(size_t)a * n + i];
-        part[tid] = acc;
-      }
-      __syncthreads();
-      for (int s = 128; s > 0; s >>= 1) {
-        if (tid < s) part[tid] += part[tid + s];
-        __syncthreads();
-      }
-      if (tid == 0) s_stat[a] = (float)(part[0] / (double)n);
-      __syncthreads();
+  float px[kMaxE], py[kMaxE], pz[kMaxE];
+  int ci[kMaxE][3];
+  if (MODE == kCube) {
+    const int* x = coords_i + (size_t)b * 3 * n;
+#pragma unroll
+    for (int e = 0; e < kMaxE; e++) {
+      const int i = e * nt + tid;
+      const bool ok = e < E && i < n;
+      ci[e][0] = ok ? x[i] : 0;
+      ci[e][1] = ok ? x[i + n] : 0;
+      ci[e][2] = ok ? x[i + 2 * n] : 0;
     }
-    mean0 = s_stat[0];
-    mean1 = s_stat[1];
-    mean2 = s_stat[2];
+  } else {
+    const float* x = coords_f + (size_t)b * 3 * n;
+#pragma unroll
+    for (int e = 0; e < kMaxE; e++) {
+      const int i = e * nt + tid;
+      const bool ok = e < E && i < n;
+      px[e] = ok ? x[i] : 0.0f;
+      py[e] = ok ? x[i + n] : 0.0f;
+      pz[e] = ok ? x[i + 2 * n] : 0.0f;
+    }
+  }
+  for (int w = tid; w < W; w += nt) bm[w] = 0u;
+
+  if (MODE == kSphNormalize) {
+    cloud_mean(px, py, pz, E, n, red, s_stat);
+    const float m0 = s_stat[0], m1 = s_stat[1], m2 = s_stat[2];
     float mx = 0.0f;
-    for (int i = tid; i < n; i += nt) {
-      float cx = x[i] - mean0, cy = x[i + n] - mean1, cz = x[i + 2 * n] - mean2;
-      float nn = __builtin_sqrtf(pcr_sumsq3f(cx, cy, cz));
-      mx = fmaxf(mx, nn);
+#pragma unroll
+    for (int e = 0; e < kMaxE; e++) {
+      if (e < E && e * nt + tid < n) {
+        px[e] -= m0;
+        py[e] -= m1;
+        pz[e] -= m2;
+        mx = fmaxf(mx, __builtin_sqrtf(pcr_sumsq3f(px[e], py[e], pz[e])));
+      }
     }
     mx = wave_max(mx);
     if ((tid & 63) == 0) scan_s[tid >> 6] = __float_as_int(mx);
@@ -136,103 +270,81 @@ __global__ __launch_bounds__(kPrepThreads) void vox_prep_kernel(
       s_stat[3] = m + 1e-20f;
     }
     __syncthreads();
-    denom = s_stat[3];
+    const float den = s_stat[3];
+#pragma unroll
+    for (int e = 0; e < kMaxE; e++) {
+      px[e] = px[e] / den;
+      py[e] = py[e] / den;
+      pz[e] = pz[e] / den;
+    }
   }
 
-  // 1. voxel index + sort keys
-  for (int i = tid; i < npad; i += nt) {
-    unsigned long long key = ~0ull;
-    if (i < n) {
+  // voxel index, devox corners, sort keys
+  unsigned long long kv[kMaxE];
+#pragma unroll
+  for (int e = 0; e < kMaxE; e++) {
+    kv[e] = ~0ull;
+    const int i = e * nt + tid;
+    if (e < E && i < n) {
       int v;
       bool valid;
       if (MODE == kCube) {
-        const int* x = coords_i + (size_t)b * 3 * n;
-        v = x[i] * r * r + x[i + n] * r + x[i + 2 * n];
+        v = ci[e][0] * r * r + ci[e][1] * r + ci[e][2];
         valid = (v >= 0 && v < r3);
       } else {
-        const float* x = coords_f + (size_t)b * 3 * n;
-        float px = x[i], py = x[i + n], pz = x[i + 2 * n];
-        if (MODE == kSphNormalize) {
-          px = (px - mean0) / denom;
-          py = (py - mean1) / denom;
-          pz = (pz - mean2) / denom;
-          if (norm_out) {
-            float* o = norm_out + (size_t)b * 3 * n;
-            o[i] = px;
-            o[i + n] = py;
-            o[i + 2 * n] = pz;
-          }
+        if (MODE == kSphNormalize && norm_out) {
+          float* o = norm_out + (size_t)b * 3 * n;
+          o[i] = px[e];
+          o[i + n] = py[e];
+          o[i + 2 * n] = pz[e];
         }
-        v = pcr_sph_index(px, py, pz, r);
+        v = pcr_sph_index(px[e], py[e], pz[e], r);
         valid = v >= 0;
         if (MODE == kSphNormalize && dinds) {
-          int ci[8];
+          int cidx[8];
           float cw[8];
           int* I = dinds + (size_t)b * 8 * n;
           float* Wt = dwgts + (size_t)b * 8 * n;
-          if (!valid) {
-            I[i] = -1;
-            for (int q = 1; q < 8; q++) I[i + (size_t)q * n] = 0;
-            for (int q = 0; q < 8; q++) Wt[i + (size_t)q * n] = 0.0f;
-          } else if (pcr_sph_corners(px, py, pz, v, r, ci, cw)) {
-            for (int q = 0; q < 8; q++) {
-              I[i + (size_t)q * n] = ci[q];
-              Wt[i + (size_t)q * n] = cw[q];
-            }
-          } else {
-            for (int q = 0; q < 8; q++) {
-              I[i + (size_t)q * n] = 0;
-              Wt[i + (size_t)q * n] = 0.0f;
-            }
+          const bool ok = valid && pcr_sph_corners(px[e], py[e], pz[e], v, r, cidx, cw);
+#pragma unroll
+          for (int q = 0; q < 8; q++) {
+            I[i + (size_t)q * n] = ok ? cidx[q] : ((q == 0 && !valid) ? -1 : 0);
+            Wt[i + (size_t)q * n] = ok ? cw[q] : 0.0f;
           }
         }
       }
       ind[(size_t)b * n + i] = v;
-      key = ((unsigned long long)(valid ? (unsigned)v : 0xFFFFFFFFu) << 32) | (unsigned)i;
+      kv[e] = ((unsigned long long)(valid ? (unsigned)v : 0xFFFFFFFFu) << 32) | (unsigned)i;
     }
-    keys[i] = key;
   }
-  for (int w = tid; w < W; w += nt) bm[w] = 0u;
+
+  // sort (unique keys: the low word is the point id -> stable by voxel)
+  block_bitonic(kv, E, keys);
+#pragma unroll
+  for (int e = 0; e < kMaxE; e++)
+    if (e < E) keys[e * nt + tid] = kv[e];
   __syncthreads();
 
-  // 2. bitonic sort of unique 64-bit keys (stable by construction: point id
-  //    is the low word)
-  for (int k = 2; k <= npad; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int t = tid; t < (npad >> 1); t += nt) {
-        int i = 2 * j * (t / j) + (t % j);
-        int l = i + j;
-        unsigned long long a = keys[i], c = keys[l];
-        bool up = (i & k) == 0;
-        if ((a > c) == up) {
-          keys[i] = c;
-          keys[l] = a;
-        }
-      }
-      __syncthreads();
-    }
-  }
-
-  // 3. segments: contiguous chunk of sorted positions per thread
+  // segments: contiguous chunk of sorted positions per thread
   const int chunk = (n + nt - 1) / nt;
   const int p0 = min(n, tid * chunk), p1 = min(n, p0 + chunk);
   int local = 0, nvalid_local = 0;
   for (int p = p0; p < p1; p++) {
-    unsigned v = (unsigned)(keys[p] >> 32);
+    const unsigned v = (unsigned)(keys[p] >> 32);
     if (v != 0xFFFFFFFFu) {
       nvalid_local++;
       if (p == 0 || (unsigned)(keys[p - 1] >> 32) != v) local++;
     }
   }
-  int incl = block_inclusive_scan(local, scan_s);
-  int nv_incl = block_inclusive_scan(nvalid_local, scan_s);
+  const int incl = block_inclusive_scan(local, scan_s);
+  const int nv_incl = block_inclusive_scan(nvalid_local, scan_s);
   int s = incl - local;
   int* perm = ws.perm + (size_t)b * n;
   int* seg_off = ws.seg_off + (size_t)b * (n + 1);
   int* seg_vox = ws.seg_vox + (size_t)b * n;
   for (int p = p0; p < p1; p++) {
-    unsigned long long kk = keys[p];
-    unsigned v = (unsigned)(kk >> 32);
+    const unsigned long long kk = keys[p];
+    const unsigned v = (unsigned)(kk >> 32);
     perm[p] = (int)(unsigned)(kk & 0xFFFFFFFFull);
     if (v != 0xFFFFFFFFu && (p == 0 || (unsigned)(keys[p - 1] >> 32) != v)) {
       seg_off[s] = p;
@@ -247,17 +359,17 @@ __global__ __launch_bounds__(kPrepThreads) void vox_prep_kernel(
   }
   __syncthreads();
 
-  // 4. bitmap + per-word exclusive prefix of popcounts
+  // bitmap + per-word exclusive prefix of popcounts
   const int wchunk = (W + nt - 1) / nt;
   const int w0 = min(W, tid * wchunk), w1 = min(W, w0 + wchunk);
   int pc = 0;
   for (int w = w0; w < w1; w++) pc += __popc(bm[w]);
-  int pincl = block_inclusive_scan(pc, scan_s);
+  const int pincl = block_inclusive_scan(pc, scan_s);
   int run = pincl - pc;
   unsigned* gbm = ws.bitmap + (size_t)b * W;
   int* gpre = ws.wprefix + (size_t)b * W;
   for (int w = w0; w < w1; w++) {
-    unsigned word = bm[w];
+    const unsigned word = bm[w];
     gbm[w] = word;
     gpre[w] = run;
     run += __popc(word);
@@ -475,43 +587,54 @@ __global__ __launch_bounds__(256) void avg_vox_grad_kernel(const float* __restri
 }
 
 // ------------------------------------------------------ normalize only
-__global__ __launch_bounds__(256) void sph_normalize_kernel(const float* __restrict__ coords,
-                                                            int n, float* __restrict__ out) {
-  __shared__ double part[256];
+__global__ __launch_bounds__(kPrepThreads) void sph_normalize_kernel(
+    const float* __restrict__ coords, int n, int E, float* __restrict__ out) {
+  __shared__ double red[48];
   __shared__ float s_stat[4];
-  __shared__ float wm[4];
+  __shared__ float wm[kPrepThreads / kWave];
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
   const float* x = coords + (size_t)b * 3 * n;
   float* o = out + (size_t)b * 3 * n;
-  for (int a = 0; a < 3; a++) {
-    double acc = 0.0;
-    for (int i = tid; i < n; i += 256) acc += (double)x[(size_t)a * n + i];
-    part[tid] = acc;
-    __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) {
-      if (tid < s) part[tid] += part[tid + s];
-      __syncthreads();
-    }
-    if (tid == 0) s_stat[a] = (float)(part[0] / (double)n);
-    __syncthreads();
+  float px[kMaxE], py[kMaxE], pz[kMaxE];
+#pragma unroll
+  for (int e = 0; e < kMaxE; e++) {
+    const int i = e * kPrepThreads + tid;
+    const bool ok = e < E && i < n;
+    px[e] = ok ? x[i] : 0.0f;
+    py[e] = ok ? x[i + n] : 0.0f;
+    pz[e] = ok ? x[i + 2 * n] : 0.0f;
   }
+  cloud_mean(px, py, pz, E, n, red, s_stat);
   const float m0 = s_stat[0], m1 = s_stat[1], m2 = s_stat[2];
   float mx = 0.0f;
-  for (int i = tid; i < n; i += 256) {
-    float cx = x[i] - m0, cy = x[i + n] - m1, cz = x[i + 2 * n] - m2;
-    mx = fmaxf(mx, __builtin_sqrtf(pcr_sumsq3f(cx, cy, cz)));
+#pragma unroll
+  for (int e = 0; e < kMaxE; e++) {
+    if (e < E && e * kPrepThreads + tid < n) {
+      px[e] -= m0;
+      py[e] -= m1;
+      pz[e] -= m2;
+      mx = fmaxf(mx, __builtin_sqrtf(pcr_sumsq3f(px[e], py[e], pz[e])));
+    }
   }
   mx = wave_max(mx);
   if ((tid & 63) == 0) wm[tid >> 6] = mx;
   __syncthreads();
-  if (tid == 0) s_stat[3] = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3])) + 1e-20f;
+  if (tid == 0) {
+    float m = 0.0f;
+    for (int w = 0; w < kPrepThreads / kWave; w++) m = fmaxf(m, wm[w]);
+    s_stat[3] = m + 1e-20f;
+  }
   __syncthreads();
   const float den = s_stat[3];
-  for (int i = tid; i < n; i += 256) {
-    o[i] = (x[i] - m0) / den;
-    o[i + n] = (x[i + n] - m1) / den;
-    o[i + 2 * n] = (x[i + 2 * n] - m2) / den;
+#pragma unroll
+  for (int e = 0; e < kMaxE; e++) {
+    const int i = e * kPrepThreads + tid;
+    if (e < E && i < n) {
+      o[i] = px[e] / den;
+      o[i + n] = py[e] / den;
+      o[i + 2 * n] = pz[e] / den;
+    }
   }
 }
 
@@ -549,7 +672,7 @@ static pcr_status run_voxelize(const float* features, const float* coords_f, con
   PCR_REQUIRE(workspace != nullptr && ws_bytes >= need, "%s: workspace too small (%zu < %zu)",
               name, ws_bytes, need);
   if (what & 1) {
-    const int npad = next_pow2(n < 2 ? 2 : n);
+    const int npad = next_pow2(n < kPrepThreads ? kPrepThreads : n);
     size_t prep_smem = (size_t)npad * 8 + (size_t)ws.W * 4;
     PCR_REQUIRE(prep_smem <= 150 * 1024, "%s: prep LDS %zu too large", name, prep_smem);
     allow_big_lds(vox_prep_kernel<MODE>, prep_smem);
@@ -624,8 +747,10 @@ extern "C" pcr_status pcr_spherical_normalize(const float* coords, int b, int n,
                                               float* norm_coords, void* stream) {
   PCR_REQUIRE(b >= 0 && n >= 1, "spherical_normalize: invalid sizes b=%d n=%d", b, n);
   if (b == 0) return PCR_OK;
-  hipLaunchKernelGGL(sph_normalize_kernel, dim3(b), dim3(256), 0, as_stream(stream), coords, n,
-                     norm_coords);
+  PCR_REQUIRE(n <= kMaxSortN, "spherical_normalize: n=%d > %d unsupported", n, kMaxSortN);
+  const int E = next_pow2(n < kPrepThreads ? kPrepThreads : n) / kPrepThreads;
+  hipLaunchKernelGGL(sph_normalize_kernel, dim3(b), dim3(kPrepThreads), 0, as_stream(stream),
+                     coords, n, E, norm_coords);
   return launch_status("spherical_normalize");
 }
 
