@@ -54,6 +54,27 @@ pcr_status knn_spatial(const float* xyz1, const float* xyz2, int b, int n, int m
 // ---------------------------------------------------------------- device
 constexpr int kWave = 64;
 
+// Diagnostic phase stamps (separate build, -DPCR_DIAG, lib/libpcr_amd_diag.so):
+// lane 0 of wave 0 of workgroup g records s_memtime at phase p into
+// pcr_diag_stamps[g][p]; read back with pcr_diag_read().  Compiled out of the
+// product library.
+#ifdef PCR_DIAG
+static __device__ unsigned long long pcr_diag_stamps[1024][16];  // one copy per TU
+#define PCR_DIAG_READER(name)                                                       \
+  extern "C" int name(unsigned long long* host) {                                  \
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(pcr::pcr_diag_stamps), sizeof(pcr::pcr_diag_stamps)); \
+  }
+#define PCR_STAMP(p)                                                              \
+  do {                                                                            \
+    if (threadIdx.x == 0 && blockIdx.x + gridDim.x * blockIdx.y < 1024)           \
+      pcr_diag_stamps[blockIdx.x + gridDim.x * blockIdx.y][p] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define PCR_STAMP(p) \
+  do {               \
+  } while (0)
+#endif
+
 // Inclusive block-wide scan of one int per thread (blockDim.x threads,
 // multiple of 64, <= 1024).  `smem` needs blockDim.x/64 + 1 ints.
 __device__ inline int block_inclusive_scan(int v, int* smem) {
@@ -92,6 +113,83 @@ __device__ inline double wave_sum_d(double v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
   return v;
+}
+
+// Block-wide sorts: kSortBlock threads, up to kMaxE keys per thread.
+constexpr int kSortBlock = 1024;
+constexpr int kMaxE = 4;
+
+__device__ inline unsigned long long shfl_xor_u64(unsigned long long v, int m) {
+  const int lo = __shfl_xor((int)(unsigned)(v & 0xFFFFFFFFull), m, kWave);
+  const int hi = __shfl_xor((int)(unsigned)(v >> 32), m, kWave);
+  return ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
+}
+
+// Ascending bitonic sort of E*1024 keys, element (e, tid) at index e*1024+tid.
+__device__ inline void block_bitonic(unsigned long long (&v)[kMaxE], int E,
+                                     unsigned long long* lds) {
+  const int tid = threadIdx.x;
+  const int npad = E * kSortBlock;
+  for (int kk = 2; kk <= npad; kk <<= 1) {
+    int j = kk >> 1;
+    // partner in another register of this thread
+    for (; j >= kSortBlock; j >>= 1) {
+      const int je = j / kSortBlock;
+#pragma unroll
+      for (int e = 0; e < kMaxE; e++) {
+        const int pe = e ^ je;
+        if (e < E && pe > e) {
+          const int i = e * kSortBlock + tid;
+          const bool up = (i & kk) == 0;
+          const unsigned long long a = v[e], b = v[pe];
+          if ((a > b) == up) {
+            v[e] = b;
+            v[pe] = a;
+          }
+        }
+      }
+    }
+    // partner in another wave: through LDS
+    if (j >= kWave) {
+#pragma unroll
+      for (int e = 0; e < kMaxE; e++)
+        if (e < E) lds[e * kSortBlock + tid] = v[e];
+      __syncthreads();
+      for (; j >= kWave; j >>= 1) {
+        for (int t = tid; t < (npad >> 1); t += kSortBlock) {
+          const int i = 2 * j * (t / j) + (t % j);
+          const int l = i + j;
+          const unsigned long long a = lds[i], b = lds[l];
+          if ((a > b) == ((i & kk) == 0)) {
+            lds[i] = b;
+            lds[l] = a;
+          }
+        }
+        __syncthreads();
+      }
+#pragma unroll
+      for (int e = 0; e < kMaxE; e++)
+        if (e < E) v[e] = lds[e * kSortBlock + tid];
+      __syncthreads();
+    }
+    // partner in the same wave: cross-lane exchange
+    for (; j > 0; j >>= 1) {
+#pragma unroll
+      for (int e = 0; e < kMaxE; e++) {
+        if (e < E) {
+          const int i = e * kSortBlock + tid;
+          const unsigned long long o = shfl_xor_u64(v[e], j);
+          const bool lower = (i & j) == 0;
+          const bool up = (i & kk) == 0;
+          // lower element keeps min when ascending, max when descending
+          const bool take_min = (lower == up);
+          const unsigned long long mn = v[e] < o ? v[e] : o;
+          const unsigned long long mx = v[e] < o ? o : v[e];
+          v[e] = take_min ? mn : mx;
+        }
+      }
+    }
+  }
 }
 
 }  // namespace pcr

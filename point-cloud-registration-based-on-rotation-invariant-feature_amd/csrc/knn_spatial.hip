@@ -21,7 +21,6 @@
 
 namespace pcr {
 
-constexpr int kSortThreads = 512;
 constexpr int kKnnMaxSortN = 4096;
 constexpr int kBlk = 64;
 
@@ -78,24 +77,31 @@ __device__ inline unsigned quant10(float v, float lo, float scale) {
   return (unsigned)t;
 }
 
-__global__ __launch_bounds__(kSortThreads) void knn_sort_kernel(const float* __restrict__ pts,
-                                                                int n, int npad_sort, KnnSet s) {
+__global__ __launch_bounds__(kSortBlock) void knn_sort_kernel(const float* __restrict__ pts,
+                                                              int n, int npad_sort, KnnSet s) {
   extern __shared__ __align__(16) unsigned long long keys[];  // [npad_sort]
-  __shared__ float red[6][kSortThreads / kWave];
+  __shared__ float red[6][kSortBlock / kWave];
   __shared__ float frame[6];
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
+  const int E = npad_sort / kSortBlock;
   const float* P = pts + (size_t)b * 3 * n;
-  // bounding box (NaN-ignoring)
+  float px[kMaxE], py[kMaxE], pz[kMaxE];
   float mn[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
   float mx[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
-  for (int i = tid; i < n; i += kSortThreads) {
 #pragma unroll
-    for (int a = 0; a < 3; a++) {
-      const float v = P[(size_t)a * n + i];
-      mn[a] = fminf(mn[a], v);
-      mx[a] = fmaxf(mx[a], v);
-    }
+  for (int e = 0; e < kMaxE; e++) {
+    const int i = e * kSortBlock + tid;
+    const bool ok = e < E && i < n;
+    px[e] = ok ? P[i] : __builtin_nanf("");
+    py[e] = ok ? P[n + i] : __builtin_nanf("");
+    pz[e] = ok ? P[2 * n + i] : __builtin_nanf("");
+    mn[0] = fminf(mn[0], px[e]);  // fminf/fmaxf ignore NaN
+    mn[1] = fminf(mn[1], py[e]);
+    mn[2] = fminf(mn[2], pz[e]);
+    mx[0] = fmaxf(mx[0], px[e]);
+    mx[1] = fmaxf(mx[1], py[e]);
+    mx[2] = fmaxf(mx[2], pz[e]);
   }
 #pragma unroll
   for (int a = 0; a < 3; a++) {
@@ -115,7 +121,7 @@ __global__ __launch_bounds__(kSortThreads) void knn_sort_kernel(const float* __r
   __syncthreads();
   if (tid < 6) {
     float v = red[tid][0];
-    for (int w = 1; w < kSortThreads / kWave; w++)
+    for (int w = 1; w < kSortBlock / kWave; w++)
       v = tid < 3 ? fminf(v, red[tid][w]) : fmaxf(v, red[tid][w]);
     frame[tid] = v;
   }
@@ -127,35 +133,27 @@ __global__ __launch_bounds__(kSortThreads) void knn_sort_kernel(const float* __r
     const float ext = frame[3 + a] - frame[a];
     sc[a] = (ext > 0.0f && ext < __builtin_inff()) ? 1023.0f / ext : 0.0f;
   }
-  for (int i = tid; i < npad_sort; i += kSortThreads) {
-    unsigned long long key = ~0ull;
-    if (i < n) {
-      const unsigned code = spread10(quant10(P[i], lo[0], sc[0])) |
-                            (spread10(quant10(P[n + i], lo[1], sc[1])) << 1) |
-                            (spread10(quant10(P[2 * n + i], lo[2], sc[2])) << 2);
-      key = ((unsigned long long)code << 32) | (unsigned)i;
+  unsigned long long kv[kMaxE];
+#pragma unroll
+  for (int e = 0; e < kMaxE; e++) {
+    const int i = e * kSortBlock + tid;
+    kv[e] = ~0ull;
+    if (e < E && i < n) {
+      const unsigned code = spread10(quant10(px[e], lo[0], sc[0])) |
+                            (spread10(quant10(py[e], lo[1], sc[1])) << 1) |
+                            (spread10(quant10(pz[e], lo[2], sc[2])) << 2);
+      kv[e] = ((unsigned long long)code << 32) | (unsigned)i;
     }
-    keys[i] = key;
   }
+  block_bitonic(kv, E, keys);
+#pragma unroll
+  for (int e = 0; e < kMaxE; e++)
+    if (e < E) keys[e * kSortBlock + tid] = kv[e];
   __syncthreads();
-  for (int k = 2; k <= npad_sort; k <<= 1) {
-    for (int jj = k >> 1; jj > 0; jj >>= 1) {
-      for (int t = tid; t < (npad_sort >> 1); t += kSortThreads) {
-        const int i = 2 * jj * (t / jj) + (t % jj);
-        const int l = i + jj;
-        const unsigned long long a = keys[i], c = keys[l];
-        if ((a > c) == ((i & k) == 0)) {
-          keys[i] = c;
-          keys[l] = a;
-        }
-      }
-      __syncthreads();
-    }
-  }
   // sorted SoA + per-block boxes (one wave per block)
   const size_t base = (size_t)b * s.npad;
   const int lane = tid & 63;
-  for (int blk = tid >> 6; blk < s.nblk; blk += kSortThreads / kWave) {
+  for (int blk = tid >> 6; blk < s.nblk; blk += kSortBlock / kWave) {
     const int p = blk * kBlk + lane;
     float x = __builtin_nanf(""), y = x, z = x;
     int j = -1;
@@ -282,6 +280,28 @@ __device__ inline float box_lb(float qx, float qy, float qz, const float* bx) {
   return d;
 }
 
+// Waves per query block: the candidate blocks of one 64-query block are
+// dealt round-robin to NW waves (more parallelism than one wave per query
+// block: B=32 x N=1024 gives only 512 query blocks for 1024 SIMDs), each wave
+// keeps its own top-k, and the lists are merged through LDS at the end.
+template <int KMAX>
+struct KnnNW {
+  static constexpr int value = KMAX <= 32 ? 4 : (KMAX <= 64 ? 2 : 1);
+};
+
+// r-th block of the visiting order home, home-1, home+1, home-2, ...
+__device__ inline int visit_block(int r, int home, int nblk) {
+  const int lo = home, hi = nblk - 1 - home;
+  const int m2 = lo < hi ? lo : hi;
+  if (r == 0) return home;
+  if (r <= 2 * m2) {
+    const int o = (r + 1) >> 1;
+    return (r & 1) ? home - o : home + o;
+  }
+  const int extra = r - 2 * m2;
+  return lo > hi ? home - (m2 + extra) : home + (m2 + extra);
+}
+
 template <int KMAX, bool PPF>
 __global__ __launch_bounds__(256) void knn_block_kernel(
     KnnSet qs, KnnSet cs, int k, float* __restrict__ dist, int* __restrict__ idx,
@@ -289,86 +309,158 @@ __global__ __launch_bounds__(256) void knn_block_kernel(
     const float* __restrict__ qxyz, const float* __restrict__ qnrm,
     const float* __restrict__ cxyz, const float* __restrict__ cnrm, int relative,
     float* __restrict__ ppf) {
+  constexpr int NW = KnnNW<KMAX>::value;
+  constexpr int QPW = 4 / NW;  // query blocks per workgroup
+  __shared__ unsigned long long qbuf[4 * kQ * kBlk];          // 32 KB batches
+  // merge lists; also holds the final lists for the PPF phase (NW > 1)
+  __shared__ unsigned long long lst[NW > 1 ? QPW * (NW / 2) * KMAX * kBlk : 1];
+  __shared__ float thr_s[4][kBlk];
   const int b = blockIdx.y;
-  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int wv = threadIdx.x >> 6;
+  const int w = wv % NW;                       // wave within its query block
+  const int qblk = blockIdx.x * QPW + wv / NW;
   const int lane = threadIdx.x & 63;
-  if (wave >= qs.nblk) return;  // wave-uniform
-  const size_t qb = (size_t)b * qs.npad + (size_t)wave * kBlk + lane;
+  const bool live = qblk < qs.nblk;            // wave-uniform
+  const size_t qb = (size_t)b * qs.npad + (size_t)(live ? qblk : 0) * kBlk + lane;
   const float qx = qs.x[qb], qy = qs.y[qb], qz = qs.z[qb];
-  const int qj = qs.j[qb];
+  const int qj = live ? qs.j[qb] : -1;
   TopKKey<KMAX> top;
   top.init(k);
-  // per-lane batch of qualifying keys, LDS [wave][slot][lane] (conflict-free)
-  __shared__ unsigned long long qbuf[4 * kQ * kBlk];
-  unsigned long long* myq = qbuf + (threadIdx.x >> 6) * kQ * kBlk + lane;
+  unsigned long long* myq = qbuf + wv * kQ * kBlk + lane;
   int qn = 0;
+  thr_s[wv][lane] = PCR_KNN_UNDEF;
+  __syncthreads();
+  PCR_STAMP(0);
+  int nflush = 0, nproc = 0;
   auto flush = [&]() {
     unsigned long long qv[kQ];
 #pragma unroll
     for (int s = 0; s < kQ; s++) qv[s] = s < qn ? myq[s * kBlk] : ~0ull;
     merge_batch<KMAX>(top.key, qv);
     qn = 0;
+    nflush++;
+    thr_s[wv][lane] = top.kth();  // publish: an upper bound of the final k-th
   };
-  const float* boxes = cs.box + (size_t)b * cs.nblk * 8;
-  const size_t cbase = (size_t)b * cs.npad;
-  // home block: same relative position in the candidate Morton order
-  int home = (int)(((long long)wave * cs.nblk) / qs.nblk);
-  if (home >= cs.nblk) home = cs.nblk - 1;
-  for (int step = 0; step < 2 * cs.nblk; step++) {
-    const int off = (step + 1) >> 1;
-    const int blk = (step & 1) ? home + off : home - off;
-    if (blk < 0 || blk >= cs.nblk) {
-      if (home - off < 0 && home + off >= cs.nblk) break;
-      continue;
-    }
-    const float* bx = boxes + (size_t)blk * 8;
-    const float lb = box_lb(qx, qy, qz, bx);
-    const float thr = top.kth();
-    if (!__any(lb <= thr)) continue;  // no lane can gain from this block
-    const size_t cp = cbase + (size_t)blk * kBlk + lane;
-    const float cx = cs.x[cp], cy = cs.y[cp], cz = cs.z[cp];
-    const int cj = cs.j[cp];
-#pragma unroll 2
-    for (int t = 0; t < kBlk; t++) {
-      const float sx = readlane_f(cx, t), sy = readlane_f(cy, t), sz = readlane_f(cz, t);
-      const int sj = __builtin_amdgcn_readlane(cj, t);
-      const float a = qx - sx, bb = qy - sy, cc = qz - sz;
-      float d = a * a;
-      d = __builtin_fmaf(bb, bb, d);
-      d = __builtin_fmaf(cc, cc, d);
-      const unsigned long long key = make_key(d, sj);
-      // batch against the (stale, hence conservative) k-th key; merge when
-      // any lane's batch is full
-      if (top.qualifies(key)) {
-        myq[qn * kBlk] = key;
-        qn++;
+  const int gbase = wv - w;  // first wave of this query block
+  if (live) {
+    const float* boxes = cs.box + (size_t)b * cs.nblk * 8;
+    const size_t cbase = (size_t)b * cs.npad;
+    int home = (int)(((long long)qblk * cs.nblk) / qs.nblk);
+    if (home >= cs.nblk) home = cs.nblk - 1;
+    for (int rr = w; rr < cs.nblk; rr += NW) {
+      const int blk = visit_block(rr, home, cs.nblk);
+      // best bound known to any wave of this query block
+      float thr = top.kth();
+#pragma unroll
+      for (int o = 0; o < NW; o++) thr = fminf(thr, thr_s[gbase + o][lane]);
+      const float lb = box_lb(qx, qy, qz, boxes + (size_t)blk * 8);
+      if (!__any(lb <= thr)) continue;  // no lane can gain from this block
+      const size_t cp = cbase + (size_t)blk * kBlk + lane;
+      const float cx = cs.x[cp], cy = cs.y[cp], cz = cs.z[cp];
+      const int cj = cs.j[cp];
+      nproc++;
+      for (int t = 0; t < kBlk; t += 2) {
+        if (__any(qn > kQ - 2)) flush();
+        const float sx0 = readlane_f(cx, t), sy0 = readlane_f(cy, t), sz0 = readlane_f(cz, t);
+        const float sx1 = readlane_f(cx, t + 1), sy1 = readlane_f(cy, t + 1),
+                    sz1 = readlane_f(cz, t + 1);
+        const int sj0 = __builtin_amdgcn_readlane(cj, t);
+        const int sj1 = __builtin_amdgcn_readlane(cj, t + 1);
+        const float a0 = qx - sx0, b0 = qy - sy0, c0 = qz - sz0;
+        const float a1 = qx - sx1, b1 = qy - sy1, c1 = qz - sz1;
+        float d0 = a0 * a0, d1 = a1 * a1;
+        d0 = __builtin_fmaf(b0, b0, d0);
+        d1 = __builtin_fmaf(b1, b1, d1);
+        d0 = __builtin_fmaf(c0, c0, d0);
+        d1 = __builtin_fmaf(c1, c1, d1);
+        const unsigned long long k0 = make_key(d0, sj0), k1 = make_key(d1, sj1);
+        // keys above this wave's (stale) k-th, or farther than another
+        // wave's k-th distance, can never reach the final list
+        if (top.qualifies(k0) && d0 <= thr) {
+          myq[qn * kBlk] = k0;
+          qn++;
+        }
+        if (top.qualifies(k1) && d1 <= thr) {
+          myq[qn * kBlk] = k1;
+          qn++;
+        }
       }
-      if (__any(qn == kQ)) flush();
+    }
+    if (__any(qn > 0)) flush();
+  }
+  PCR_STAMP(1);
+  (void)nflush;
+  (void)nproc;
+#ifdef PCR_DIAG
+  if (threadIdx.x == 0 && blockIdx.x + gridDim.x * blockIdx.y < 1024) {
+    pcr_diag_stamps[blockIdx.x + gridDim.x * blockIdx.y][8] = nflush;
+    pcr_diag_stamps[blockIdx.x + gridDim.x * blockIdx.y][9] = nproc;
+  }
+#endif
+  // merge the NW lists of a query block: tree of bitonic merges through LDS
+#pragma unroll
+  for (int half = NW / 2; half >= 1; half >>= 1) {
+    __syncthreads();
+    if (live && w >= half && w < 2 * half) {
+      unsigned long long* dst = lst + (size_t)((wv / NW) * (NW / 2) + (w - half)) * KMAX * kBlk;
+#pragma unroll
+      for (int s = 0; s < KMAX; s++) dst[s * kBlk + lane] = top.key[s];
+    }
+    __syncthreads();
+    if (live && w < half) {
+      const unsigned long long* src = lst + (size_t)((wv / NW) * (NW / 2) + w) * KMAX * kBlk;
+      // C[i] = min(A[i], B[K-1-i]) then bitonic merge
+#pragma unroll
+      for (int i = 0; i < KMAX; i++) {
+        const unsigned long long o = src[(KMAX - 1 - i) * kBlk + lane];
+        top.key[i] = top.key[i] < o ? top.key[i] : o;
+      }
+#pragma unroll
+      for (int jj = KMAX >> 1; jj > 0; jj >>= 1) {
+#pragma unroll
+        for (int i = 0; i < KMAX; i++) {
+          const int l = i ^ jj;
+          if (l > i) cex_up(top.key[i], top.key[l]);
+        }
+      }
     }
   }
-  if (__any(qn > 0)) flush();
-  if (qj < 0) return;
+  PCR_STAMP(2);
   const int n = qs.n;
   const int base = KMAX - k;
+  if (live && w == 0 && qj >= 0) {
 #pragma unroll
-  for (int s = 0; s < KMAX; s++) {
-    if (s >= base) {
-      const size_t o = ((size_t)b * k + (s - base)) * n + qj;
-      if (dist) dist[o] = __uint_as_float((unsigned)(top.key[s] >> 32));
-      idx[o] = (int)(unsigned)(top.key[s] & 0xFFFFFFFFull);
+    for (int s = 0; s < KMAX; s++) {
+      if (s >= base) {
+        const size_t o = ((size_t)b * k + (s - base)) * n + qj;
+        if (dist) dist[o] = __uint_as_float((unsigned)(top.key[s] >> 32));
+        idx[o] = (int)(unsigned)(top.key[s] & 0xFFFFFFFFull);
+      }
     }
   }
   if (PPF) {
+    // every wave of the query block takes a share of the slots
+    unsigned long long* fin = lst + (size_t)(wv / NW) * KMAX * kBlk;
+    if (NW > 1) {
+      __syncthreads();  // merge reads of lst are complete
+      if (live && w == 0) {
+#pragma unroll
+        for (int s = 0; s < KMAX; s++) fin[s * kBlk + lane] = top.key[s];
+      }
+      __syncthreads();
+    }
+    if (!live || qj < 0) return;
     const int m = cs.n;
     const float* cb = cxyz + (size_t)b * 3 * m;
     const float* nb = cnrm + (size_t)b * 3 * m;
-    const float* qn = qnrm + (size_t)b * 3 * n;
+    const float* qnr = qnrm + (size_t)b * 3 * n;
     const float* qo = qxyz + (size_t)b * 3 * n;
     const float ox = qo[qj], oy = qo[qj + n], oz = qo[qj + 2 * n];
-    const float cnx = qn[qj], cny = qn[qj + n], cnz = qn[qj + 2 * n];
+    const float cnx = qnr[qj], cny = qnr[qj + n], cnz = qnr[qj + 2 * n];
 #pragma unroll 1
-    for (int slot = 0; slot < k; slot++) {
-      const int jn = idx[((size_t)b * k + slot) * n + qj];
+    for (int slot = w; slot < k; slot += NW) {
+      const int jn = NW > 1 ? (int)(unsigned)(fin[(base + slot) * kBlk + lane] & 0xFFFFFFFFull)
+                            : idx[((size_t)b * k + slot) * n + qj];
       float o[4];
       pcr_local_ppf(ox, oy, oz, cnx, cny, cnz, cb[jn], cb[jn + m], cb[jn + 2 * m], nb[jn],
                     nb[jn + m], nb[jn + 2 * m], relative, o);
@@ -390,32 +482,35 @@ static int next_pow2i(int v) {
 }
 
 static void launch_sort(const float* pts, int b, int n, const KnnSet& s, hipStream_t st) {
-  const int npad_sort = next_pow2i(n < 2 ? 2 : n);
+  const int npad_sort = next_pow2i(n < kSortBlock ? kSortBlock : n);
   const size_t smem = (size_t)npad_sort * 8;
   allow_big_lds(knn_sort_kernel, smem);
-  hipLaunchKernelGGL(knn_sort_kernel, dim3(b), dim3(kSortThreads), smem, st, pts, n, npad_sort,
-                     s);
+  hipLaunchKernelGGL(knn_sort_kernel, dim3(b), dim3(kSortBlock), smem, st, pts, n, npad_sort, s);
+}
+
+template <int KM, bool PPF>
+static void launch_block_k(const KnnSet& qs, const KnnSet& cs, int b, int k, float* dist,
+                           int* idx, const float* qxyz, const float* qnrm, const float* cxyz,
+                           const float* cnrm, int relative, float* ppf, hipStream_t st) {
+  dim3 grid(ceil_div(qs.nblk, 4 / KnnNW<KM>::value), b);
+  hipLaunchKernelGGL((knn_block_kernel<KM, PPF>), grid, dim3(256), 0, st, qs, cs, k, dist, idx,
+                     qxyz, qnrm, cxyz, cnrm, relative, ppf);
 }
 
 template <bool PPF>
 static pcr_status launch_block(const KnnSet& qs, const KnnSet& cs, int b, int k, float* dist,
                                int* idx, const float* qxyz, const float* qnrm, const float* cxyz,
                                const float* cnrm, int relative, float* ppf, hipStream_t st) {
-  dim3 grid(ceil_div(qs.nblk, 4), b);
-#define PCR_KB(KM)                                                                        \
-  hipLaunchKernelGGL((knn_block_kernel<KM, PPF>), grid, dim3(256), 0, st, qs, cs, k, dist, idx, \
-                     qxyz, qnrm, cxyz, cnrm, relative, ppf)
   if (k <= 16)
-    PCR_KB(16);
+    launch_block_k<16, PPF>(qs, cs, b, k, dist, idx, qxyz, qnrm, cxyz, cnrm, relative, ppf, st);
   else if (k <= 32)
-    PCR_KB(32);
+    launch_block_k<32, PPF>(qs, cs, b, k, dist, idx, qxyz, qnrm, cxyz, cnrm, relative, ppf, st);
   else if (k <= 64)
-    PCR_KB(64);
+    launch_block_k<64, PPF>(qs, cs, b, k, dist, idx, qxyz, qnrm, cxyz, cnrm, relative, ppf, st);
   else if (k <= 128)
-    PCR_KB(128);
+    launch_block_k<128, PPF>(qs, cs, b, k, dist, idx, qxyz, qnrm, cxyz, cnrm, relative, ppf, st);
   else
     return PCR_ERR_UNSUPPORTED;
-#undef PCR_KB
   return PCR_OK;
 }
 
@@ -452,3 +547,7 @@ extern "C" size_t pcr_knn_workspace_size(int b, int n, int m) {
   if (b <= 0 || n <= 0 || m <= 0) return 256;
   return pcr::knn_ws_size(b, n, m);
 }
+
+#ifdef PCR_DIAG
+PCR_DIAG_READER(pcr_diag_read_knn)
+#endif

@@ -29,4 +29,5 @@ pcr_status launch_status(const char* what) {
 }  // namespace pcr
 
 extern "C" const char* pcr_last_error(void) { return pcr::g_err; }
+
 extern "C" const char* pcr_version(void) { return "pcr_amd 0.1.0 gfx950"; }

@@ -28,8 +28,8 @@
 
 namespace pcr {
 
-constexpr int kPrepThreads = 1024;
-constexpr int kMaxSortN = 4096;
+constexpr int kPrepThreads = kSortBlock;
+constexpr int kMaxSortN = kSortBlock * kMaxE;
 constexpr int kGridThreads = 256;
 constexpr int kMaxG = 8;
 
@@ -89,7 +89,6 @@ static inline int next_pow2(int v) {
 // stages run in registers (partner in the same thread), with DPP/shuffles
 // (partner in the same wave) or through LDS (other waves) -- 10 barriers for
 // 1024 keys instead of 55.
-constexpr int kMaxE = kMaxSortN / kPrepThreads;
 
 // Fixed-order per-axis mean of a cloud in double, the order the oracle
 // restates (orc_cloud_mean): thread t sums points t, t+1024, ... ascending;
@@ -131,79 +130,6 @@ __device__ inline void cloud_mean(const float (&px)[kMaxE], const float (&py)[kM
   __syncthreads();
 }
 
-__device__ inline unsigned long long shfl_xor_u64(unsigned long long v, int m) {
-  const int lo = __shfl_xor((int)(unsigned)(v & 0xFFFFFFFFull), m, kWave);
-  const int hi = __shfl_xor((int)(unsigned)(v >> 32), m, kWave);
-  return ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
-}
-
-// Ascending bitonic sort of E*1024 keys, element (e, tid) at index e*1024+tid.
-__device__ inline void block_bitonic(unsigned long long (&v)[kMaxE], int E,
-                                     unsigned long long* lds) {
-  const int tid = threadIdx.x;
-  const int npad = E * kPrepThreads;
-  for (int kk = 2; kk <= npad; kk <<= 1) {
-    int j = kk >> 1;
-    // partner in another register of this thread
-    for (; j >= kPrepThreads; j >>= 1) {
-      const int je = j / kPrepThreads;
-#pragma unroll
-      for (int e = 0; e < kMaxE; e++) {
-        const int pe = e ^ je;
-        if (e < E && pe > e) {
-          const int i = e * kPrepThreads + tid;
-          const bool up = (i & kk) == 0;
-          const unsigned long long a = v[e], b = v[pe];
-          if ((a > b) == up) {
-            v[e] = b;
-            v[pe] = a;
-          }
-        }
-      }
-    }
-    // partner in another wave: through LDS
-    if (j >= kWave) {
-#pragma unroll
-      for (int e = 0; e < kMaxE; e++)
-        if (e < E) lds[e * kPrepThreads + tid] = v[e];
-      __syncthreads();
-      for (; j >= kWave; j >>= 1) {
-        for (int t = tid; t < (npad >> 1); t += kPrepThreads) {
-          const int i = 2 * j * (t / j) + (t % j);
-          const int l = i + j;
-          const unsigned long long a = lds[i], b = lds[l];
-          if ((a > b) == ((i & kk) == 0)) {
-            lds[i] = b;
-            lds[l] = a;
-          }
-        }
-        __syncthreads();
-      }
-#pragma unroll
-      for (int e = 0; e < kMaxE; e++)
-        if (e < E) v[e] = lds[e * kPrepThreads + tid];
-      __syncthreads();
-    }
-    // partner in the same wave: cross-lane exchange
-    for (; j > 0; j >>= 1) {
-#pragma unroll
-      for (int e = 0; e < kMaxE; e++) {
-        if (e < E) {
-          const int i = e * kPrepThreads + tid;
-          const unsigned long long o = shfl_xor_u64(v[e], j);
-          const bool lower = (i & j) == 0;
-          const bool up = (i & kk) == 0;
-          // lower element keeps min when ascending, max when descending
-          const bool take_min = (lower == up);
-          const unsigned long long mn = v[e] < o ? v[e] : o;
-          const unsigned long long mx = v[e] < o ? o : v[e];
-          v[e] = take_min ? mn : mx;
-        }
-      }
-    }
-  }
-}
-
 template <int MODE>
 __global__ __launch_bounds__(kPrepThreads) void vox_prep_kernel(
     const float* __restrict__ coords_f, const int* __restrict__ coords_i, int n, int r, int npad,
@@ -222,6 +148,7 @@ __global__ __launch_bounds__(kPrepThreads) void vox_prep_kernel(
   const int r3 = r * r * r;
   const int W = ws.W;
   const int E = npad / kPrepThreads;
+  PCR_STAMP(0);
 
   float px[kMaxE], py[kMaxE], pz[kMaxE];
   int ci[kMaxE][3];
@@ -250,6 +177,7 @@ __global__ __launch_bounds__(kPrepThreads) void vox_prep_kernel(
 
   if (MODE == kSphNormalize) {
     cloud_mean(px, py, pz, E, n, red, s_stat);
+    PCR_STAMP(1);
     const float m0 = s_stat[0], m1 = s_stat[1], m2 = s_stat[2];
     float mx = 0.0f;
 #pragma unroll
@@ -279,6 +207,7 @@ __global__ __launch_bounds__(kPrepThreads) void vox_prep_kernel(
     }
   }
 
+  PCR_STAMP(2);
   // voxel index, devox corners, sort keys
   unsigned long long kv[kMaxE];
 #pragma unroll
@@ -318,8 +247,10 @@ __global__ __launch_bounds__(kPrepThreads) void vox_prep_kernel(
     }
   }
 
+  PCR_STAMP(3);
   // sort (unique keys: the low word is the point id -> stable by voxel)
   block_bitonic(kv, E, keys);
+  PCR_STAMP(4);
 #pragma unroll
   for (int e = 0; e < kMaxE; e++)
     if (e < E) keys[e * nt + tid] = kv[e];
@@ -358,6 +289,7 @@ __global__ __launch_bounds__(kPrepThreads) void vox_prep_kernel(
     seg_off[incl] = nv_incl;
   }
   __syncthreads();
+  PCR_STAMP(5);
 
   // bitmap + per-word exclusive prefix of popcounts
   const int wchunk = (W + nt - 1) / nt;
@@ -374,6 +306,7 @@ __global__ __launch_bounds__(kPrepThreads) void vox_prep_kernel(
     gpre[w] = run;
     run += __popc(word);
   }
+  PCR_STAMP(6);
 }
 
 // ------------------------------------------------------------ grid kernel
@@ -796,3 +729,7 @@ extern "C" pcr_status pcr_extractor_voxel_stage(const float* xyz, const float* f
                                      workspace_bytes, as_stream(stream), norm_coords, devox,
                                      dinds, dwgts, desc, "extractor_voxel_stage");
 }
+
+#ifdef PCR_DIAG
+PCR_DIAG_READER(pcr_diag_read_vox)
+#endif
