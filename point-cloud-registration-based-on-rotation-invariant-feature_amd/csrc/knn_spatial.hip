@@ -234,7 +234,7 @@ __device__ inline void cex_up(unsigned long long& a, unsigned long long& b) {
 // sort of the batch, C[i] = min(A[i], Q[K-1-i]) (the K smallest of A u Q as
 // a bitonic sequence), then a bitonic merge.  kQ*log2(kQ)^2/4 + kQ +
 // (K/2)*log2(K) compare-exchanges for kQ keys instead of kQ*K selects.
-constexpr int kQ = 16;
+constexpr int kQ = 8;
 template <int KMAX>
 __device__ inline void merge_batch(unsigned long long (&key)[KMAX], unsigned long long (&q)[kQ]) {
 #pragma unroll
@@ -311,9 +311,13 @@ __global__ __launch_bounds__(256) void knn_block_kernel(
     float* __restrict__ ppf) {
   constexpr int NW = KnnNW<KMAX>::value;
   constexpr int QPW = 4 / NW;  // query blocks per workgroup
-  __shared__ unsigned long long qbuf[4 * kQ * kBlk];          // 32 KB batches
-  // merge lists; also holds the final lists for the PPF phase (NW > 1)
-  __shared__ unsigned long long lst[NW > 1 ? QPW * (NW / 2) * KMAX * kBlk : 1];
+  // LDS: the per-lane batches (scan phase) and the merge lists (merge / PPF
+  // phase) are never live together -> one union
+  constexpr int kQBytes = 4 * kQ * kBlk * 8;
+  constexpr int kLBytes = NW > 1 ? QPW * (NW / 2) * KMAX * kBlk * 8 : 8;
+  __shared__ __align__(16) unsigned char lds_u[kQBytes > kLBytes ? kQBytes : kLBytes];
+  unsigned long long* qbuf = (unsigned long long*)lds_u;
+  unsigned long long* lst = (unsigned long long*)lds_u;
   __shared__ float thr_s[4][kBlk];
   const int b = blockIdx.y;
   const int wv = threadIdx.x >> 6;
@@ -335,7 +339,9 @@ __global__ __launch_bounds__(256) void knn_block_kernel(
   auto flush = [&]() {
     unsigned long long qv[kQ];
 #pragma unroll
-    for (int s = 0; s < kQ; s++) qv[s] = s < qn ? myq[s * kBlk] : ~0ull;
+    for (int s = 0; s < kQ; s++) qv[s] = myq[s * kBlk];
+#pragma unroll
+    for (int s = 0; s < kQ; s++) qv[s] = s < qn ? qv[s] : ~0ull;
     merge_batch<KMAX>(top.key, qv);
     qn = 0;
     nflush++;
@@ -376,14 +382,11 @@ __global__ __launch_bounds__(256) void knn_block_kernel(
         const unsigned long long k0 = make_key(d0, sj0), k1 = make_key(d1, sj1);
         // keys above this wave's (stale) k-th, or farther than another
         // wave's k-th distance, can never reach the final list
-        if (top.qualifies(k0) && d0 <= thr) {
-          myq[qn * kBlk] = k0;
-          qn++;
-        }
-        if (top.qualifies(k1) && d1 <= thr) {
-          myq[qn * kBlk] = k1;
-          qn++;
-        }
+        // branch-free append: slot qn is free (flushed above when < 2 left)
+        myq[qn * kBlk] = k0;
+        qn += (top.qualifies(k0) && d0 <= thr) ? 1 : 0;
+        myq[qn * kBlk] = k1;
+        qn += (top.qualifies(k1) && d1 <= thr) ? 1 : 0;
       }
     }
     if (__any(qn > 0)) flush();
@@ -397,7 +400,10 @@ __global__ __launch_bounds__(256) void knn_block_kernel(
     pcr_diag_stamps[blockIdx.x + gridDim.x * blockIdx.y][9] = nproc;
   }
 #endif
-  // merge the NW lists of a query block: tree of bitonic merges through LDS
+  // merge the NW lists of a query block: tree of bitonic merges through LDS.
+  // The partner's k-k front sentinels (key 0) must not enter the result:
+  // they read as +inf.
+  const int base = KMAX - k;
 #pragma unroll
   for (int half = NW / 2; half >= 1; half >>= 1) {
     __syncthreads();
@@ -412,7 +418,8 @@ __global__ __launch_bounds__(256) void knn_block_kernel(
       // C[i] = min(A[i], B[K-1-i]) then bitonic merge
 #pragma unroll
       for (int i = 0; i < KMAX; i++) {
-        const unsigned long long o = src[(KMAX - 1 - i) * kBlk + lane];
+        const unsigned long long o =
+            (KMAX - 1 - i) < base ? ~0ull : src[(KMAX - 1 - i) * kBlk + lane];
         top.key[i] = top.key[i] < o ? top.key[i] : o;
       }
 #pragma unroll
@@ -427,7 +434,6 @@ __global__ __launch_bounds__(256) void knn_block_kernel(
   }
   PCR_STAMP(2);
   const int n = qs.n;
-  const int base = KMAX - k;
   if (live && w == 0 && qj >= 0) {
 #pragma unroll
     for (int s = 0; s < KMAX; s++) {

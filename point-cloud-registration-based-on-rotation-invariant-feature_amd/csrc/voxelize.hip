@@ -248,64 +248,119 @@ __global__ __launch_bounds__(kPrepThreads) void vox_prep_kernel(
   }
 
   PCR_STAMP(3);
-  // sort (unique keys: the low word is the point id -> stable by voxel)
-  block_bitonic(kv, E, keys);
-  PCR_STAMP(4);
-#pragma unroll
-  for (int e = 0; e < kMaxE; e++)
-    if (e < E) keys[e * nt + tid] = kv[e];
-  __syncthreads();
-
-  // segments: contiguous chunk of sorted positions per thread
-  const int chunk = (n + nt - 1) / nt;
-  const int p0 = min(n, tid * chunk), p1 = min(n, p0 + chunk);
-  int local = 0, nvalid_local = 0;
-  for (int p = p0; p < p1; p++) {
-    const unsigned v = (unsigned)(keys[p] >> 32);
-    if (v != 0xFFFFFFFFu) {
-      nvalid_local++;
-      if (p == 0 || (unsigned)(keys[p - 1] >> 32) != v) local++;
-    }
-  }
-  const int incl = block_inclusive_scan(local, scan_s);
-  const int nv_incl = block_inclusive_scan(nvalid_local, scan_s);
-  int s = incl - local;
   int* perm = ws.perm + (size_t)b * n;
   int* seg_off = ws.seg_off + (size_t)b * (n + 1);
   int* seg_vox = ws.seg_vox + (size_t)b * n;
-  for (int p = p0; p < p1; p++) {
-    const unsigned long long kk = keys[p];
-    const unsigned v = (unsigned)(kk >> 32);
-    perm[p] = (int)(unsigned)(kk & 0xFFFFFFFFull);
-    if (v != 0xFFFFFFFFu && (p == 0 || (unsigned)(keys[p - 1] >> 32) != v)) {
-      seg_off[s] = p;
-      seg_vox[s] = (int)v;
-      atomicOr(&bm[v >> 5], 1u << (v & 31));
-      s++;
-    }
-  }
-  if (tid == nt - 1) {
-    ws.nseg[b] = incl;
-    seg_off[incl] = nv_incl;
-  }
-  __syncthreads();
-  PCR_STAMP(5);
-
-  // bitmap + per-word exclusive prefix of popcounts
-  const int wchunk = (W + nt - 1) / nt;
-  const int w0 = min(W, tid * wchunk), w1 = min(W, w0 + wchunk);
-  int pc = 0;
-  for (int w = w0; w < w1; w++) pc += __popc(bm[w]);
-  const int pincl = block_inclusive_scan(pc, scan_s);
-  int run = pincl - pc;
   unsigned* gbm = ws.bitmap + (size_t)b * W;
   int* gpre = ws.wprefix + (size_t)b * W;
-  for (int w = w0; w < w1; w++) {
-    const unsigned word = bm[w];
-    gbm[w] = word;
-    gpre[w] = run;
-    run += __popc(word);
+  int* pre_l = (int*)(bm + W);            // [W] word prefix
+  int* cnt_l = pre_l + W;                 // [n] points per occupied voxel
+  int* perm_l = cnt_l + n;                // [n] points grouped by voxel
+
+  // 1. occupancy bitmap
+  for (int i = tid; i < n; i += nt) cnt_l[i] = 0;
+#pragma unroll
+  for (int e = 0; e < kMaxE; e++) {
+    const unsigned v = (unsigned)(kv[e] >> 32);
+    if (e < E && v != 0xFFFFFFFFu) atomicOr(&bm[v >> 5], 1u << (v & 31));
   }
+  __syncthreads();
+  // 2. per-word exclusive prefix of popcounts (rank of a voxel among the
+  //    occupied ones == its segment id, segments in voxel order)
+  {
+    const int wchunk = (W + nt - 1) / nt;
+    const int w0 = min(W, tid * wchunk), w1 = min(W, w0 + wchunk);
+    int pc = 0;
+    for (int w = w0; w < w1; w++) pc += __popc(bm[w]);
+    const int pincl = block_inclusive_scan(pc, scan_s);
+    int run = pincl - pc;
+    for (int w = w0; w < w1; w++) {
+      const unsigned word = bm[w];
+      gbm[w] = word;
+      gpre[w] = run;
+      pre_l[w] = run;
+      run += __popc(word);
+    }
+    if (tid == nt - 1) s_stat[0] = __int_as_float(pincl);  // number of segments
+  }
+  __syncthreads();
+  const int nseg = __float_as_int(s_stat[0]);
+  // 3. counts per segment; arrival slot within the segment (unstable)
+  int seg_of[kMaxE], slot_of[kMaxE];
+#pragma unroll
+  for (int e = 0; e < kMaxE; e++) {
+    const unsigned v = (unsigned)(kv[e] >> 32);
+    seg_of[e] = -1;
+    if (e < E && v != 0xFFFFFFFFu) {
+      const unsigned bit = 1u << (v & 31);
+      const int sg = pre_l[v >> 5] + __popc(bm[v >> 5] & (bit - 1u));
+      seg_of[e] = sg;
+      slot_of[e] = atomicAdd(&cnt_l[sg], 1);
+      seg_vox[sg] = (int)v;
+    }
+  }
+  __syncthreads();
+  // 4. exclusive scan of the counts -> segment offsets; largest segment
+  int big = 0;
+  {
+    const int chunk = (nseg + nt - 1) / nt;
+    const int s0 = min(nseg, tid * chunk), s1 = min(nseg, s0 + chunk);
+    int sum = 0;
+    for (int q = s0; q < s1; q++) {
+      sum += cnt_l[q];
+      big = max(big, cnt_l[q]);
+    }
+    const int incl = block_inclusive_scan(sum, scan_s);
+    int run = incl - sum;
+    __syncthreads();
+    for (int q = s0; q < s1; q++) {
+      const int c = cnt_l[q];
+      cnt_l[q] = run;  // now the segment start
+      seg_off[q] = run;
+      run += c;
+    }
+    if (tid == nt - 1) {
+      ws.nseg[b] = nseg;
+      seg_off[nseg] = incl;
+      s_stat[1] = __int_as_float(incl);  // number of valid points
+    }
+  }
+  // 5. place the points, then restore ascending point order inside each
+  //    voxel (the order the means are accumulated in) with a per-voxel
+  //    insertion sort; a cloud with a crowded voxel takes the bitonic path
+  const int crowded = __syncthreads_or(big > 32);
+  if (!crowded) {
+#pragma unroll
+    for (int e = 0; e < kMaxE; e++)
+      if (seg_of[e] >= 0) perm_l[cnt_l[seg_of[e]] + slot_of[e]] = (int)(unsigned)(kv[e] & 0xFFFFFFFFull);
+    __syncthreads();
+    for (int q = tid; q < nseg; q += nt) {
+      const int o0 = cnt_l[q], o1 = (q + 1 < nseg) ? cnt_l[q + 1] : __float_as_int(s_stat[1]);
+      for (int x = o0 + 1; x < o1; x++) {
+        const int val = perm_l[x];
+        int y = x - 1;
+        while (y >= o0 && perm_l[y] > val) {
+          perm_l[y + 1] = perm_l[y];
+          y--;
+        }
+        perm_l[y + 1] = val;
+      }
+    }
+    __syncthreads();
+    const int nvalid = __float_as_int(s_stat[1]);
+    for (int p = tid; p < nvalid; p += nt) perm[p] = perm_l[p];
+  } else {
+    // unique 64-bit keys (the low word is the point id): sorting them is a
+    // stable sort by voxel
+    block_bitonic(kv, E, keys);
+#pragma unroll
+    for (int e = 0; e < kMaxE; e++)
+      if (e < E) keys[e * nt + tid] = kv[e];
+    __syncthreads();
+    for (int p = tid; p < n; p += nt) perm[p] = (int)(unsigned)(keys[p] & 0xFFFFFFFFull);
+  }
+  PCR_STAMP(4);
+  PCR_STAMP(5);
   PCR_STAMP(6);
 }
 
@@ -606,7 +661,7 @@ static pcr_status run_voxelize(const float* features, const float* coords_f, con
               name, ws_bytes, need);
   if (what & 1) {
     const int npad = next_pow2(n < kPrepThreads ? kPrepThreads : n);
-    size_t prep_smem = (size_t)npad * 8 + (size_t)ws.W * 4;
+    size_t prep_smem = (size_t)npad * 8 + (size_t)ws.W * 8 + (size_t)n * 8;
     PCR_REQUIRE(prep_smem <= 150 * 1024, "%s: prep LDS %zu too large", name, prep_smem);
     allow_big_lds(vox_prep_kernel<MODE>, prep_smem);
     hipLaunchKernelGGL(vox_prep_kernel<MODE>, dim3(b), dim3(kPrepThreads), prep_smem, stream,
