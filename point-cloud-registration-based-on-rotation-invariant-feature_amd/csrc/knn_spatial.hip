@@ -133,22 +133,43 @@ __global__ __launch_bounds__(kSortBlock) void knn_sort_kernel(const float* __res
     const float ext = frame[3 + a] - frame[a];
     sc[a] = (ext > 0.0f && ext < __builtin_inff()) ? 1023.0f / ext : 0.0f;
   }
-  unsigned long long kv[kMaxE];
+  // coarse counting sort on the top 12 Morton bits (16^3 cells).  The order
+  // inside a cell is arbitrary: KNN results never depend on the visiting
+  // order (keys are compared lexicographically), only its speed does.
+  int* hist = (int*)keys;     // [4096]
+  int* order = hist + 4096;   // [n]
+  __shared__ int scan_b[kSortBlock / kWave + 1];
+  for (int c = tid; c < 4096; c += kSortBlock) hist[c] = 0;
+  __syncthreads();
+  int cell[kMaxE], slot[kMaxE];
 #pragma unroll
   for (int e = 0; e < kMaxE; e++) {
     const int i = e * kSortBlock + tid;
-    kv[e] = ~0ull;
+    cell[e] = -1;
     if (e < E && i < n) {
       const unsigned code = spread10(quant10(px[e], lo[0], sc[0])) |
                             (spread10(quant10(py[e], lo[1], sc[1])) << 1) |
                             (spread10(quant10(pz[e], lo[2], sc[2])) << 2);
-      kv[e] = ((unsigned long long)code << 32) | (unsigned)i;
+      cell[e] = (int)(code >> 18);
+      slot[e] = atomicAdd(&hist[cell[e]], 1);
     }
   }
-  block_bitonic(kv, E, keys);
+  __syncthreads();
+  {
+    const int c0 = tid * 4;  // 4096 bins / 1024 threads
+    const int h0 = hist[c0], h1 = hist[c0 + 1], h2 = hist[c0 + 2], h3 = hist[c0 + 3];
+    const int sum = h0 + h1 + h2 + h3;
+    const int incl = block_inclusive_scan(sum, scan_b);
+    const int run = incl - sum;
+    hist[c0] = run;
+    hist[c0 + 1] = run + h0;
+    hist[c0 + 2] = run + h0 + h1;
+    hist[c0 + 3] = run + h0 + h1 + h2;
+  }
+  __syncthreads();
 #pragma unroll
   for (int e = 0; e < kMaxE; e++)
-    if (e < E) keys[e * kSortBlock + tid] = kv[e];
+    if (cell[e] >= 0) order[hist[cell[e]] + slot[e]] = e * kSortBlock + tid;
   __syncthreads();
   // sorted SoA + per-block boxes (one wave per block)
   const size_t base = (size_t)b * s.npad;
@@ -158,7 +179,7 @@ __global__ __launch_bounds__(kSortBlock) void knn_sort_kernel(const float* __res
     float x = __builtin_nanf(""), y = x, z = x;
     int j = -1;
     if (p < n) {
-      j = (int)(unsigned)(keys[p] & 0xFFFFFFFFull);
+      j = order[p];
       x = P[j];
       y = P[n + j];
       z = P[2 * n + j];
@@ -348,47 +369,55 @@ __global__ __launch_bounds__(256) void knn_block_kernel(
     thr_s[wv][lane] = top.kth();  // publish: an upper bound of the final k-th
   };
   const int gbase = wv - w;  // first wave of this query block
-  if (live) {
-    const float* boxes = cs.box + (size_t)b * cs.nblk * 8;
-    const size_t cbase = (size_t)b * cs.npad;
-    int home = (int)(((long long)qblk * cs.nblk) / qs.nblk);
-    if (home >= cs.nblk) home = cs.nblk - 1;
-    for (int rr = w; rr < cs.nblk; rr += NW) {
-      const int blk = visit_block(rr, home, cs.nblk);
-      // best bound known to any wave of this query block
-      float thr = top.kth();
+  const float* boxes = cs.box + (size_t)b * cs.nblk * 8;
+  const size_t cbase = (size_t)b * cs.npad;
+  int home = (int)(((long long)(live ? qblk : 0) * cs.nblk) / qs.nblk);
+  if (home >= cs.nblk) home = cs.nblk - 1;
+  auto scan_block = [&](int blk) {
+    // best bound known to any wave of this query block
+    float thr = top.kth();
 #pragma unroll
-      for (int o = 0; o < NW; o++) thr = fminf(thr, thr_s[gbase + o][lane]);
-      const float lb = box_lb(qx, qy, qz, boxes + (size_t)blk * 8);
-      if (!__any(lb <= thr)) continue;  // no lane can gain from this block
-      const size_t cp = cbase + (size_t)blk * kBlk + lane;
-      const float cx = cs.x[cp], cy = cs.y[cp], cz = cs.z[cp];
-      const int cj = cs.j[cp];
-      nproc++;
-      for (int t = 0; t < kBlk; t += 2) {
-        if (__any(qn > kQ - 2)) flush();
-        const float sx0 = readlane_f(cx, t), sy0 = readlane_f(cy, t), sz0 = readlane_f(cz, t);
-        const float sx1 = readlane_f(cx, t + 1), sy1 = readlane_f(cy, t + 1),
-                    sz1 = readlane_f(cz, t + 1);
-        const int sj0 = __builtin_amdgcn_readlane(cj, t);
-        const int sj1 = __builtin_amdgcn_readlane(cj, t + 1);
-        const float a0 = qx - sx0, b0 = qy - sy0, c0 = qz - sz0;
-        const float a1 = qx - sx1, b1 = qy - sy1, c1 = qz - sz1;
-        float d0 = a0 * a0, d1 = a1 * a1;
-        d0 = __builtin_fmaf(b0, b0, d0);
-        d1 = __builtin_fmaf(b1, b1, d1);
-        d0 = __builtin_fmaf(c0, c0, d0);
-        d1 = __builtin_fmaf(c1, c1, d1);
-        const unsigned long long k0 = make_key(d0, sj0), k1 = make_key(d1, sj1);
-        // keys above this wave's (stale) k-th, or farther than another
-        // wave's k-th distance, can never reach the final list
-        // branch-free append: slot qn is free (flushed above when < 2 left)
-        myq[qn * kBlk] = k0;
-        qn += (top.qualifies(k0) && d0 <= thr) ? 1 : 0;
-        myq[qn * kBlk] = k1;
-        qn += (top.qualifies(k1) && d1 <= thr) ? 1 : 0;
-      }
+    for (int o = 0; o < NW; o++) thr = fminf(thr, thr_s[gbase + o][lane]);
+    const float lb = box_lb(qx, qy, qz, boxes + (size_t)blk * 8);
+    if (!__any(lb <= thr)) return;  // no lane can gain from this block
+    const size_t cp = cbase + (size_t)blk * kBlk + lane;
+    const float cx = cs.x[cp], cy = cs.y[cp], cz = cs.z[cp];
+    const int cj = cs.j[cp];
+    nproc++;
+    for (int t = 0; t < kBlk; t += 2) {
+      if (__any(qn > kQ - 2)) flush();
+      const float sx0 = readlane_f(cx, t), sy0 = readlane_f(cy, t), sz0 = readlane_f(cz, t);
+      const float sx1 = readlane_f(cx, t + 1), sy1 = readlane_f(cy, t + 1),
+                  sz1 = readlane_f(cz, t + 1);
+      const int sj0 = __builtin_amdgcn_readlane(cj, t);
+      const int sj1 = __builtin_amdgcn_readlane(cj, t + 1);
+      const float a0 = qx - sx0, b0 = qy - sy0, c0 = qz - sz0;
+      const float a1 = qx - sx1, b1 = qy - sy1, c1 = qz - sz1;
+      float d0 = a0 * a0, d1 = a1 * a1;
+      d0 = __builtin_fmaf(b0, b0, d0);
+      d1 = __builtin_fmaf(b1, b1, d1);
+      d0 = __builtin_fmaf(c0, c0, d0);
+      d1 = __builtin_fmaf(c1, c1, d1);
+      const unsigned long long k0 = make_key(d0, sj0), k1 = make_key(d1, sj1);
+      // keys above this wave's (stale) k-th, or farther than another wave's
+      // k-th distance, can never reach the final list.  Branch-free append:
+      // slot qn is free (flushed above when fewer than 2 are left).
+      myq[qn * kBlk] = k0;
+      qn += (top.qualifies(k0) && d0 <= thr) ? 1 : 0;
+      myq[qn * kBlk] = k1;
+      qn += (top.qualifies(k1) && d1 <= thr) ? 1 : 0;
     }
+  };
+  // warm-up: wave 0 alone scans the home block and publishes its k-th
+  // distance, so the other waves start with a tight bound instead of each
+  // filling a list of its own from scratch
+  if (live && w == 0) {
+    scan_block(home);
+    if (__any(qn > 0)) flush();
+  }
+  if (NW > 1) __syncthreads();
+  if (live) {
+    for (int rr = (w == 0 ? NW : w); rr < cs.nblk; rr += NW) scan_block(visit_block(rr, home, cs.nblk));
     if (__any(qn > 0)) flush();
   }
   PCR_STAMP(1);
@@ -489,7 +518,7 @@ static int next_pow2i(int v) {
 
 static void launch_sort(const float* pts, int b, int n, const KnnSet& s, hipStream_t st) {
   const int npad_sort = next_pow2i(n < kSortBlock ? kSortBlock : n);
-  const size_t smem = (size_t)npad_sort * 8;
+  const size_t smem = 4096 * 4 + (size_t)n * 4;
   allow_big_lds(knn_sort_kernel, smem);
   hipLaunchKernelGGL(knn_sort_kernel, dim3(b), dim3(kSortBlock), smem, st, pts, n, npad_sort, s);
 }
