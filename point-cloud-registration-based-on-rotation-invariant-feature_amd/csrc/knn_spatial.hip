@@ -212,52 +212,53 @@ __global__ __launch_bounds__(kSortBlock) void knn_sort_kernel(const float* __res
 
 // Top-k in registers as packed keys (float bits of the squared distance << 32
 // | index).  Squared distances are >= +0 or NaN, so unsigned key order is the
-// lexicographic (distance, index) order and NaN sorts above the 10000
-// sentinel (never kept, as in the reference).  Valid region = the last k
-// slots; the first KMAX-k hold key 0 and are never displaced.
-template <int KMAX>
-struct TopKKey {
-  unsigned long long key[KMAX];
-  __device__ void init(int k) {
-    const unsigned long long undef = (unsigned long long)__float_as_uint(PCR_KNN_UNDEF) << 32;
-#pragma unroll
-    for (int q = 0; q < KMAX; q++) key[q] = (q < KMAX - k) ? 0ull : undef;
-  }
-  __device__ bool qualifies(unsigned long long x) const { return x < key[KMAX - 1]; }
-  __device__ float kth() const { return __uint_as_float((unsigned)(key[KMAX - 1] >> 32)); }
-  // Insert x into the sorted array, dropping the largest:
-  // new[q] = min(old[q], max(old[q-1], x)).  Every slot depends only on the
-  // old array, so the update has full instruction-level parallelism (the
-  // carry-chain form is a 32-deep dependent chain) and each lane mask dies
-  // right after its select.  A non-qualifying x leaves the array unchanged.
-  __device__ void insert(unsigned long long x) {
-#pragma unroll
-    for (int q = KMAX - 1; q > 0; q--) {
-      const unsigned long long hi = key[q - 1] > x ? key[q - 1] : x;
-      key[q] = key[q] < hi ? key[q] : hi;
-    }
-    key[0] = key[0] < x ? key[0] : x;
-  }
-};
+// lexicographic (distance, index) order.  The same 64 bits read as an IEEE
+// double have the same order (positive, non-NaN doubles order like their
+// bits), so compare-exchanges are one v_min_f64 + one v_max_f64 -- no lane
+// masks, no VCC hazards, full ILP -- instead of two 64-bit integer compares
+// and four selects.  Keys of NaN distances never enter the array (they fail
+// the `< k-th` test).  f64 denormals (distance 0 with small index) are
+// preserved by the default float mode.  Valid region = the last k slots; the
+// first KMAX-k hold +0.0 and are never displaced.
+typedef double kkey;
+#define PCR_KEY_PAD 1.7976931348623157e308  // DBL_MAX: above every real key
 
-__device__ inline unsigned long long make_key(float d, int j) {
-  return ((unsigned long long)__float_as_uint(d) << 32) | (unsigned)j;
+__device__ inline kkey make_key(float d, int j) {
+  return __longlong_as_double((long long)(((unsigned long long)__float_as_uint(d) << 32) |
+                                          (unsigned)j));
+}
+__device__ inline float key_dist(kkey k) {
+  return __uint_as_float((unsigned)((unsigned long long)__double_as_longlong(k) >> 32));
+}
+__device__ inline int key_idx(kkey k) {
+  return (int)(unsigned)((unsigned long long)__double_as_longlong(k) & 0xFFFFFFFFull);
 }
 
-__device__ inline void cex_up(unsigned long long& a, unsigned long long& b) {
-  const unsigned long long lo = a < b ? a : b;
-  const unsigned long long hi = a < b ? b : a;
+template <int KMAX>
+struct TopKKey {
+  kkey key[KMAX];
+  __device__ void init(int k) {
+    const kkey undef = make_key(PCR_KNN_UNDEF, 0);
+#pragma unroll
+    for (int q = 0; q < KMAX; q++) key[q] = (q < KMAX - k) ? 0.0 : undef;
+  }
+  __device__ bool qualifies(kkey x) const { return x < key[KMAX - 1]; }
+  __device__ float kth() const { return key_dist(key[KMAX - 1]); }
+};
+
+__device__ inline void cex_up(kkey& a, kkey& b) {
+  const kkey lo = __builtin_fmin(a, b);
+  const kkey hi = __builtin_fmax(a, b);
   a = lo;
   b = hi;
 }
 
 // Merge a batch of kQ (unsorted) keys into the sorted top-k array: bitonic
 // sort of the batch, C[i] = min(A[i], Q[K-1-i]) (the K smallest of A u Q as
-// a bitonic sequence), then a bitonic merge.  kQ*log2(kQ)^2/4 + kQ +
-// (K/2)*log2(K) compare-exchanges for kQ keys instead of kQ*K selects.
+// a bitonic sequence), then a bitonic merge.
 constexpr int kQ = 8;
 template <int KMAX>
-__device__ inline void merge_batch(unsigned long long (&key)[KMAX], unsigned long long (&q)[kQ]) {
+__device__ inline void merge_batch(kkey (&key)[KMAX], kkey (&q)[kQ]) {
 #pragma unroll
   for (int kk = 2; kk <= kQ; kk <<= 1) {
 #pragma unroll
@@ -275,7 +276,7 @@ __device__ inline void merge_batch(unsigned long long (&key)[KMAX], unsigned lon
     }
   }
 #pragma unroll
-  for (int i = KMAX - kQ; i < KMAX; i++) key[i] = key[i] < q[KMAX - 1 - i] ? key[i] : q[KMAX - 1 - i];
+  for (int i = KMAX - kQ; i < KMAX; i++) key[i] = __builtin_fmin(key[i], q[KMAX - 1 - i]);
 #pragma unroll
   for (int jj = KMAX >> 1; jj > 0; jj >>= 1) {
 #pragma unroll
@@ -337,8 +338,8 @@ __global__ __launch_bounds__(256) void knn_block_kernel(
   constexpr int kQBytes = 4 * kQ * kBlk * 8;
   constexpr int kLBytes = NW > 1 ? QPW * (NW / 2) * KMAX * kBlk * 8 : 8;
   __shared__ __align__(16) unsigned char lds_u[kQBytes > kLBytes ? kQBytes : kLBytes];
-  unsigned long long* qbuf = (unsigned long long*)lds_u;
-  unsigned long long* lst = (unsigned long long*)lds_u;
+  kkey* qbuf = (kkey*)lds_u;
+  kkey* lst = (kkey*)lds_u;
   __shared__ float thr_s[4][kBlk];
   const int b = blockIdx.y;
   const int wv = threadIdx.x >> 6;
@@ -351,18 +352,18 @@ __global__ __launch_bounds__(256) void knn_block_kernel(
   const int qj = live ? qs.j[qb] : -1;
   TopKKey<KMAX> top;
   top.init(k);
-  unsigned long long* myq = qbuf + wv * kQ * kBlk + lane;
+  kkey* myq = qbuf + wv * kQ * kBlk + lane;
   int qn = 0;
   thr_s[wv][lane] = PCR_KNN_UNDEF;
   __syncthreads();
   PCR_STAMP(0);
   int nflush = 0, nproc = 0;
   auto flush = [&]() {
-    unsigned long long qv[kQ];
+    kkey qv[kQ];
 #pragma unroll
     for (int s = 0; s < kQ; s++) qv[s] = myq[s * kBlk];
 #pragma unroll
-    for (int s = 0; s < kQ; s++) qv[s] = s < qn ? qv[s] : ~0ull;
+    for (int s = 0; s < kQ; s++) qv[s] = s < qn ? qv[s] : PCR_KEY_PAD;
     merge_batch<KMAX>(top.key, qv);
     qn = 0;
     nflush++;
@@ -398,7 +399,7 @@ __global__ __launch_bounds__(256) void knn_block_kernel(
       d1 = __builtin_fmaf(b1, b1, d1);
       d0 = __builtin_fmaf(c0, c0, d0);
       d1 = __builtin_fmaf(c1, c1, d1);
-      const unsigned long long k0 = make_key(d0, sj0), k1 = make_key(d1, sj1);
+      const kkey k0 = make_key(d0, sj0), k1 = make_key(d1, sj1);
       // keys above this wave's (stale) k-th, or farther than another wave's
       // k-th distance, can never reach the final list.  Branch-free append:
       // slot qn is free (flushed above when fewer than 2 are left).
@@ -437,19 +438,19 @@ __global__ __launch_bounds__(256) void knn_block_kernel(
   for (int half = NW / 2; half >= 1; half >>= 1) {
     __syncthreads();
     if (live && w >= half && w < 2 * half) {
-      unsigned long long* dst = lst + (size_t)((wv / NW) * (NW / 2) + (w - half)) * KMAX * kBlk;
+      kkey* dst = lst + (size_t)((wv / NW) * (NW / 2) + (w - half)) * KMAX * kBlk;
 #pragma unroll
       for (int s = 0; s < KMAX; s++) dst[s * kBlk + lane] = top.key[s];
     }
     __syncthreads();
     if (live && w < half) {
-      const unsigned long long* src = lst + (size_t)((wv / NW) * (NW / 2) + w) * KMAX * kBlk;
+      const kkey* src = lst + (size_t)((wv / NW) * (NW / 2) + w) * KMAX * kBlk;
       // C[i] = min(A[i], B[K-1-i]) then bitonic merge
 #pragma unroll
       for (int i = 0; i < KMAX; i++) {
-        const unsigned long long o =
-            (KMAX - 1 - i) < base ? ~0ull : src[(KMAX - 1 - i) * kBlk + lane];
-        top.key[i] = top.key[i] < o ? top.key[i] : o;
+        // partner's reals ascending then padding: B''[t] = B[base + t] (t < k)
+        const kkey o = i >= base ? src[(base + KMAX - 1 - i) * kBlk + lane] : PCR_KEY_PAD;
+        top.key[i] = __builtin_fmin(top.key[i], o);
       }
 #pragma unroll
       for (int jj = KMAX >> 1; jj > 0; jj >>= 1) {
@@ -468,14 +469,14 @@ __global__ __launch_bounds__(256) void knn_block_kernel(
     for (int s = 0; s < KMAX; s++) {
       if (s >= base) {
         const size_t o = ((size_t)b * k + (s - base)) * n + qj;
-        if (dist) dist[o] = __uint_as_float((unsigned)(top.key[s] >> 32));
-        idx[o] = (int)(unsigned)(top.key[s] & 0xFFFFFFFFull);
+        if (dist) dist[o] = key_dist(top.key[s]);
+        idx[o] = key_idx(top.key[s]);
       }
     }
   }
   if (PPF) {
     // every wave of the query block takes a share of the slots
-    unsigned long long* fin = lst + (size_t)(wv / NW) * KMAX * kBlk;
+    kkey* fin = lst + (size_t)(wv / NW) * KMAX * kBlk;
     if (NW > 1) {
       __syncthreads();  // merge reads of lst are complete
       if (live && w == 0) {
@@ -494,7 +495,7 @@ __global__ __launch_bounds__(256) void knn_block_kernel(
     const float cnx = qnr[qj], cny = qnr[qj + n], cnz = qnr[qj + 2 * n];
 #pragma unroll 1
     for (int slot = w; slot < k; slot += NW) {
-      const int jn = NW > 1 ? (int)(unsigned)(fin[(base + slot) * kBlk + lane] & 0xFFFFFFFFull)
+      const int jn = NW > 1 ? key_idx(fin[(base + slot) * kBlk + lane])
                             : idx[((size_t)b * k + slot) * n + qj];
       float o[4];
       pcr_local_ppf(ox, oy, oz, cnx, cny, cnz, cb[jn], cb[jn + m], cb[jn + 2 * m], nb[jn],
