@@ -64,10 +64,11 @@ static __device__ unsigned long long pcr_diag_stamps[1024][16];  // one copy per
   extern "C" int name(unsigned long long* host) {                                  \
     return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(pcr::pcr_diag_stamps), sizeof(pcr::pcr_diag_stamps)); \
   }
+#define PCR_WG_LINEAR (blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z))
 #define PCR_STAMP(p)                                                              \
   do {                                                                            \
-    if (threadIdx.x == 0 && blockIdx.x + gridDim.x * blockIdx.y < 1024)           \
-      pcr_diag_stamps[blockIdx.x + gridDim.x * blockIdx.y][p] = __builtin_amdgcn_s_memtime(); \
+    if (threadIdx.x == 0 && PCR_WG_LINEAR < 1024)                                 \
+      pcr_diag_stamps[PCR_WG_LINEAR][p] = __builtin_amdgcn_s_memtime();           \
   } while (0)
 #else
 #define PCR_STAMP(p) \

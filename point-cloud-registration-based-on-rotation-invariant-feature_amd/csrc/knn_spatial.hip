@@ -308,7 +308,9 @@ __device__ inline float box_lb(float qx, float qy, float qz, const float* bx) {
 // keeps its own top-k, and the lists are merged through LDS at the end.
 template <int KMAX>
 struct KnnNW {
-  static constexpr int value = KMAX <= 32 ? 4 : (KMAX <= 64 ? 2 : 1);
+  // waves per query block / waves per workgroup
+  static constexpr int value = KMAX <= 32 ? 8 : (KMAX <= 64 ? 2 : 1);
+  static constexpr int wg = KMAX <= 32 ? 8 : 4;
 };
 
 // r-th block of the visiting order home, home-1, home+1, home-2, ...
@@ -325,22 +327,23 @@ __device__ inline int visit_block(int r, int home, int nblk) {
 }
 
 template <int KMAX, bool PPF>
-__global__ __launch_bounds__(256) void knn_block_kernel(
+__global__ __launch_bounds__(KnnNW<KMAX>::wg * 64) void knn_block_kernel(
     KnnSet qs, KnnSet cs, int k, float* __restrict__ dist, int* __restrict__ idx,
     // fused local PPF: original candidate coords/normals and query normals
     const float* __restrict__ qxyz, const float* __restrict__ qnrm,
     const float* __restrict__ cxyz, const float* __restrict__ cnrm, int relative,
     float* __restrict__ ppf) {
   constexpr int NW = KnnNW<KMAX>::value;
-  constexpr int QPW = 4 / NW;  // query blocks per workgroup
+  constexpr int WGW = KnnNW<KMAX>::wg;  // waves per workgroup
+  constexpr int QPW = WGW / NW;          // query blocks per workgroup
   // LDS: the per-lane batches (scan phase) and the merge lists (merge / PPF
   // phase) are never live together -> one union
-  constexpr int kQBytes = 4 * kQ * kBlk * 8;
+  constexpr int kQBytes = WGW * kQ * kBlk * 8;
   constexpr int kLBytes = NW > 1 ? QPW * (NW / 2) * KMAX * kBlk * 8 : 8;
   __shared__ __align__(16) unsigned char lds_u[kQBytes > kLBytes ? kQBytes : kLBytes];
   kkey* qbuf = (kkey*)lds_u;
   kkey* lst = (kkey*)lds_u;
-  __shared__ float thr_s[4][kBlk];
+  __shared__ float thr_s[WGW][kBlk];
   const int b = blockIdx.y;
   const int wv = threadIdx.x >> 6;
   const int w = wv % NW;                       // wave within its query block
@@ -358,6 +361,7 @@ __global__ __launch_bounds__(256) void knn_block_kernel(
   __syncthreads();
   PCR_STAMP(0);
   int nflush = 0, nproc = 0;
+  kkey thr_key = top.key[KMAX - 1];
   auto flush = [&]() {
     kkey qv[kQ];
 #pragma unroll
@@ -368,6 +372,7 @@ __global__ __launch_bounds__(256) void knn_block_kernel(
     qn = 0;
     nflush++;
     thr_s[wv][lane] = top.kth();  // publish: an upper bound of the final k-th
+    thr_key = __builtin_fmin(thr_key, top.key[KMAX - 1]);
   };
   const int gbase = wv - w;  // first wave of this query block
   const float* boxes = cs.box + (size_t)b * cs.nblk * 8;
@@ -379,6 +384,11 @@ __global__ __launch_bounds__(256) void knn_block_kernel(
     float thr = top.kth();
 #pragma unroll
     for (int o = 0; o < NW; o++) thr = fminf(thr, thr_s[gbase + o][lane]);
+    // one key bound: below this wave's k-th key and at most the best k-th
+    // distance any wave of the query block has published
+    thr_key = __builtin_fmin(top.key[KMAX - 1],
+                             __longlong_as_double((long long)(((unsigned long long)
+                                 __float_as_uint(thr) << 32) | 0xFFFFFFFFull)));
     const float lb = box_lb(qx, qy, qz, boxes + (size_t)blk * 8);
     if (!__any(lb <= thr)) return;  // no lane can gain from this block
     const size_t cp = cbase + (size_t)blk * kBlk + lane;
@@ -404,9 +414,9 @@ __global__ __launch_bounds__(256) void knn_block_kernel(
       // k-th distance, can never reach the final list.  Branch-free append:
       // slot qn is free (flushed above when fewer than 2 are left).
       myq[qn * kBlk] = k0;
-      qn += (top.qualifies(k0) && d0 <= thr) ? 1 : 0;
+      qn += k0 < thr_key ? 1 : 0;
       myq[qn * kBlk] = k1;
-      qn += (top.qualifies(k1) && d1 <= thr) ? 1 : 0;
+      qn += k1 < thr_key ? 1 : 0;
     }
   };
   // warm-up: wave 0 alone scans the home block and publishes its k-th
@@ -425,9 +435,9 @@ __global__ __launch_bounds__(256) void knn_block_kernel(
   (void)nflush;
   (void)nproc;
 #ifdef PCR_DIAG
-  if (threadIdx.x == 0 && blockIdx.x + gridDim.x * blockIdx.y < 1024) {
-    pcr_diag_stamps[blockIdx.x + gridDim.x * blockIdx.y][8] = nflush;
-    pcr_diag_stamps[blockIdx.x + gridDim.x * blockIdx.y][9] = nproc;
+  if (threadIdx.x == 0 && PCR_WG_LINEAR < 1024) {
+    pcr_diag_stamps[PCR_WG_LINEAR][8] = nflush;
+    pcr_diag_stamps[PCR_WG_LINEAR][9] = nproc;
   }
 #endif
   // merge the NW lists of a query block: tree of bitonic merges through LDS.
@@ -528,8 +538,9 @@ template <int KM, bool PPF>
 static void launch_block_k(const KnnSet& qs, const KnnSet& cs, int b, int k, float* dist,
                            int* idx, const float* qxyz, const float* qnrm, const float* cxyz,
                            const float* cnrm, int relative, float* ppf, hipStream_t st) {
-  dim3 grid(ceil_div(qs.nblk, 4 / KnnNW<KM>::value), b);
-  hipLaunchKernelGGL((knn_block_kernel<KM, PPF>), grid, dim3(256), 0, st, qs, cs, k, dist, idx,
+  dim3 grid(ceil_div(qs.nblk, KnnNW<KM>::wg / KnnNW<KM>::value), b);
+  hipLaunchKernelGGL((knn_block_kernel<KM, PPF>), grid, dim3(KnnNW<KM>::wg * 64), 0, st, qs, cs, k,
+                     dist, idx,
                      qxyz, qnrm, cxyz, cnrm, relative, ppf);
 }
 

@@ -385,6 +385,7 @@ __global__ __launch_bounds__(kGridThreads) void vox_grid_kernel(
   const int c0 = grp * G;
   const int gcount = min(G, c - c0);
 
+  PCR_STAMP(8);
   const unsigned* gbm = ws.bitmap + (size_t)b * W;
   const int* gpre = ws.wprefix + (size_t)b * W;
   const int nseg = ws.nseg[b];
@@ -417,6 +418,7 @@ __global__ __launch_bounds__(kGridThreads) void vox_grid_kernel(
   }
   __syncthreads();
 
+  PCR_STAMP(9);
   // voxel means, ascending point order inside each voxel (spherical_vox.cu:112-116
   // accumulates feat * (1/cnt) in an arbitrary atomic order; the oracle and
   // this kernel both use ascending point order)
@@ -442,6 +444,7 @@ __global__ __launch_bounds__(kGridThreads) void vox_grid_kernel(
   }
   __syncthreads();
 
+  PCR_STAMP(10);
   // stream the [gcount, cell0..cell1) slab once; zeros included
   float* ob = out + ((size_t)b * c + c0) * r3;
   int* cb = (cnt_out && grp == 0) ? cnt_out + (size_t)b * r3 : nullptr;
@@ -487,6 +490,7 @@ __global__ __launch_bounds__(kGridThreads) void vox_grid_kernel(
     }
   }
 
+  PCR_STAMP(11);
   if (FUSED) {
     // spherical devoxelisation of this grid (spherical_trilinear_devox.cu:127-134)
     // evaluated from the LDS-resident means; requires one tile per cloud.
@@ -545,6 +549,7 @@ __global__ __launch_bounds__(kGridThreads) void vox_grid_kernel(
       }
     }
   }
+  PCR_STAMP(12);
 }
 
 // ------------------------------------------------------ backward gather

@@ -30,6 +30,7 @@ for _ in range(3):
 torch.cuda.synchronize()
 s = torch.cuda.current_stream().cuda_stream
 for name, fn, reader, nwg in (("vox_prep", lambda: ex.voxel_prep(xyz, s), lib.pcr_diag_read_vox, b),
+                              ("vox_grid", lambda: ex.voxel_grid(feat, s), lib.pcr_diag_read_vox, 512),
                               ("knn", lambda: ex.neighbor_stage(xyz, nrm, s), lib.pcr_diag_read_knn,
                                b * n // 64)):
     fn()
@@ -37,11 +38,15 @@ for name, fn, reader, nwg in (("vox_prep", lambda: ex.voxel_prep(xyz, s), lib.pc
     reader(buf)
     a = np.frombuffer(buf, dtype=np.uint64).reshape(1024, 16)[:min(nwg, 1024)].astype(np.int64)
     print(name, "workgroups", a.shape[0])
-    for p in range(1, 8):
+    for p in list(range(1, 8)) + list(range(9, 13)):
         d = a[:, p] - a[:, p - 1]
         ok = (a[:, p] > 0) & (a[:, p - 1] > 0)
         if ok.any():
             print("  phase %d->%d: median %d  max %d cycles" % (p - 1, p, np.median(d[ok]), d[ok].max()))
+    if name == "vox_grid":
+        t0 = a[:, 8][a[:, 8] > 0]
+        t1 = a[:, 12][a[:, 12] > 0]
+        print("  kernel span %d cycles; WG durations median %d" % (t1.max() - t0.min(), np.median(t1 - t0)))
     if name == "knn":
         print("  flushes/wave median %d max %d; blocks processed median %d max %d"
               % (np.median(a[:, 8]), a[:, 8].max(), np.median(a[:, 9]), a[:, 9].max()))
