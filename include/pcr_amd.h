@@ -186,17 +186,23 @@ pcr_status pcr_extractor_voxel_stage(const float *xyz, const float *features, in
                                      float *desc, void *workspace, size_t workspace_bytes,
                                      void *stream);
 
-/* The two launches of pcr_extractor_voxel_stage, separately (so a caller can
- * time the grid kernel with events on its stream): prep = normalise + index
- * + sort + corners; grid = means + dense grid/cnt + devox + descriptor.  The
- * workspace carries the prep results to the grid launch. */
+/* The launches of pcr_extractor_voxel_stage, separately, so a caller can run
+ * the grid and devox launches on two streams (they are independent once prep
+ * is done) and time the grid kernel with events on its stream:
+ *   prep  = normalise + voxel index + occupancy/segments + devox corners
+ *   grid  = voxel means -> dense grid [b,c,r^3] + cnt, written once
+ *   devox = voxel means -> spherical devoxelisation [b,c,n] + descriptor
+ * The workspace carries the prep results to the other two. */
 pcr_status pcr_extractor_voxel_prep(const float *xyz, int b, int n, int r, float *norm_coords,
                                     int *ind, int *dinds, float *dwgts, void *workspace,
                                     size_t workspace_bytes, void *stream);
 pcr_status pcr_extractor_voxel_grid(const float *features, int b, int c, int n, int r, int *cnt,
-                                    float *grid, float *devox, const int *dinds,
-                                    const float *dwgts, float *desc, void *workspace,
-                                    size_t workspace_bytes, void *stream);
+                                    float *grid, void *workspace, size_t workspace_bytes,
+                                    void *stream);
+pcr_status pcr_extractor_voxel_devox(const float *features, int b, int c, int n, int r,
+                                     float *devox, const int *dinds, const float *dwgts,
+                                     float *desc, void *workspace, size_t workspace_bytes,
+                                     void *stream);
 
 /* ------------------------------------------------------ self tests ------
  * Device evaluation of the shared bit-exact math (include/pcr_math.h) for

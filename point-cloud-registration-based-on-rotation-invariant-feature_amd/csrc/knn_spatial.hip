@@ -224,8 +224,10 @@ typedef double kkey;
 #define PCR_KEY_PAD 1.7976931348623157e308  // DBL_MAX: above every real key
 
 __device__ inline kkey make_key(float d, int j) {
-  return __longlong_as_double((long long)(((unsigned long long)__float_as_uint(d) << 32) |
-                                          (unsigned)j));
+  // sign cleared: a NaN distance (e.g. a NaN-padded candidate; subtraction
+  // flips the NaN's sign) must read as a huge positive key, never negative
+  return __longlong_as_double((long long)(((unsigned long long)(__float_as_uint(d) & 0x7FFFFFFFu)
+                                           << 32) | (unsigned)j));
 }
 __device__ inline float key_dist(kkey k) {
   return __uint_as_float((unsigned)((unsigned long long)__double_as_longlong(k) >> 32));

@@ -366,7 +366,8 @@ __global__ __launch_bounds__(kPrepThreads) void vox_prep_kernel(
 
 // ------------------------------------------------------------ grid kernel
 // One workgroup per (cell tile, channel group, cloud).
-template <bool FUSED>
+// PART: 1 = stream the grid (+cnt), 2 = devoxelise + descriptor, 3 = both.
+template <int PART>
 __global__ __launch_bounds__(kGridThreads) void vox_grid_kernel(
     const float* __restrict__ feat, int c, int n, int r3, int G, int tile_cells, VoxWs ws,
     float* __restrict__ out, int* __restrict__ cnt_out, const int* __restrict__ dinds,
@@ -448,7 +449,8 @@ __global__ __launch_bounds__(kGridThreads) void vox_grid_kernel(
   // stream the [gcount, cell0..cell1) slab once; zeros included
   float* ob = out + ((size_t)b * c + c0) * r3;
   int* cb = (cnt_out && grp == 0) ? cnt_out + (size_t)b * r3 : nullptr;
-  if ((r3 & 3) == 0) {
+  if (!(PART & 1)) {
+  } else if ((r3 & 3) == 0) {
     for (int base = cell0 + tid * 4; base < cell1; base += kGridThreads * 4) {
       const int wl = (base >> 5) - wb;
       const unsigned word = bm_s[wl];
@@ -491,7 +493,7 @@ __global__ __launch_bounds__(kGridThreads) void vox_grid_kernel(
   }
 
   PCR_STAMP(11);
-  if (FUSED) {
+  if (PART & 2) {
     // spherical devoxelisation of this grid (spherical_trilinear_devox.cu:127-134)
     // evaluated from the LDS-resident means; requires one tile per cloud.
     const int* I = dinds + (size_t)b * 8 * n;
@@ -672,7 +674,9 @@ static pcr_status run_voxelize(const float* features, const float* coords_f, con
     hipLaunchKernelGGL(vox_prep_kernel<MODE>, dim3(b), dim3(kPrepThreads), prep_smem, stream,
                        coords_f, coords_i, n, r, npad, norm_out, ind, ws, dinds, dwgts);
   }
-  if (what & 2) {
+  const bool do_grid = (what & 2) != 0;
+  const bool do_dev = (what & 4) != 0 && devox != nullptr;
+  if (do_grid || do_dev) {
     int G = 1;
     const int ngrp = c > 0 ? pick_groups(c, n, &G) : 1;
     // one tile covers the whole grid when its bitmap fits comfortably
@@ -681,19 +685,23 @@ static pcr_status run_voxelize(const float* features, const float* coords_f, con
     const int nw = (tile + 31) / 32 + 1;
     size_t smem = grid_smem_bytes(G, n, nw);
     PCR_REQUIRE(smem <= 150 * 1024, "%s: grid LDS %zu too large", name, smem);
-    allow_big_lds(vox_grid_kernel<true>, smem);
-    allow_big_lds(vox_grid_kernel<false>, smem);
-    if (devox) {
+    allow_big_lds(vox_grid_kernel<1>, smem);
+    allow_big_lds(vox_grid_kernel<2>, smem);
+    allow_big_lds(vox_grid_kernel<3>, smem);
+    if (do_dev) {
       PCR_REQUIRE(ntiles == 1, "%s: fused devoxelisation needs r^3 <= 65536", name);
       PCR_REQUIRE(c > 0, "%s: fused devoxelisation needs c > 0", name);
-      hipLaunchKernelGGL(vox_grid_kernel<true>, dim3(ntiles, ngrp, b), dim3(kGridThreads), smem,
-                         stream, features, c, n, r3, G, tile, ws, out, cnt, dinds, dwgts, devox,
-                         desc);
-    } else if (c > 0 || cnt) {
-      hipLaunchKernelGGL(vox_grid_kernel<false>, dim3(ntiles, ngrp, b), dim3(kGridThreads), smem,
-                         stream, features, c, n, r3, G, tile, ws, out, cnt, nullptr, nullptr,
-                         nullptr, nullptr);
     }
+    const dim3 grid(do_dev ? 1 : ntiles, ngrp, b);
+    if (do_grid && do_dev)
+      hipLaunchKernelGGL(vox_grid_kernel<3>, grid, dim3(kGridThreads), smem, stream, features, c,
+                         n, r3, G, tile, ws, out, cnt, dinds, dwgts, devox, desc);
+    else if (do_dev)
+      hipLaunchKernelGGL(vox_grid_kernel<2>, grid, dim3(kGridThreads), smem, stream, features, c,
+                         n, r3, G, tile, ws, nullptr, nullptr, dinds, dwgts, devox, desc);
+    else if (c > 0 || cnt)
+      hipLaunchKernelGGL(vox_grid_kernel<1>, grid, dim3(kGridThreads), smem, stream, features, c,
+                         n, r3, G, tile, ws, out, cnt, nullptr, nullptr, nullptr, nullptr);
   }
   return launch_status(name);
 }
@@ -764,16 +772,24 @@ extern "C" pcr_status pcr_extractor_voxel_prep(const float* xyz, int b, int n, i
 }
 
 extern "C" pcr_status pcr_extractor_voxel_grid(const float* features, int b, int c, int n, int r,
-                                               int* cnt, float* grid, float* devox,
-                                               const int* dinds, const float* dwgts, float* desc,
-                                               void* workspace, size_t workspace_bytes,
-                                               void* stream) {
-  PCR_REQUIRE(grid != nullptr && devox != nullptr && dinds != nullptr && dwgts != nullptr,
-              "extractor_voxel_grid: grid, devox, dinds, dwgts required");
+                                               int* cnt, float* grid, void* workspace,
+                                               size_t workspace_bytes, void* stream) {
+  PCR_REQUIRE(grid != nullptr, "extractor_voxel_grid: grid required");
   return run_voxelize<kSphNormalize>(features, nullptr, nullptr, b, c, n, r, grid, nullptr, cnt,
-                                     workspace, workspace_bytes, as_stream(stream), nullptr, devox,
-                                     const_cast<int*>(dinds), const_cast<float*>(dwgts), desc,
-                                     "extractor_voxel_grid", 2);
+                                     workspace, workspace_bytes, as_stream(stream), nullptr,
+                                     nullptr, nullptr, nullptr, nullptr, "extractor_voxel_grid", 2);
+}
+
+extern "C" pcr_status pcr_extractor_voxel_devox(const float* features, int b, int c, int n, int r,
+                                                float* devox, const int* dinds, const float* dwgts,
+                                                float* desc, void* workspace,
+                                                size_t workspace_bytes, void* stream) {
+  PCR_REQUIRE(devox != nullptr && dinds != nullptr && dwgts != nullptr,
+              "extractor_voxel_devox: devox, dinds, dwgts required");
+  return run_voxelize<kSphNormalize>(features, nullptr, nullptr, b, c, n, r, nullptr, nullptr,
+                                     nullptr, workspace, workspace_bytes, as_stream(stream), nullptr,
+                                     devox, const_cast<int*>(dinds), const_cast<float*>(dwgts),
+                                     desc, "extractor_voxel_devox", 4);
 }
 
 extern "C" pcr_status pcr_extractor_voxel_stage(const float* xyz, const float* features, int b,
@@ -787,7 +803,7 @@ extern "C" pcr_status pcr_extractor_voxel_stage(const float* xyz, const float* f
   PCR_REQUIRE(desc == nullptr || devox != nullptr, "extractor_voxel_stage: desc needs devox");
   return run_voxelize<kSphNormalize>(features, xyz, nullptr, b, c, n, r, grid, ind, cnt, workspace,
                                      workspace_bytes, as_stream(stream), norm_coords, devox,
-                                     dinds, dwgts, desc, "extractor_voxel_stage");
+                                     dinds, dwgts, desc, "extractor_voxel_stage", 7);
 }
 
 #ifdef PCR_DIAG

@@ -7,13 +7,16 @@ features [B,C,N], all resident on the GPU):
       = knn_forward_cuda + the model's local-PPF block
         (PVCNN/models/pvcnn_classify.py:252-269), fused in one kernel
   voxel stage (stream B): Spherical_Voxelization normalisation
-      (PVCNN/modules/spherical_vox.py:16-20) -> spherical_avg_voxelize
-      (grid [B,C,r^3], ind, cnt) -> spherical_trilinear_devoxelize of that grid
-      ([B,C,N] + inds/wgts) -> per-cloud descriptor (max over points) [B,C]
+      (PVCNN/modules/spherical_vox.py:16-20) + voxel index / occupancy (prep),
+      then spherical_avg_voxelize's dense grid [B,C,r^3] + cnt (grid kernel),
+      and on stream C the spherical_trilinear_devoxelize of that grid
+      ([B,C,N] + inds/wgts) + per-cloud descriptor (max over points) [B,C]
+      (devox kernel; it re-forms the voxel means in LDS instead of re-reading
+      the grid, so it runs beside the grid kernel)
 
-The two stages are independent, so they run on two HIP streams forked from
-and joined back to the caller's stream; the whole step is capturable into a
-hipGraph (``capture()`` / ``replay()``) so a step costs one graph launch.
+The stages run on HIP streams forked from and joined back to the caller's
+stream; the whole step is capturable into a hipGraph (``capture()`` /
+``replay()``) so a step costs one graph launch.
 """
 import torch
 
@@ -49,6 +52,7 @@ class SphExtractor:
                         device=dev)
         self.s_nbr = torch.cuda.Stream(device=dev)
         self.s_vox = torch.cuda.Stream(device=dev)
+        self.s_dev = torch.cuda.Stream(device=dev)
         self.graph = None
         self._static_in = None
 
@@ -73,11 +77,16 @@ class SphExtractor:
             "extractor_voxel_prep")
 
     def voxel_grid(self, features, stream):
-        """The dominant kernel (vox_grid_kernel<true>) on its own."""
+        """The dominant kernel (vox_grid_kernel<1>: means -> dense grid + cnt)."""
         _lib.check(_lib.load().pcr_extractor_voxel_grid(
             _ptr(features), self.b, self.c, self.n, self.r, _ptr(self.cnt), _ptr(self.grid),
-            _ptr(self.devox), _ptr(self.dinds), _ptr(self.dwgts), _ptr(self.desc), _ptr(self.ws),
-            self.ws.numel(), stream), "extractor_voxel_grid")
+            _ptr(self.ws), self.ws.numel(), stream), "extractor_voxel_grid")
+
+    def voxel_devox(self, features, stream):
+        _lib.check(_lib.load().pcr_extractor_voxel_devox(
+            _ptr(features), self.b, self.c, self.n, self.r, _ptr(self.devox), _ptr(self.dinds),
+            _ptr(self.dwgts), _ptr(self.desc), _ptr(self.ws), self.ws.numel(), stream),
+            "extractor_voxel_devox")
 
     def forward(self, xyz, normals, features):
         """Enqueue one step on the current stream (fork/join over two streams)."""
@@ -91,9 +100,14 @@ class SphExtractor:
         self.s_nbr.wait_stream(cur)
         self.s_vox.wait_stream(cur)
         self.neighbor_stage(xyz, normals, self.s_nbr.cuda_stream)
-        self.voxel_stage(xyz, features, self.s_vox.cuda_stream)
+        self.voxel_prep(xyz, self.s_vox.cuda_stream)
+        # grid streaming and devoxelisation only share the prep results
+        self.s_dev.wait_stream(self.s_vox)
+        self.voxel_grid(features, self.s_vox.cuda_stream)
+        self.voxel_devox(features, self.s_dev.cuda_stream)
         cur.wait_stream(self.s_nbr)
         cur.wait_stream(self.s_vox)
+        cur.wait_stream(self.s_dev)
         return self.outputs()
 
     def outputs(self):
@@ -125,12 +139,13 @@ class SphExtractor:
 
 
 def grid_kernel_bytes_per_cloud(n, r, c):
-    """Algorithmic HBM bytes of the dominant kernel (fused vox grid + devox +
-    descriptor) per cloud: features read 4CN, grid written 4C r^3, cnt
-    written 4 r^3, devox written 4CN, corner inds+wgts read 64N, descriptor
-    4C.  (The <= 80 hot grid cells devox reads come from LDS, not HBM.)"""
+    """Algorithmic HBM bytes of the dominant kernel (vox_grid_kernel<1>: the
+    spherical_avg_voxelize output) per cloud: features read
+    4CN, grid written 4C r^3, cnt written 4 r^3.  The prep metadata it also
+    reads (occupancy bitmap + word prefix r^3/4 bytes, segment offsets and
+    point order 8N) is not counted: it is an artefact of this design."""
     r3 = r ** 3
-    return 4 * c * n + 4 * c * r3 + 4 * r3 + 4 * c * n + 64 * n + 4 * c
+    return 4 * c * n + 4 * c * r3 + 4 * r3
 
 
 def algorithmic_bytes_per_cloud(n, k, r, c):
