@@ -13,7 +13,7 @@ GPU (torch.distributed, RCCL), the batch is sharded by cloud (weak scaling:
 (registration matching), overlapped on a side stream.
 
 Prints ONE JSON line (rank 0).  `roofline` prices the dominant kernel (the
-fused voxel-grid kernel) from its HIP-event-timed average duration;
+voxel-grid kernel, vox_grid_kernel<1>: dense [B,C,r^3] grid + cnt) from its HIP-event-timed average duration;
 `cpu_baseline` times the CPU restatement (oracle/, the "port") on a bounded
 sample of the same workload on this box's host cores.
 """
@@ -172,7 +172,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # dominant kernel: fused voxel-grid kernel, HIP events on its stream
+    # dominant kernel: voxel-grid kernel, HIP events on its stream
     s_k = ex.s_vox
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.kernel_iters)]
@@ -223,7 +223,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic,
-                     "kernel": "vox_grid_kernel<true> (fused sph-vox grid + devox + desc)",
+                     "kernel": "vox_grid_kernel<1> (sph-vox dense grid + cnt)",
                      "kernel_avg_ms": round(grid_avg_ms, 5),
                      "kernel_bytes_per_launch": grid_bytes},
         "step_algorithmic_GBps": round(step_bytes * world * args.steps / elapsed / 1e9, 1),

@@ -8,6 +8,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
+export TMPDIR=/tmp
 run() {  # name limit cmd...
   local name=$1 limit=$2; shift 2
   echo "=== $name ($(date +%T))"
@@ -27,7 +28,8 @@ for step in "$@"; do
     prof) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
           run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline ;;
     pmc)  run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --kernel-iters 5 --no-cpu-baseline --no-graph
-          run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --kernel-iters 5 --no-cpu-baseline --no-graph ;;
+          run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --kernel-iters 5 --no-cpu-baseline --no-graph
+          run pmc_json 60 python3 scripts/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc_traffic.json 32 1024 32 32 64 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""Turn the two rocprofv3 --pmc passes of scripts/gpu_steps.sh (FETCH_SIZE,
+WRITE_SIZE; separate passes, TCC slots) into profiles/pmc_traffic.json, the
+per-launch HBM bytes of the dominant kernel that bench.py reports as
+roofline.traffic.
+
+gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports half
+the bytes of a wide coalesced streaming read, so it is doubled; WRITE_SIZE is
+exact for 16-B-per-lane streaming stores (the grid kernel's float4 stores).
+Both counters are in KiB.
+  usage: scripts/pmc_traffic.py <fetch_dir> <write_dir> <out.json> B N K R C
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+KERNEL = "vox_grid_kernel<1>"
+
+
+def per_dispatch(d, counter):
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    if not files:
+        raise SystemExit(f"no counter_collection.csv under {d}")
+    acc = defaultdict(float)
+    for fn in files:
+        for row in csv.DictReader(open(fn)):
+            if KERNEL not in row.get("Kernel_Name", ""):
+                continue
+            if row.get("Counter_Name") != counter:
+                continue
+            acc[row["Dispatch_Id"]] += float(row["Counter_Value"])
+    if not acc:
+        raise SystemExit(f"no {counter} rows for {KERNEL} under {d}")
+    return list(acc.values())
+
+
+def main():
+    fd, wd, out = sys.argv[1:4]
+    cfg = [int(x) for x in sys.argv[4:9]]
+    f = per_dispatch(fd, "FETCH_SIZE")
+    w = per_dispatch(wd, "WRITE_SIZE")
+    fetch = 2.0 * sum(f) / len(f) * 1024.0
+    write = sum(w) / len(w) * 1024.0
+    res = {"kernel": KERNEL, "config": cfg,
+           "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
+           "grid_kernel_hbm_bytes_per_launch": fetch + write,
+           "dispatches": [len(f), len(w)],
+           "note": "FETCH_SIZE x2 (gfx950 half-count on wide streaming reads), WRITE_SIZE as is; KiB -> bytes"}
+    with open(out, "w") as fh:
+        json.dump(res, fh, indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
