@@ -518,6 +518,277 @@ __global__ __launch_bounds__(KnnNW<KMAX>::wg * 64) void knn_block_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// knn_select_kernel (k <= 32): threshold selection instead of per-wave top-k
+// lists.  One workgroup of NW waves serves 64 Morton-consecutive queries (one
+// per lane); the candidate blocks are dealt round-robin to the waves.
+//
+//  1. bound   D_q = min over candidate blocks holding >= k points of the
+//             largest distance from q to the block's box (the same rounding
+//             chain, so >= every candidate distance in it): at least k
+//             candidates lie within D_q, hence kth(q) <= D_q.
+//  2. count   histogram of every candidate distance in quarter-octave bins
+//             of d (float bits >> 21) over the kNB bins ending at D_q's bin
+//             (bin 0 takes everything below); LDS no-return atomics, one
+//             counter per (bin, lane) -> conflict-free.
+//  3. cut     first bin where the running count reaches k: every candidate
+//             with bits >> 21 <= that bin is collected (at most ~1.3 k for
+//             smooth clouds, kCap = 64 slots per query).
+//  4. collect each wave counts its qualifiers, a prefix over the waves gives
+//             its slot base, a second sweep writes the (d, index) keys.
+//  5. rank    the keys are unique; each wave ranks its share of the
+//             collected keys against all of them, a key of rank r < k is
+//             output slot r (and its local PPF is computed right there).
+// A query block where some query has no finite bound below 10000 (fewer than
+// k points, NaN / huge coordinates) or more than kCap collected keys
+// (duplicates, extreme clustering) takes the exact fallback: wave 0 runs the
+// reference's insertion scan with the list in LDS.  Both paths give the
+// reference's result: the k lexicographically smallest (d, index) with
+// d < 10000, unfilled slots (10000, 0).
+constexpr int kNB = 24;
+constexpr int kCap = 64;
+
+// Upper bound of the FMA-chain squared distance from q to any point of box.
+__device__ inline float box_ub(float qx, float qy, float qz, const float* bx) {
+  const float gx = fmaxf(fabsf(qx - bx[0]), fabsf(qx - bx[3]));
+  const float gy = fmaxf(fabsf(qy - bx[1]), fabsf(qy - bx[4]));
+  const float gz = fmaxf(fabsf(qz - bx[2]), fabsf(qz - bx[5]));
+  float d = gx * gx;
+  d = __builtin_fmaf(gy, gy, d);
+  d = __builtin_fmaf(gz, gz, d);
+  return d;
+}
+
+__device__ inline float cand_dist(float qx, float qy, float qz, float sx, float sy, float sz) {
+  const float a = qx - sx, bq = qy - sy, c = qz - sz;
+  float d = a * a;
+  d = __builtin_fmaf(bq, bq, d);
+  d = __builtin_fmaf(c, c, d);
+  return d;
+}
+
+template <int NW, bool PPF>
+__global__ __launch_bounds__(NW * 64) void knn_select_kernel(
+    KnnSet qs, KnnSet cs, int k, float* __restrict__ dist, int* __restrict__ idx,
+    const float* __restrict__ qxyz, const float* __restrict__ qnrm,
+    const float* __restrict__ cxyz, const float* __restrict__ cnrm, int relative,
+    float* __restrict__ ppf) {
+  // hist_s is dead once the cut is chosen; the per-wave counts reuse it
+  __shared__ unsigned hist_s[(kNB + 1) * kBlk];
+  __shared__ kkey buf_s[(kCap + 1) * kBlk];  // row kCap: sink of masked writes
+  __shared__ unsigned dest_s[kBlk];
+  int* wcnt_s = (int*)hist_s;  // [NW][kBlk]
+  static_assert(NW * kBlk <= (kNB + 1) * kBlk, "wave counts alias the histogram");
+  const int b = blockIdx.y;
+  const int qblk = blockIdx.x;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const size_t qb = (size_t)b * qs.npad + (size_t)qblk * kBlk + lane;
+  const float qx = qs.x[qb], qy = qs.y[qb], qz = qs.z[qb];
+  const int qj = qs.j[qb];
+  const bool qlive = qj >= 0;
+  const int m = cs.n;
+  const int nblk = cs.nblk;
+  const float* boxes = cs.box + (size_t)b * nblk * 8;
+  const size_t cbase = (size_t)b * cs.npad;
+
+  for (int i = threadIdx.x; i < (kNB + 1) * kBlk; i += NW * kBlk) hist_s[i] = 0u;
+  if (wv == 0) dest_s[lane] = 0x7F800000u;  // +inf
+  __syncthreads();
+
+  // 1. bound
+  {
+    float dq = __builtin_inff();
+    for (int blk = wv; blk < nblk; blk += NW) {
+      const int real = min(kBlk, m - blk * kBlk);
+      if (real >= k) dq = fminf(dq, box_ub(qx, qy, qz, boxes + (size_t)blk * 8));
+    }
+    atomicMin(&dest_s[lane], __float_as_uint(dq));  // NaN never wins: fminf drops it
+  }
+  __syncthreads();
+  const unsigned dbits = dest_s[lane];
+  bool fallback = __any(qlive && !(dbits < __float_as_uint(PCR_KNN_UNDEF)));
+  const int etop = (int)(dbits >> 21);
+  const int ebase = etop - (kNB - 1);
+  // smallest distance that is not counted (0 for padding lanes: they never
+  // keep a block alive)
+  const float ftop = (qlive && !fallback) ? __uint_as_float((unsigned)(etop + 1) << 21) : 0.0f;
+
+  // 2. count
+  if (!fallback) {
+    for (int blk = wv; blk < nblk; blk += NW) {
+      if (!__any(box_lb(qx, qy, qz, boxes + (size_t)blk * 8) < ftop)) continue;
+      const float* bx = cs.x + cbase + (size_t)blk * kBlk;
+      const float* by = cs.y + cbase + (size_t)blk * kBlk;
+      const float* bz = cs.z + cbase + (size_t)blk * kBlk;
+#pragma unroll 8
+      for (int t = 0; t < kBlk; t++) {
+        const float d = cand_dist(qx, qy, qz, bx[t], by[t], bz[t]);
+        int bin = (int)(__float_as_uint(d) >> 21) - ebase;
+        bin = bin < 0 ? 0 : (bin > kNB ? kNB : bin);  // kNB = not counted
+        __hip_atomic_fetch_add(&hist_s[bin * kBlk + lane], 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+  }
+  __syncthreads();
+
+  // 3. cut (every wave computes the same values for its 64 queries)
+  int total = 0;
+  unsigned ucut = 0u;
+  if (!fallback) {
+    int cum = 0, bstar = -1;
+#pragma unroll
+    for (int bin = 0; bin < kNB; bin++) {
+      cum += (int)hist_s[bin * kBlk + lane];
+      if (bstar < 0 && cum >= k) {
+        bstar = bin;
+        total = cum;
+      }
+    }
+    fallback = __any(qlive && (bstar < 0 || total > kCap));
+    if (qlive && !fallback) ucut = (unsigned)(ebase + bstar + 1) << 21;
+  }
+
+  if (!fallback) {
+    const float fcut = __uint_as_float(ucut);
+    // 4. collect: count, prefix over the waves, write
+    int mine = 0;
+    for (int blk = wv; blk < nblk; blk += NW) {
+      if (!__any(box_lb(qx, qy, qz, boxes + (size_t)blk * 8) < fcut)) continue;
+      const float* bx = cs.x + cbase + (size_t)blk * kBlk;
+      const float* by = cs.y + cbase + (size_t)blk * kBlk;
+      const float* bz = cs.z + cbase + (size_t)blk * kBlk;
+#pragma unroll 8
+      for (int t = 0; t < kBlk; t++)
+        mine += __float_as_uint(cand_dist(qx, qy, qz, bx[t], by[t], bz[t])) < ucut ? 1 : 0;
+    }
+    __syncthreads();  // histogram reads done before the counts overwrite it
+    wcnt_s[wv * kBlk + lane] = mine;
+    __syncthreads();
+    int slot = 0;
+    for (int w = 0; w < wv; w++) slot += wcnt_s[w * kBlk + lane];
+    for (int blk = wv; blk < nblk; blk += NW) {
+      if (!__any(box_lb(qx, qy, qz, boxes + (size_t)blk * 8) < fcut)) continue;
+      const float* bx = cs.x + cbase + (size_t)blk * kBlk;
+      const float* by = cs.y + cbase + (size_t)blk * kBlk;
+      const float* bz = cs.z + cbase + (size_t)blk * kBlk;
+      const int* bj = cs.j + cbase + (size_t)blk * kBlk;
+#pragma unroll 8
+      for (int t = 0; t < kBlk; t++) {
+        const float d = cand_dist(qx, qy, qz, bx[t], by[t], bz[t]);
+        const bool take = __float_as_uint(d) < ucut;
+        buf_s[(take ? slot : kCap) * kBlk + lane] = make_key(d, bj[t]);
+        slot += take ? 1 : 0;
+      }
+    }
+    __syncthreads();
+
+    // 5. rank
+    constexpr int kE = kCap / NW;  // collected keys ranked per wave
+    kkey key[kE];
+    int rank[kE];
+#pragma unroll
+    for (int e = 0; e < kE; e++) {
+      const int i = wv + e * NW;
+      key[e] = i < total ? buf_s[i * kBlk + lane] : PCR_KEY_PAD;
+      rank[e] = 0;
+    }
+    int tmax = total;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) tmax = max(tmax, __shfl_xor(tmax, off, kWave));
+    for (int j2 = 0; j2 < tmax; j2++) {
+      const kkey o = j2 < total ? buf_s[j2 * kBlk + lane] : PCR_KEY_PAD;
+#pragma unroll
+      for (int e = 0; e < kE; e++) rank[e] += o < key[e] ? 1 : 0;
+    }
+    if (!qlive) return;
+    const int n = qs.n;
+    float ox = 0.f, oy = 0.f, oz = 0.f, cnx = 0.f, cny = 0.f, cnz = 0.f;
+    if (PPF) {
+      const float* qo = qxyz + (size_t)b * 3 * n;
+      const float* qnr = qnrm + (size_t)b * 3 * n;
+      ox = qo[qj];
+      oy = qo[qj + n];
+      oz = qo[qj + 2 * n];
+      cnx = qnr[qj];
+      cny = qnr[qj + n];
+      cnz = qnr[qj + 2 * n];
+    }
+#pragma unroll
+    for (int e = 0; e < kE; e++) {
+      const int i = wv + e * NW;
+      if (i < total && rank[e] < k) {
+        const size_t o = ((size_t)b * k + rank[e]) * n + qj;
+        if (dist) dist[o] = key_dist(key[e]);
+        const int jn = key_idx(key[e]);
+        idx[o] = jn;
+        if (PPF) {
+          const float* cb = cxyz + (size_t)b * 3 * m;
+          const float* nb = cnrm + (size_t)b * 3 * m;
+          float f[4];
+          pcr_local_ppf(ox, oy, oz, cnx, cny, cnz, cb[jn], cb[jn + m], cb[jn + 2 * m], nb[jn],
+                        nb[jn + m], nb[jn + 2 * m], relative, f);
+#pragma unroll
+          for (int ch = 0; ch < 4; ch++)
+            ppf[(((size_t)b * 4 + ch) * k + rank[e]) * n + qj] = f[ch];
+        }
+      }
+    }
+    return;
+  }
+
+  // fallback: wave 0, reference insertion scan, list in LDS (rows 0..k-1)
+  if (wv != 0) return;
+  const kkey undef = make_key(PCR_KNN_UNDEF, 0);
+  for (int s = 0; s < k; s++) buf_s[s * kBlk + lane] = undef;
+  kkey kth = undef;
+  for (int blk = 0; blk < nblk; blk++) {
+    const float* bx = cs.x + cbase + (size_t)blk * kBlk;
+    const float* by = cs.y + cbase + (size_t)blk * kBlk;
+    const float* bz = cs.z + cbase + (size_t)blk * kBlk;
+    const int* bj = cs.j + cbase + (size_t)blk * kBlk;
+    for (int t = 0; t < kBlk; t++) {
+      const kkey x = make_key(cand_dist(qx, qy, qz, bx[t], by[t], bz[t]), bj[t]);
+      if (x < kth) {
+        int s = k - 1;
+        while (s > 0) {
+          const kkey p = buf_s[(s - 1) * kBlk + lane];
+          if (p < x) break;
+          buf_s[s * kBlk + lane] = p;
+          s--;
+        }
+        buf_s[s * kBlk + lane] = x;
+        kth = buf_s[(k - 1) * kBlk + lane];
+      }
+    }
+  }
+  if (!qlive) return;
+  const int n = qs.n;
+  for (int s = 0; s < k; s++) {
+    const kkey x = buf_s[s * kBlk + lane];
+    const size_t o = ((size_t)b * k + s) * n + qj;
+    if (dist) dist[o] = key_dist(x);
+    idx[o] = key_idx(x);
+  }
+  if (PPF) {
+    const float* qo = qxyz + (size_t)b * 3 * n;
+    const float* qnr = qnrm + (size_t)b * 3 * n;
+    const float* cb = cxyz + (size_t)b * 3 * m;
+    const float* nb = cnrm + (size_t)b * 3 * m;
+    const float ox = qo[qj], oy = qo[qj + n], oz = qo[qj + 2 * n];
+    const float cnx = qnr[qj], cny = qnr[qj + n], cnz = qnr[qj + 2 * n];
+    for (int s = 0; s < k; s++) {
+      const int jn = key_idx(buf_s[s * kBlk + lane]);
+      float f[4];
+      pcr_local_ppf(ox, oy, oz, cnx, cny, cnz, cb[jn], cb[jn + m], cb[jn + 2 * m], nb[jn],
+                    nb[jn + m], nb[jn + 2 * m], relative, f);
+#pragma unroll
+      for (int ch = 0; ch < 4; ch++) ppf[(((size_t)b * 4 + ch) * k + s) * n + qj] = f[ch];
+    }
+  }
+}
+
 size_t knn_ws_size(int b, int n, int m) {
   size_t off = knn_set_layout(b, n, nullptr, nullptr, 0);
   return knn_set_layout(b, m, nullptr, nullptr, off);
@@ -550,7 +821,11 @@ template <bool PPF>
 static pcr_status launch_block(const KnnSet& qs, const KnnSet& cs, int b, int k, float* dist,
                                int* idx, const float* qxyz, const float* qnrm, const float* cxyz,
                                const float* cnrm, int relative, float* ppf, hipStream_t st) {
-  if (k <= 16)
+  if (k <= 32) {
+    constexpr int NW = 8;
+    hipLaunchKernelGGL((knn_select_kernel<NW, PPF>), dim3(qs.nblk, b), dim3(NW * 64), 0, st, qs, cs,
+                       k, dist, idx, qxyz, qnrm, cxyz, cnrm, relative, ppf);
+  } else if (k <= 16)
     launch_block_k<16, PPF>(qs, cs, b, k, dist, idx, qxyz, qnrm, cxyz, cnrm, relative, ppf, st);
   else if (k <= 32)
     launch_block_k<32, PPF>(qs, cs, b, k, dist, idx, qxyz, qnrm, cxyz, cnrm, relative, ppf, st);
