@@ -532,8 +532,8 @@ __global__ __launch_bounds__(KnnNW<KMAX>::wg * 64) void knn_block_kernel(
 //             (bin 0 takes everything below); LDS no-return atomics, one
 //             counter per (bin, lane) -> conflict-free.
 //  3. cut     first bin where the running count reaches k: every candidate
-//             with bits >> 21 <= that bin is collected (at most ~1.3 k for
-//             smooth clouds, kCap = 64 slots per query).
+//             with bits >> 21 <= that bin is collected (~1.2-1.9 k for
+//             smooth clouds, kCap = 128 slots per query).
 //  4. collect each wave counts its qualifiers, a prefix over the waves gives
 //             its slot base, a second sweep writes the (d, index) keys.
 //  5. rank    the keys are unique; each wave ranks its share of the
@@ -546,7 +546,7 @@ __global__ __launch_bounds__(KnnNW<KMAX>::wg * 64) void knn_block_kernel(
 // reference's result: the k lexicographically smallest (d, index) with
 // d < 10000, unfilled slots (10000, 0).
 constexpr int kNB = 24;
-constexpr int kCap = 64;
+constexpr int kCap = 128;
 
 // Upper bound of the FMA-chain squared distance from q to any point of box.
 __device__ inline float box_ub(float qx, float qy, float qz, const float* bx) {
@@ -595,6 +595,7 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
   for (int i = threadIdx.x; i < (kNB + 1) * kBlk; i += NW * kBlk) hist_s[i] = 0u;
   if (wv == 0) dest_s[lane] = 0x7F800000u;  // +inf
   __syncthreads();
+  PCR_STAMP(0);
 
   // 1. bound
   {
@@ -614,6 +615,7 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
   // keep a block alive)
   const float ftop = (qlive && !fallback) ? __uint_as_float((unsigned)(etop + 1) << 21) : 0.0f;
 
+  PCR_STAMP(1);
   // 2. count
   if (!fallback) {
     for (int blk = wv; blk < nblk; blk += NW) {
@@ -633,6 +635,7 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
   }
   __syncthreads();
 
+  PCR_STAMP(2);
   // 3. cut (every wave computes the same values for its 64 queries)
   int total = 0;
   unsigned ucut = 0u;
@@ -649,6 +652,12 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     fallback = __any(qlive && (bstar < 0 || total > kCap));
     if (qlive && !fallback) ucut = (unsigned)(ebase + bstar + 1) << 21;
   }
+#ifdef PCR_DIAG
+  if (threadIdx.x == 0 && PCR_WG_LINEAR < 1024) {
+    pcr_diag_stamps[PCR_WG_LINEAR][8] = fallback ? 1 : 0;
+    pcr_diag_stamps[PCR_WG_LINEAR][9] = (unsigned long long)total;
+  }
+#endif
 
   if (!fallback) {
     const float fcut = __uint_as_float(ucut);
@@ -683,25 +692,39 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
       }
     }
     __syncthreads();
+    PCR_STAMP(3);
 
     // 5. rank
     constexpr int kE = kCap / NW;  // collected keys ranked per wave
     kkey key[kE];
     int rank[kE];
+    int tmax = total;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) tmax = max(tmax, __shfl_xor(tmax, off, kWave));
+    tmax = __builtin_amdgcn_readfirstlane(tmax);
 #pragma unroll
     for (int e = 0; e < kE; e++) {
       const int i = wv + e * NW;
       key[e] = i < total ? buf_s[i * kBlk + lane] : PCR_KEY_PAD;
       rank[e] = 0;
     }
-    int tmax = total;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) tmax = max(tmax, __shfl_xor(tmax, off, kWave));
+    // elements this wave holds: wv + e * NW < tmax
+    const int ne = (tmax - wv + NW - 1) / NW;
     for (int j2 = 0; j2 < tmax; j2++) {
       const kkey o = j2 < total ? buf_s[j2 * kBlk + lane] : PCR_KEY_PAD;
 #pragma unroll
-      for (int e = 0; e < kE; e++) rank[e] += o < key[e] ? 1 : 0;
+      for (int e = 0; e < kE; e++)
+        if (e < ne) rank[e] += o < key[e] ? 1 : 0;
     }
+    // scatter the winners to their output slots in LDS (rows 0..k-1), then
+    // every wave takes k / NW slots: output writes + local PPF
+    __syncthreads();  // all ranking reads of buf_s are done
+#pragma unroll
+    for (int e = 0; e < kE; e++) {
+      const int i = wv + e * NW;
+      if (e < ne && i < total && rank[e] < k) buf_s[rank[e] * kBlk + lane] = key[e];
+    }
+    __syncthreads();
     if (!qlive) return;
     const int n = qs.n;
     float ox = 0.f, oy = 0.f, oz = 0.f, cnx = 0.f, cny = 0.f, cnz = 0.f;
@@ -715,26 +738,24 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
       cny = qnr[qj + n];
       cnz = qnr[qj + 2 * n];
     }
+#pragma unroll 1
+    for (int slot = wv; slot < k; slot += NW) {
+      const kkey x = buf_s[slot * kBlk + lane];
+      const size_t o = ((size_t)b * k + slot) * n + qj;
+      if (dist) dist[o] = key_dist(x);
+      const int jn = key_idx(x);
+      idx[o] = jn;
+      if (PPF) {
+        const float* cb = cxyz + (size_t)b * 3 * m;
+        const float* nb = cnrm + (size_t)b * 3 * m;
+        float f[4];
+        pcr_local_ppf(ox, oy, oz, cnx, cny, cnz, cb[jn], cb[jn + m], cb[jn + 2 * m], nb[jn],
+                      nb[jn + m], nb[jn + 2 * m], relative, f);
 #pragma unroll
-    for (int e = 0; e < kE; e++) {
-      const int i = wv + e * NW;
-      if (i < total && rank[e] < k) {
-        const size_t o = ((size_t)b * k + rank[e]) * n + qj;
-        if (dist) dist[o] = key_dist(key[e]);
-        const int jn = key_idx(key[e]);
-        idx[o] = jn;
-        if (PPF) {
-          const float* cb = cxyz + (size_t)b * 3 * m;
-          const float* nb = cnrm + (size_t)b * 3 * m;
-          float f[4];
-          pcr_local_ppf(ox, oy, oz, cnx, cny, cnz, cb[jn], cb[jn + m], cb[jn + 2 * m], nb[jn],
-                        nb[jn + m], nb[jn + 2 * m], relative, f);
-#pragma unroll
-          for (int ch = 0; ch < 4; ch++)
-            ppf[(((size_t)b * 4 + ch) * k + rank[e]) * n + qj] = f[ch];
-        }
+        for (int ch = 0; ch < 4; ch++) ppf[(((size_t)b * 4 + ch) * k + slot) * n + qj] = f[ch];
       }
     }
+    PCR_STAMP(4);
     return;
   }
 
@@ -821,7 +842,12 @@ template <bool PPF>
 static pcr_status launch_block(const KnnSet& qs, const KnnSet& cs, int b, int k, float* dist,
                                int* idx, const float* qxyz, const float* qnrm, const float* cxyz,
                                const float* cnrm, int relative, float* ppf, hipStream_t st) {
-  if (k <= 32) {
+#ifdef PCR_DIAG
+  static const int impl = getenv("PCR_KNN_IMPL") ? atoi(getenv("PCR_KNN_IMPL")) : 0;
+#else
+  constexpr int impl = 0;
+#endif
+  if (k <= 32 && impl == 0) {
     constexpr int NW = 8;
     hipLaunchKernelGGL((knn_select_kernel<NW, PPF>), dim3(qs.nblk, b), dim3(NW * 64), 0, st, qs, cs,
                        k, dist, idx, qxyz, qnrm, cxyz, cnrm, relative, ppf);

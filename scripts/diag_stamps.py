@@ -48,5 +48,5 @@ for name, fn, reader, nwg in (("vox_prep", lambda: ex.voxel_prep(xyz, s), lib.pc
         t1 = a[:, 12][a[:, 12] > 0]
         print("  kernel span %d cycles; WG durations median %d" % (t1.max() - t0.min(), np.median(t1 - t0)))
     if name == "knn":
-        print("  flushes/wave median %d max %d; blocks processed median %d max %d"
-              % (np.median(a[:, 8]), a[:, 8].max(), np.median(a[:, 9]), a[:, 9].max()))
+        print("  fallback blocks %d of %d; collected keys (lane 0) median %d max %d"
+              % (a[:, 8].sum(), a.shape[0], np.median(a[:, 9]), a[:, 9].max()))
