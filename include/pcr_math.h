@@ -139,16 +139,16 @@ PCR_HD double pcr_atan_core(double t) {
 }
 
 PCR_HD double pcr_acos_d(double x) {
+  /* three ranges, evaluated without branches (one polynomial, one sqrt):
+   *   |x| <= 0.5:  pi/2 - asin(x)
+   *   x > 0.5:     2 asin(sqrt((1 - x) / 2))
+   *   x < -0.5:    pi - 2 asin(sqrt((1 + x) / 2))   (also the NaN path)
+   * 1 - |x| is exactly the 1 - x resp. 1 + x of the branches. */
   double ax = __builtin_fabs(x);
-  if (ax <= 0.5) return PCR_PIO2 - pcr_asin_core(x);
-  if (x > 0.0) {
-    double s = __builtin_sqrt((1.0 - x) * 0.5);
-    return 2.0 * pcr_asin_core(s);
-  }
-  {
-    double s = __builtin_sqrt((1.0 + x) * 0.5); /* also the NaN path */
-    return PCR_PI - 2.0 * pcr_asin_core(s);
-  }
+  int mid = ax <= 0.5;
+  double s = mid ? x : __builtin_sqrt((1.0 - ax) * 0.5);
+  double p = pcr_asin_core(s);
+  return mid ? PCR_PIO2 - p : (x > 0.0 ? 2.0 * p : PCR_PI - 2.0 * p);
 }
 
 PCR_HD double pcr_atan_d(double x) {

@@ -521,7 +521,11 @@ __global__ __launch_bounds__(KnnNW<KMAX>::wg * 64) void knn_block_kernel(
 // ---------------------------------------------------------------------------
 // knn_select_kernel (k <= 32): threshold selection instead of per-wave top-k
 // lists.  One workgroup of NW waves serves 64 Morton-consecutive queries (one
-// per lane); the candidate blocks are dealt round-robin to the waves.
+// per lane); the candidate blocks are dealt round-robin to the waves.  At
+// N = 1024 no block can be skipped for a whole 64-query block (the 64 k-NN
+// balls cover most of the cloud), so every pass is a brute-force sweep over
+// the candidates, broadcast from SGPRs, two candidates per packed-fp32
+// instruction.
 //
 //  1. bound   D_q = min over candidate blocks holding >= k points of the
 //             largest distance from q to the block's box (the same rounding
@@ -529,16 +533,19 @@ __global__ __launch_bounds__(KnnNW<KMAX>::wg * 64) void knn_block_kernel(
 //             candidates lie within D_q, hence kth(q) <= D_q.
 //  2. count   histogram of every candidate distance in quarter-octave bins
 //             of d (float bits >> 21) over the kNB bins ending at D_q's bin
-//             (bin 0 takes everything below); LDS no-return atomics, one
-//             counter per (bin, lane) -> conflict-free.
+//             (bin 0 takes everything below).  One LDS counter per (bin,
+//             lane) holds CB-bit fields, one per wave, so the same no-return
+//             atomics also give every wave its own counts.
 //  3. cut     first bin where the running count reaches k: every candidate
 //             with bits >> 21 <= that bin is collected (~1.2-1.9 k for
-//             smooth clouds, kCap = 128 slots per query).
-//  4. collect each wave counts its qualifiers, a prefix over the waves gives
-//             its slot base, a second sweep writes the (d, index) keys.
-//  5. rank    the keys are unique; each wave ranks its share of the
-//             collected keys against all of them, a key of rank r < k is
-//             output slot r (and its local PPF is computed right there).
+//             smooth clouds, kCap slots per query).  A wave's slot base is
+//             the count of the waves before it, read from the fields.
+//  4. collect one sweep writes the (d, index) keys of the collected
+//             candidates into the wave's slots.
+//  5. rank    the keys are unique; each wave ranks its share of them against
+//             all; a key of rank r < k is output slot r.  Every wave then
+//             writes k / NW slots and their local PPF (neighbour loads issued
+//             for all its slots before any arithmetic).
 // A query block where some query has no finite bound below 10000 (fewer than
 // k points, NaN / huge coordinates) or more than kCap collected keys
 // (duplicates, extreme clustering) takes the exact fallback: wave 0 runs the
@@ -547,6 +554,9 @@ __global__ __launch_bounds__(KnnNW<KMAX>::wg * 64) void knn_block_kernel(
 // d < 10000, unfilled slots (10000, 0).
 constexpr int kNB = 24;
 constexpr int kCap = 128;
+constexpr int kSelMaxK = 32;
+
+typedef float pf2 __attribute__((ext_vector_type(2)));
 
 // Upper bound of the FMA-chain squared distance from q to any point of box.
 __device__ inline float box_ub(float qx, float qy, float qz, const float* bx) {
@@ -567,18 +577,36 @@ __device__ inline float cand_dist(float qx, float qy, float qz, float sx, float 
   return d;
 }
 
-template <int NW, bool PPF>
+// two candidates at once (v_pk_add / v_pk_mul / v_pk_fma_f32); per element
+// the same operations and roundings as cand_dist
+__device__ inline pf2 cand_dist2(pf2 qx, pf2 qy, pf2 qz, pf2 sx, pf2 sy, pf2 sz) {
+  const pf2 a = qx - sx, bq = qy - sy, c = qz - sz;
+  pf2 d = a * a;
+  d = __builtin_elementwise_fma(bq, bq, d);
+  d = __builtin_elementwise_fma(c, c, d);
+  return d;
+}
+
+template <int CB>
+__device__ inline unsigned field_sum(unsigned v) {
+  if (CB == 8) {
+    v = (v & 0x00FF00FFu) + ((v >> 8) & 0x00FF00FFu);
+    return (v & 0xFFFFu) + (v >> 16);
+  }
+  return (v & 0xFFFFu) + (v >> 16);
+}
+
+template <int NW, int CB, bool PPF>
 __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     KnnSet qs, KnnSet cs, int k, float* __restrict__ dist, int* __restrict__ idx,
     const float* __restrict__ qxyz, const float* __restrict__ qnrm,
     const float* __restrict__ cxyz, const float* __restrict__ cnrm, int relative,
     float* __restrict__ ppf) {
-  // hist_s is dead once the cut is chosen; the per-wave counts reuse it
-  __shared__ unsigned hist_s[(kNB + 1) * kBlk];
+  constexpr int FPD = 32 / CB;              // wave fields per counter dword
+  constexpr int NG = (NW + FPD - 1) / FPD;  // counter dwords per (bin, lane)
+  __shared__ unsigned hist_s[NG * (kNB + 1) * kBlk];
   __shared__ kkey buf_s[(kCap + 1) * kBlk];  // row kCap: sink of masked writes
   __shared__ unsigned dest_s[kBlk];
-  int* wcnt_s = (int*)hist_s;  // [NW][kBlk]
-  static_assert(NW * kBlk <= (kNB + 1) * kBlk, "wave counts alias the histogram");
   const int b = blockIdx.y;
   const int qblk = blockIdx.x;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -591,8 +619,9 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
   const int nblk = cs.nblk;
   const float* boxes = cs.box + (size_t)b * nblk * 8;
   const size_t cbase = (size_t)b * cs.npad;
+  const pf2 qx2 = {qx, qx}, qy2 = {qy, qy}, qz2 = {qz, qz};
 
-  for (int i = threadIdx.x; i < (kNB + 1) * kBlk; i += NW * kBlk) hist_s[i] = 0u;
+  for (int i = threadIdx.x; i < NG * (kNB + 1) * kBlk; i += NW * kBlk) hist_s[i] = 0u;
   if (wv == 0) dest_s[lane] = 0x7F800000u;  // +inf
   __syncthreads();
   PCR_STAMP(0);
@@ -618,18 +647,24 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
   PCR_STAMP(1);
   // 2. count
   if (!fallback) {
+    unsigned* hw = hist_s + (size_t)(wv / FPD) * (kNB + 1) * kBlk + lane;
+    const unsigned inc = 1u << ((wv % FPD) * CB);
     for (int blk = wv; blk < nblk; blk += NW) {
       if (!__any(box_lb(qx, qy, qz, boxes + (size_t)blk * 8) < ftop)) continue;
       const float* bx = cs.x + cbase + (size_t)blk * kBlk;
       const float* by = cs.y + cbase + (size_t)blk * kBlk;
       const float* bz = cs.z + cbase + (size_t)blk * kBlk;
 #pragma unroll 8
-      for (int t = 0; t < kBlk; t++) {
-        const float d = cand_dist(qx, qy, qz, bx[t], by[t], bz[t]);
-        int bin = (int)(__float_as_uint(d) >> 21) - ebase;
-        bin = bin < 0 ? 0 : (bin > kNB ? kNB : bin);  // kNB = not counted
-        __hip_atomic_fetch_add(&hist_s[bin * kBlk + lane], 1u, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_WORKGROUP);
+      for (int t = 0; t < kBlk; t += 2) {
+        const pf2 d = cand_dist2(qx2, qy2, qz2, pf2{bx[t], bx[t + 1]}, pf2{by[t], by[t + 1]},
+                                 pf2{bz[t], bz[t + 1]});
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+          int bin = (int)(__float_as_uint(d[h]) >> 21) - ebase;
+          bin = bin < 0 ? 0 : (bin > kNB ? kNB : bin);  // kNB = not counted
+          __hip_atomic_fetch_add(hw + bin * kBlk, inc, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
       }
     }
   }
@@ -637,20 +672,36 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
 
   PCR_STAMP(2);
   // 3. cut (every wave computes the same values for its 64 queries)
-  int total = 0;
+  int total = 0, slot = 0;
   unsigned ucut = 0u;
   if (!fallback) {
-    int cum = 0, bstar = -1;
+    unsigned cum[NG], cut[NG];
+#pragma unroll
+    for (int g = 0; g < NG; g++) cum[g] = cut[g] = 0u;
+    int bstar = -1;
 #pragma unroll
     for (int bin = 0; bin < kNB; bin++) {
-      cum += (int)hist_s[bin * kBlk + lane];
-      if (bstar < 0 && cum >= k) {
+      int tb = 0;
+#pragma unroll
+      for (int g = 0; g < NG; g++) {
+        cum[g] += hist_s[(g * (kNB + 1) + bin) * kBlk + lane];
+        tb += (int)field_sum<CB>(cum[g]);
+      }
+      if (bstar < 0 && tb >= k) {
         bstar = bin;
-        total = cum;
+        total = tb;
+#pragma unroll
+        for (int g = 0; g < NG; g++) cut[g] = cum[g];
       }
     }
     fallback = __any(qlive && (bstar < 0 || total > kCap));
     if (qlive && !fallback) ucut = (unsigned)(ebase + bstar + 1) << 21;
+    // slots of the waves before this one
+    const int mg = wv / FPD;
+    const unsigned below = (1u << ((wv % FPD) * CB)) - 1u;
+#pragma unroll
+    for (int g = 0; g < NG; g++)
+      slot += (int)field_sum<CB>(g < mg ? cut[g] : (g == mg ? (cut[g] & below) : 0u));
   }
 #ifdef PCR_DIAG
   if (threadIdx.x == 0 && PCR_WG_LINEAR < 1024) {
@@ -660,23 +711,8 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
 #endif
 
   if (!fallback) {
+    // 4. collect
     const float fcut = __uint_as_float(ucut);
-    // 4. collect: count, prefix over the waves, write
-    int mine = 0;
-    for (int blk = wv; blk < nblk; blk += NW) {
-      if (!__any(box_lb(qx, qy, qz, boxes + (size_t)blk * 8) < fcut)) continue;
-      const float* bx = cs.x + cbase + (size_t)blk * kBlk;
-      const float* by = cs.y + cbase + (size_t)blk * kBlk;
-      const float* bz = cs.z + cbase + (size_t)blk * kBlk;
-#pragma unroll 8
-      for (int t = 0; t < kBlk; t++)
-        mine += __float_as_uint(cand_dist(qx, qy, qz, bx[t], by[t], bz[t])) < ucut ? 1 : 0;
-    }
-    __syncthreads();  // histogram reads done before the counts overwrite it
-    wcnt_s[wv * kBlk + lane] = mine;
-    __syncthreads();
-    int slot = 0;
-    for (int w = 0; w < wv; w++) slot += wcnt_s[w * kBlk + lane];
     for (int blk = wv; blk < nblk; blk += NW) {
       if (!__any(box_lb(qx, qy, qz, boxes + (size_t)blk * 8) < fcut)) continue;
       const float* bx = cs.x + cbase + (size_t)blk * kBlk;
@@ -684,11 +720,15 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
       const float* bz = cs.z + cbase + (size_t)blk * kBlk;
       const int* bj = cs.j + cbase + (size_t)blk * kBlk;
 #pragma unroll 8
-      for (int t = 0; t < kBlk; t++) {
-        const float d = cand_dist(qx, qy, qz, bx[t], by[t], bz[t]);
-        const bool take = __float_as_uint(d) < ucut;
-        buf_s[(take ? slot : kCap) * kBlk + lane] = make_key(d, bj[t]);
-        slot += take ? 1 : 0;
+      for (int t = 0; t < kBlk; t += 2) {
+        const pf2 d = cand_dist2(qx2, qy2, qz2, pf2{bx[t], bx[t + 1]}, pf2{by[t], by[t + 1]},
+                                 pf2{bz[t], bz[t + 1]});
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+          const bool take = __float_as_uint(d[h]) < ucut;
+          buf_s[(take ? slot : kCap) * kBlk + lane] = make_key(d[h], bj[t + h]);
+          slot += take ? 1 : 0;
+        }
       }
     }
     __syncthreads();
@@ -702,22 +742,19 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) tmax = max(tmax, __shfl_xor(tmax, off, kWave));
     tmax = __builtin_amdgcn_readfirstlane(tmax);
+    const int ne = (tmax - wv + NW - 1) / NW;  // keys this wave holds: wv + e * NW < tmax
 #pragma unroll
     for (int e = 0; e < kE; e++) {
       const int i = wv + e * NW;
       key[e] = i < total ? buf_s[i * kBlk + lane] : PCR_KEY_PAD;
       rank[e] = 0;
     }
-    // elements this wave holds: wv + e * NW < tmax
-    const int ne = (tmax - wv + NW - 1) / NW;
     for (int j2 = 0; j2 < tmax; j2++) {
       const kkey o = j2 < total ? buf_s[j2 * kBlk + lane] : PCR_KEY_PAD;
 #pragma unroll
       for (int e = 0; e < kE; e++)
         if (e < ne) rank[e] += o < key[e] ? 1 : 0;
     }
-    // scatter the winners to their output slots in LDS (rows 0..k-1), then
-    // every wave takes k / NW slots: output writes + local PPF
     __syncthreads();  // all ranking reads of buf_s are done
 #pragma unroll
     for (int e = 0; e < kE; e++) {
@@ -726,33 +763,51 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     }
     __syncthreads();
     if (!qlive) return;
+
+    // output slots wv, wv + NW, ...
+    constexpr int SPW = (kSelMaxK + NW - 1) / NW;
     const int n = qs.n;
-    float ox = 0.f, oy = 0.f, oz = 0.f, cnx = 0.f, cny = 0.f, cnz = 0.f;
+    int jn[SPW];
+#pragma unroll
+    for (int u = 0; u < SPW; u++) {
+      const int sl = wv + u * NW;
+      jn[u] = 0;
+      if (sl < k) {
+        const kkey x = buf_s[sl * kBlk + lane];
+        const size_t o = ((size_t)b * k + sl) * n + qj;
+        jn[u] = key_idx(x);
+        if (dist) dist[o] = key_dist(x);
+        idx[o] = jn[u];
+      }
+    }
     if (PPF) {
       const float* qo = qxyz + (size_t)b * 3 * n;
       const float* qnr = qnrm + (size_t)b * 3 * n;
-      ox = qo[qj];
-      oy = qo[qj + n];
-      oz = qo[qj + 2 * n];
-      cnx = qnr[qj];
-      cny = qnr[qj + n];
-      cnz = qnr[qj + 2 * n];
-    }
-#pragma unroll 1
-    for (int slot = wv; slot < k; slot += NW) {
-      const kkey x = buf_s[slot * kBlk + lane];
-      const size_t o = ((size_t)b * k + slot) * n + qj;
-      if (dist) dist[o] = key_dist(x);
-      const int jn = key_idx(x);
-      idx[o] = jn;
-      if (PPF) {
-        const float* cb = cxyz + (size_t)b * 3 * m;
-        const float* nb = cnrm + (size_t)b * 3 * m;
-        float f[4];
-        pcr_local_ppf(ox, oy, oz, cnx, cny, cnz, cb[jn], cb[jn + m], cb[jn + 2 * m], nb[jn],
-                      nb[jn + m], nb[jn + 2 * m], relative, f);
+      const float* cb = cxyz + (size_t)b * 3 * m;
+      const float* nb = cnrm + (size_t)b * 3 * m;
+      const float ox = qo[qj], oy = qo[qj + n], oz = qo[qj + 2 * n];
+      const float cnx = qnr[qj], cny = qnr[qj + n], cnz = qnr[qj + 2 * n];
+      float nbr[SPW][6];
 #pragma unroll
-        for (int ch = 0; ch < 4; ch++) ppf[(((size_t)b * 4 + ch) * k + slot) * n + qj] = f[ch];
+      for (int u = 0; u < SPW; u++) {
+        const int j = jn[u];
+        nbr[u][0] = cb[j];
+        nbr[u][1] = cb[j + m];
+        nbr[u][2] = cb[j + 2 * m];
+        nbr[u][3] = nb[j];
+        nbr[u][4] = nb[j + m];
+        nbr[u][5] = nb[j + 2 * m];
+      }
+#pragma unroll
+      for (int u = 0; u < SPW; u++) {
+        const int sl = wv + u * NW;
+        if (sl < k) {
+          float f[4];
+          pcr_local_ppf(ox, oy, oz, cnx, cny, cnz, nbr[u][0], nbr[u][1], nbr[u][2], nbr[u][3],
+                        nbr[u][4], nbr[u][5], relative, f);
+#pragma unroll
+          for (int ch = 0; ch < 4; ch++) ppf[(((size_t)b * 4 + ch) * k + sl) * n + qj] = f[ch];
+        }
       }
     }
     PCR_STAMP(4);
@@ -762,7 +817,7 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
   // fallback: wave 0, reference insertion scan, list in LDS (rows 0..k-1)
   if (wv != 0) return;
   const kkey undef = make_key(PCR_KNN_UNDEF, 0);
-  for (int s = 0; s < k; s++) buf_s[s * kBlk + lane] = undef;
+  for (int s2 = 0; s2 < k; s2++) buf_s[s2 * kBlk + lane] = undef;
   kkey kth = undef;
   for (int blk = 0; blk < nblk; blk++) {
     const float* bx = cs.x + cbase + (size_t)blk * kBlk;
@@ -772,23 +827,23 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     for (int t = 0; t < kBlk; t++) {
       const kkey x = make_key(cand_dist(qx, qy, qz, bx[t], by[t], bz[t]), bj[t]);
       if (x < kth) {
-        int s = k - 1;
-        while (s > 0) {
-          const kkey p = buf_s[(s - 1) * kBlk + lane];
+        int s2 = k - 1;
+        while (s2 > 0) {
+          const kkey p = buf_s[(s2 - 1) * kBlk + lane];
           if (p < x) break;
-          buf_s[s * kBlk + lane] = p;
-          s--;
+          buf_s[s2 * kBlk + lane] = p;
+          s2--;
         }
-        buf_s[s * kBlk + lane] = x;
+        buf_s[s2 * kBlk + lane] = x;
         kth = buf_s[(k - 1) * kBlk + lane];
       }
     }
   }
   if (!qlive) return;
   const int n = qs.n;
-  for (int s = 0; s < k; s++) {
-    const kkey x = buf_s[s * kBlk + lane];
-    const size_t o = ((size_t)b * k + s) * n + qj;
+  for (int s2 = 0; s2 < k; s2++) {
+    const kkey x = buf_s[s2 * kBlk + lane];
+    const size_t o = ((size_t)b * k + s2) * n + qj;
     if (dist) dist[o] = key_dist(x);
     idx[o] = key_idx(x);
   }
@@ -799,15 +854,29 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     const float* nb = cnrm + (size_t)b * 3 * m;
     const float ox = qo[qj], oy = qo[qj + n], oz = qo[qj + 2 * n];
     const float cnx = qnr[qj], cny = qnr[qj + n], cnz = qnr[qj + 2 * n];
-    for (int s = 0; s < k; s++) {
-      const int jn = key_idx(buf_s[s * kBlk + lane]);
+    for (int s2 = 0; s2 < k; s2++) {
+      const int j = key_idx(buf_s[s2 * kBlk + lane]);
       float f[4];
-      pcr_local_ppf(ox, oy, oz, cnx, cny, cnz, cb[jn], cb[jn + m], cb[jn + 2 * m], nb[jn],
-                    nb[jn + m], nb[jn + 2 * m], relative, f);
+      pcr_local_ppf(ox, oy, oz, cnx, cny, cnz, cb[j], cb[j + m], cb[j + 2 * m], nb[j],
+                    nb[j + m], nb[j + 2 * m], relative, f);
 #pragma unroll
-      for (int ch = 0; ch < 4; ch++) ppf[(((size_t)b * 4 + ch) * k + s) * n + qj] = f[ch];
+      for (int ch = 0; ch < 4; ch++) ppf[(((size_t)b * 4 + ch) * k + s2) * n + qj] = f[ch];
     }
   }
+}
+
+template <int NW, bool PPF>
+static void launch_select(const KnnSet& qs, const KnnSet& cs, int b, int k, float* dist,
+                          int* idx, const float* qxyz, const float* qnrm, const float* cxyz,
+                          const float* cnrm, int relative, float* ppf, hipStream_t st) {
+  // a wave sees ceil(nblk / NW) * 64 candidates: byte fields when that fits
+  const int per_wave = ceil_div(cs.nblk, NW) * kBlk;
+  if (per_wave <= 255)
+    hipLaunchKernelGGL((knn_select_kernel<NW, 8, PPF>), dim3(qs.nblk, b), dim3(NW * 64), 0, st,
+                       qs, cs, k, dist, idx, qxyz, qnrm, cxyz, cnrm, relative, ppf);
+  else
+    hipLaunchKernelGGL((knn_select_kernel<NW, 16, PPF>), dim3(qs.nblk, b), dim3(NW * 64), 0, st,
+                       qs, cs, k, dist, idx, qxyz, qnrm, cxyz, cnrm, relative, ppf);
 }
 
 size_t knn_ws_size(int b, int n, int m) {
@@ -847,10 +916,8 @@ static pcr_status launch_block(const KnnSet& qs, const KnnSet& cs, int b, int k,
 #else
   constexpr int impl = 0;
 #endif
-  if (k <= 32 && impl == 0) {
-    constexpr int NW = 8;
-    hipLaunchKernelGGL((knn_select_kernel<NW, PPF>), dim3(qs.nblk, b), dim3(NW * 64), 0, st, qs, cs,
-                       k, dist, idx, qxyz, qnrm, cxyz, cnrm, relative, ppf);
+  if (k <= kSelMaxK && impl == 0) {
+    launch_select<8, PPF>(qs, cs, b, k, dist, idx, qxyz, qnrm, cxyz, cnrm, relative, ppf, st);
   } else if (k <= 16)
     launch_block_k<16, PPF>(qs, cs, b, k, dist, idx, qxyz, qnrm, cxyz, cnrm, relative, ppf, st);
   else if (k <= 32)

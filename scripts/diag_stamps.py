@@ -7,7 +7,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "point-cloud-registration-based-on-rotation-invariant-feature_amd")
-os.environ["PCR_AMD_LIB"] = os.path.join(PKG, "lib", "libpcr_amd_diag.so")
+os.environ.setdefault("PCR_AMD_LIB", os.path.join(PKG, "lib", "libpcr_amd_diag.so"))
 sys.path[:0] = [ROOT, PKG]
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
