@@ -524,8 +524,10 @@ __global__ __launch_bounds__(KnnNW<KMAX>::wg * 64) void knn_block_kernel(
 // per lane); the candidate blocks are dealt round-robin to the waves.  At
 // N = 1024 no block can be skipped for a whole 64-query block (the 64 k-NN
 // balls cover most of the cloud), so every pass is a brute-force sweep over
-// the candidates, broadcast from SGPRs, two candidates per packed-fp32
-// instruction.
+// the candidates, two per packed-fp32 instruction.  Clouds of <= kSelCache
+// points are staged in LDS once per workgroup and read as broadcast
+// ds_read_b128 (in-order LDS returns: no scalar-load round trip in the
+// loop); larger ones are read through scalar loads.
 //
 //  1. bound   D_q = min over candidate blocks holding >= k points of the
 //             largest distance from q to the block's box (the same rounding
@@ -553,7 +555,8 @@ __global__ __launch_bounds__(KnnNW<KMAX>::wg * 64) void knn_block_kernel(
 // reference's result: the k lexicographically smallest (d, index) with
 // d < 10000, unfilled slots (10000, 0).
 constexpr int kNB = 24;
-constexpr int kCap = 128;
+constexpr int kCap = 96;
+constexpr int kSelCache = 1024;  // candidates staged in LDS per workgroup
 constexpr int kSelMaxK = 32;
 
 typedef float pf2 __attribute__((ext_vector_type(2)));
@@ -596,7 +599,7 @@ __device__ inline unsigned field_sum(unsigned v) {
   return (v & 0xFFFFu) + (v >> 16);
 }
 
-template <int NW, int CB, bool PPF>
+template <int NW, int CB, bool CL, bool PPF>
 __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     KnnSet qs, KnnSet cs, int k, float* __restrict__ dist, int* __restrict__ idx,
     const float* __restrict__ qxyz, const float* __restrict__ qnrm,
@@ -607,6 +610,7 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
   __shared__ unsigned hist_s[NG * (kNB + 1) * kBlk];
   __shared__ kkey buf_s[(kCap + 1) * kBlk];  // row kCap: sink of masked writes
   __shared__ unsigned dest_s[kBlk];
+  __shared__ __align__(16) float cand_s[CL ? 3 * kSelCache : 4];  // x | y | z
   const int b = blockIdx.y;
   const int qblk = blockIdx.x;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -623,6 +627,27 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
 
   for (int i = threadIdx.x; i < NG * (kNB + 1) * kBlk; i += NW * kBlk) hist_s[i] = 0u;
   if (wv == 0) dest_s[lane] = 0x7F800000u;  // +inf
+  if (CL) {
+    const int np = cs.npad;
+    for (int i = threadIdx.x; i < np; i += NW * kBlk) {
+      cand_s[i] = cs.x[cbase + i];
+      cand_s[kSelCache + i] = cs.y[cbase + i];
+      cand_s[2 * kSelCache + i] = cs.z[cbase + i];
+    }
+  }
+  // four candidates of block blk from position t (t % 4 == 0)
+  auto cand4 = [&](int blk, int t, float4& X, float4& Y, float4& Z) {
+    const int o = blk * kBlk + t;
+    if (CL) {
+      X = *(const float4*)(cand_s + o);
+      Y = *(const float4*)(cand_s + kSelCache + o);
+      Z = *(const float4*)(cand_s + 2 * kSelCache + o);
+    } else {
+      X = *(const float4*)(cs.x + cbase + o);
+      Y = *(const float4*)(cs.y + cbase + o);
+      Z = *(const float4*)(cs.z + cbase + o);
+    }
+  };
   __syncthreads();
   PCR_STAMP(0);
 
@@ -651,15 +676,15 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     const unsigned inc = 1u << ((wv % FPD) * CB);
     for (int blk = wv; blk < nblk; blk += NW) {
       if (!__any(box_lb(qx, qy, qz, boxes + (size_t)blk * 8) < ftop)) continue;
-      const float* bx = cs.x + cbase + (size_t)blk * kBlk;
-      const float* by = cs.y + cbase + (size_t)blk * kBlk;
-      const float* bz = cs.z + cbase + (size_t)blk * kBlk;
-#pragma unroll 8
-      for (int t = 0; t < kBlk; t += 2) {
-        const pf2 d = cand_dist2(qx2, qy2, qz2, pf2{bx[t], bx[t + 1]}, pf2{by[t], by[t + 1]},
-                                 pf2{bz[t], bz[t + 1]});
+#pragma unroll 4
+      for (int t = 0; t < kBlk; t += 4) {
+        float4 X, Y, Z;
+        cand4(blk, t, X, Y, Z);
+        const pf2 d0 = cand_dist2(qx2, qy2, qz2, pf2{X.x, X.y}, pf2{Y.x, Y.y}, pf2{Z.x, Z.y});
+        const pf2 d1 = cand_dist2(qx2, qy2, qz2, pf2{X.z, X.w}, pf2{Y.z, Y.w}, pf2{Z.z, Z.w});
+        const float d[4] = {d0[0], d0[1], d1[0], d1[1]};
 #pragma unroll
-        for (int h = 0; h < 2; h++) {
+        for (int h = 0; h < 4; h++) {
           int bin = (int)(__float_as_uint(d[h]) >> 21) - ebase;
           bin = bin < 0 ? 0 : (bin > kNB ? kNB : bin);  // kNB = not counted
           __hip_atomic_fetch_add(hw + bin * kBlk, inc, __ATOMIC_RELAXED,
@@ -715,16 +740,16 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     const float fcut = __uint_as_float(ucut);
     for (int blk = wv; blk < nblk; blk += NW) {
       if (!__any(box_lb(qx, qy, qz, boxes + (size_t)blk * 8) < fcut)) continue;
-      const float* bx = cs.x + cbase + (size_t)blk * kBlk;
-      const float* by = cs.y + cbase + (size_t)blk * kBlk;
-      const float* bz = cs.z + cbase + (size_t)blk * kBlk;
       const int* bj = cs.j + cbase + (size_t)blk * kBlk;
-#pragma unroll 8
-      for (int t = 0; t < kBlk; t += 2) {
-        const pf2 d = cand_dist2(qx2, qy2, qz2, pf2{bx[t], bx[t + 1]}, pf2{by[t], by[t + 1]},
-                                 pf2{bz[t], bz[t + 1]});
+#pragma unroll 4
+      for (int t = 0; t < kBlk; t += 4) {
+        float4 X, Y, Z;
+        cand4(blk, t, X, Y, Z);
+        const pf2 d0 = cand_dist2(qx2, qy2, qz2, pf2{X.x, X.y}, pf2{Y.x, Y.y}, pf2{Z.x, Z.y});
+        const pf2 d1 = cand_dist2(qx2, qy2, qz2, pf2{X.z, X.w}, pf2{Y.z, Y.w}, pf2{Z.z, Z.w});
+        const float d[4] = {d0[0], d0[1], d1[0], d1[1]};
 #pragma unroll
-        for (int h = 0; h < 2; h++) {
+        for (int h = 0; h < 4; h++) {
           const bool take = __float_as_uint(d[h]) < ucut;
           buf_s[(take ? slot : kCap) * kBlk + lane] = make_key(d[h], bj[t + h]);
           slot += take ? 1 : 0;
@@ -871,12 +896,16 @@ static void launch_select(const KnnSet& qs, const KnnSet& cs, int b, int k, floa
                           const float* cnrm, int relative, float* ppf, hipStream_t st) {
   // a wave sees ceil(nblk / NW) * 64 candidates: byte fields when that fits
   const int per_wave = ceil_div(cs.nblk, NW) * kBlk;
-  if (per_wave <= 255)
-    hipLaunchKernelGGL((knn_select_kernel<NW, 8, PPF>), dim3(qs.nblk, b), dim3(NW * 64), 0, st,
-                       qs, cs, k, dist, idx, qxyz, qnrm, cxyz, cnrm, relative, ppf);
+  const dim3 grid(qs.nblk, b), blk(NW * 64);
+  if (per_wave <= 255 && cs.npad <= kSelCache)
+    hipLaunchKernelGGL((knn_select_kernel<NW, 8, true, PPF>), grid, blk, 0, st, qs, cs, k, dist,
+                       idx, qxyz, qnrm, cxyz, cnrm, relative, ppf);
+  else if (per_wave <= 255)
+    hipLaunchKernelGGL((knn_select_kernel<NW, 8, false, PPF>), grid, blk, 0, st, qs, cs, k, dist,
+                       idx, qxyz, qnrm, cxyz, cnrm, relative, ppf);
   else
-    hipLaunchKernelGGL((knn_select_kernel<NW, 16, PPF>), dim3(qs.nblk, b), dim3(NW * 64), 0, st,
-                       qs, cs, k, dist, idx, qxyz, qnrm, cxyz, cnrm, relative, ppf);
+    hipLaunchKernelGGL((knn_select_kernel<NW, 16, false, PPF>), grid, blk, 0, st, qs, cs, k, dist,
+                       idx, qxyz, qnrm, cxyz, cnrm, relative, ppf);
 }
 
 size_t knn_ws_size(int b, int n, int m) {
