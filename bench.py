@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--steps-per-graph", type=int, default=10,
+                    help="pipelined steps captured per hipGraph (must divide --steps and --warmup)")
     return ap.parse_args()
 
 
@@ -122,24 +124,32 @@ def main():
     xyz, nrm, feat = synthetic_inputs(b, n, c, dev, seed=1234 + rank)
     ex = SphExtractor(b, n, c, k, r, device=dev)
 
+    # S pipelined steps per graph launch (one launch = S batches); S must
+    # divide the step counts so exactly --steps steps are timed
+    S = 1 if args.no_graph else max(1, args.steps_per_graph)
+    if args.steps % S or (args.warmup and args.warmup % S):
+        S = 1
     comm = torch.cuda.Stream(device=dev) if world > 1 else None
-    desc_out = [torch.empty((world * b, c), device=dev) for _ in range(2)]
-    desc_in = [torch.empty((b, c), device=dev) for _ in range(2)]
+    desc_out = [torch.empty((world * S * b, c), device=dev) for _ in range(2)]
+    desc_in = [torch.empty((S * b, c), device=dev) for _ in range(2)]
     pending = []
 
     if not args.no_graph:
-        ex.capture(xyz, nrm, feat)
+        ex.capture(xyz, nrm, feat, steps=S)
 
-    def step(s):
+    def launch(i):
+        """Steps i*S .. i*S+S-1: one graph replay (or S eager steps)."""
         if args.no_graph:
             ex.forward(xyz, nrm, feat)
+            src = ex.desc
         else:
             ex.replay()
+            src = ex.desc_steps.view(S * b, c)
         if world > 1:
-            # descriptor all-gather (registration matching), overlapped with
-            # the next step on a side stream; double-buffered
-            slot = s & 1
-            desc_in[slot].copy_(ex.desc)
+            # descriptor all-gather of the S batches (registration matching),
+            # overlapped with the next launch on a side stream; double-buffered
+            slot = i & 1
+            desc_in[slot].copy_(src)
             comm.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(comm):
                 pending.append(dist.all_gather_into_tensor(desc_out[slot], desc_in[slot],
@@ -147,8 +157,8 @@ def main():
             if len(pending) > 2:
                 pending.pop(0).wait()
 
-    for s in range(args.warmup):
-        step(s)
+    for i in range(args.warmup // S):
+        launch(i)
     for w in pending:
         w.wait()
     pending.clear()
@@ -157,8 +167,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for s in range(args.steps):
-        step(s)
+    for i in range(args.steps // S):
+        launch(i)
     for w in pending:
         w.wait()
     pending.clear()
@@ -219,7 +229,8 @@ def main():
                                "sph-vox r=%d^3 + sph-devox + descriptor" % (k, r),
                    "clouds_per_gpu": b, "points": n, "k": k, "resolution": r, "channels": c,
                    "global_batch": b * world, "parallelism": "dp%d (clouds sharded, "
-                   "descriptor all-gather)" % world, "graph": not args.no_graph},
+                   "descriptor all-gather)" % world, "graph": not args.no_graph,
+                   "steps_per_graph": S},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic,

@@ -15,8 +15,9 @@ features [B,C,N], all resident on the GPU):
       the grid, so it runs beside the grid kernel)
 
 The stages run on HIP streams forked from and joined back to the caller's
-stream; the whole step is capturable into a hipGraph (``capture()`` /
-``replay()``) so a step costs one graph launch.
+stream.  ``capture(steps=S)`` records S consecutive steps into one hipGraph
+with no join between them, so step i+1's neighbour stage overlaps step i's
+voxel stage and S steps cost one graph launch.
 """
 import torch
 
@@ -82,32 +83,50 @@ class SphExtractor:
             _ptr(features), self.b, self.c, self.n, self.r, _ptr(self.cnt), _ptr(self.grid),
             _ptr(self.ws), self.ws.numel(), stream), "extractor_voxel_grid")
 
-    def voxel_devox(self, features, stream):
+    def voxel_devox(self, features, stream, desc=None):
+        d = self.desc if desc is None else desc
         _lib.check(_lib.load().pcr_extractor_voxel_devox(
             _ptr(features), self.b, self.c, self.n, self.r, _ptr(self.devox), _ptr(self.dinds),
-            _ptr(self.dwgts), _ptr(self.desc), _ptr(self.ws), self.ws.numel(), stream),
+            _ptr(self.dwgts), _ptr(d), _ptr(self.ws), self.ws.numel(), stream),
             "extractor_voxel_devox")
 
-    def forward(self, xyz, normals, features):
-        """Enqueue one step on the current stream (fork/join over two streams)."""
+    def _check_inputs(self, xyz, normals, features):
         for t, name in ((xyz, "xyz"), (normals, "normals"), (features, "features")):
             if not (t.is_cuda and t.is_contiguous() and t.dtype == torch.float32):
                 raise RuntimeError("%s must be a contiguous float CUDA tensor" % name)
         if tuple(xyz.shape) != (self.b, 3, self.n) or tuple(features.shape) != (self.b, self.c,
                                                                                   self.n):
             raise RuntimeError("input shape does not match the extractor configuration")
-        cur = torch.cuda.current_stream(self.device)
-        self.s_nbr.wait_stream(cur)
-        self.s_vox.wait_stream(cur)
+
+    def enqueue(self, xyz, normals, features, desc=None):
+        """Enqueue one step on the extractor's own streams, no fork/join.
+        Stream order carries the step-to-step dependencies, so consecutive
+        steps pipeline: step i+1's neighbour stage runs beside step i's voxel
+        stage.  The only cross-stream edges: devox after prep (it reads the
+        prep results) and the next prep after devox (prep overwrites them)."""
         self.neighbor_stage(xyz, normals, self.s_nbr.cuda_stream)
+        self.s_vox.wait_stream(self.s_dev)
         self.voxel_prep(xyz, self.s_vox.cuda_stream)
-        # grid streaming and devoxelisation only share the prep results
         self.s_dev.wait_stream(self.s_vox)
         self.voxel_grid(features, self.s_vox.cuda_stream)
-        self.voxel_devox(features, self.s_dev.cuda_stream)
-        cur.wait_stream(self.s_nbr)
-        cur.wait_stream(self.s_vox)
-        cur.wait_stream(self.s_dev)
+        self.voxel_devox(features, self.s_dev.cuda_stream, desc)
+
+    def _fork(self):
+        cur = torch.cuda.current_stream(self.device)
+        for st in (self.s_nbr, self.s_vox, self.s_dev):
+            st.wait_stream(cur)
+        return cur
+
+    def _join(self, cur):
+        for st in (self.s_nbr, self.s_vox, self.s_dev):
+            cur.wait_stream(st)
+
+    def forward(self, xyz, normals, features):
+        """Enqueue one step, forked from and joined back to the current stream."""
+        self._check_inputs(xyz, normals, features)
+        cur = self._fork()
+        self.enqueue(xyz, normals, features)
+        self._join(cur)
         return self.outputs()
 
     def outputs(self):
@@ -117,10 +136,14 @@ class SphExtractor:
             "dinds": self.dinds, "dwgts": self.dwgts, "desc": self.desc,
         }
 
-    # ---------------------------------------------------------------- graphs
-    def capture(self, xyz, normals, features):
-        """Capture one step into a hipGraph bound to these input tensors."""
+    def capture(self, xyz, normals, features, steps=1):
+        """Capture `steps` pipelined steps over these input tensors into one
+        hipGraph.  Step s writes its descriptor to desc_steps[s]; the other
+        outputs hold the last step's values."""
+        self._check_inputs(xyz, normals, features)
         self._static_in = (xyz, normals, features)
+        self.desc_steps = torch.empty((steps, self.b, self.c), dtype=torch.float32,
+                                      device=self.device)
         side = torch.cuda.Stream(device=self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(side):
@@ -129,8 +152,12 @@ class SphExtractor:
         torch.cuda.synchronize(self.device)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            self.forward(xyz, normals, features)
+            cur = self._fork()
+            for s in range(steps):
+                self.enqueue(xyz, normals, features, desc=self.desc_steps[s])
+            self._join(cur)
         self.graph = g
+        self.graph_steps = steps
         return g
 
     def replay(self):
