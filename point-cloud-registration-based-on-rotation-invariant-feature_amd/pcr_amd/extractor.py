@@ -98,14 +98,17 @@ class SphExtractor:
                                                                                   self.n):
             raise RuntimeError("input shape does not match the extractor configuration")
 
-    def enqueue(self, xyz, normals, features, desc=None):
+    def enqueue(self, xyz, normals, features, desc=None, first=True):
         """Enqueue one step on the extractor's own streams, no fork/join.
         Stream order carries the step-to-step dependencies, so consecutive
         steps pipeline: step i+1's neighbour stage runs beside step i's voxel
         stage.  The only cross-stream edges: devox after prep (it reads the
-        prep results) and the next prep after devox (prep overwrites them)."""
+        prep results) and the next prep after devox (prep overwrites them);
+        `first` = nothing of this extractor is pending on the streams since
+        the last fork (no previous devox to wait for)."""
         self.neighbor_stage(xyz, normals, self.s_nbr.cuda_stream)
-        self.s_vox.wait_stream(self.s_dev)
+        if not first:
+            self.s_vox.wait_stream(self.s_dev)
         self.voxel_prep(xyz, self.s_vox.cuda_stream)
         self.s_dev.wait_stream(self.s_vox)
         self.voxel_grid(features, self.s_vox.cuda_stream)
@@ -154,7 +157,7 @@ class SphExtractor:
         with torch.cuda.graph(g):
             cur = self._fork()
             for s in range(steps):
-                self.enqueue(xyz, normals, features, desc=self.desc_steps[s])
+                self.enqueue(xyz, normals, features, desc=self.desc_steps[s], first=s == 0)
             self._join(cur)
         self.graph = g
         self.graph_steps = steps
