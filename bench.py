@@ -48,9 +48,11 @@ def parse():
     ap.add_argument("--kernel-iters", type=int, default=50)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--steps-per-graph", type=int, default=10,
-                    help="pipelined steps captured per hipGraph (must divide --steps and --warmup)")
+    ap.add_argument("--mode", choices=("pipelined", "graph", "eager"), default="pipelined",
+                    help="pipelined: S steps enqueued with no join between them; graph: one "
+                         "hipGraph replay per step; eager: fork/join launches per step")
+    ap.add_argument("--steps-per-launch", type=int, default=10,
+                    help="pipelined steps per launch group (must divide --steps and --warmup)")
     return ap.parse_args()
 
 
@@ -126,7 +128,7 @@ def main():
 
     # S pipelined steps per graph launch (one launch = S batches); S must
     # divide the step counts so exactly --steps steps are timed
-    S = 1 if args.no_graph else max(1, args.steps_per_graph)
+    S = max(1, args.steps_per_launch) if args.mode == "pipelined" else 1
     if args.steps % S or (args.warmup and args.warmup % S):
         S = 1
     comm = torch.cuda.Stream(device=dev) if world > 1 else None
@@ -134,17 +136,21 @@ def main():
     desc_in = [torch.empty((S * b, c), device=dev) for _ in range(2)]
     pending = []
 
-    if not args.no_graph:
-        ex.capture(xyz, nrm, feat, steps=S)
+    desc_steps = torch.empty((S, b, c), device=dev)
+    if args.mode == "graph":
+        ex.capture(xyz, nrm, feat)
 
     def launch(i):
-        """Steps i*S .. i*S+S-1: one graph replay (or S eager steps)."""
-        if args.no_graph:
-            ex.forward(xyz, nrm, feat)
+        """Steps i*S .. i*S+S-1."""
+        if args.mode == "pipelined":
+            ex.run_pipelined(xyz, nrm, feat, S, desc_steps)
+            src = desc_steps.view(S * b, c)
+        elif args.mode == "graph":
+            ex.replay()
             src = ex.desc
         else:
-            ex.replay()
-            src = ex.desc_steps.view(S * b, c)
+            ex.forward(xyz, nrm, feat)
+            src = ex.desc
         if world > 1:
             # descriptor all-gather of the S batches (registration matching),
             # overlapped with the next launch on a side stream; double-buffered
@@ -229,8 +235,8 @@ def main():
                                "sph-vox r=%d^3 + sph-devox + descriptor" % (k, r),
                    "clouds_per_gpu": b, "points": n, "k": k, "resolution": r, "channels": c,
                    "global_batch": b * world, "parallelism": "dp%d (clouds sharded, "
-                   "descriptor all-gather)" % world, "graph": not args.no_graph,
-                   "steps_per_graph": S},
+                   "descriptor all-gather)" % world, "launch": args.mode,
+                   "steps_per_launch": S},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic,

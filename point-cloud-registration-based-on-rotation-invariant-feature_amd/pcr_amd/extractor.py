@@ -15,9 +15,9 @@ features [B,C,N], all resident on the GPU):
       the grid, so it runs beside the grid kernel)
 
 The stages run on HIP streams forked from and joined back to the caller's
-stream.  ``capture(steps=S)`` records S consecutive steps into one hipGraph
-with no join between them, so step i+1's neighbour stage overlaps step i's
-voxel stage and S steps cost one graph launch.
+stream.  ``capture()`` records one step into a hipGraph; ``run_pipelined()``
+enqueues S consecutive steps with no join between them, so step i+1's
+neighbour stage overlaps step i's voxel stage.
 """
 import torch
 
@@ -139,14 +139,24 @@ class SphExtractor:
             "dinds": self.dinds, "dwgts": self.dwgts, "desc": self.desc,
         }
 
-    def capture(self, xyz, normals, features, steps=1):
-        """Capture `steps` pipelined steps over these input tensors into one
-        hipGraph.  Step s writes its descriptor to desc_steps[s]; the other
-        outputs hold the last step's values."""
+    def run_pipelined(self, xyz, normals, features, steps, desc_steps=None):
+        """Enqueue `steps` consecutive steps with no join between them (step
+        i+1's neighbour stage overlaps step i's voxel stage), forked from and
+        joined back to the current stream once.  Step s writes its descriptor
+        to desc_steps[s] when given.  Eager launches: ROCm's stream capture
+        does not take the prep-after-devox edge between two steps."""
+        self._check_inputs(xyz, normals, features)
+        cur = self._fork()
+        for s in range(steps):
+            d = None if desc_steps is None else desc_steps[s]
+            self.enqueue(xyz, normals, features, desc=d, first=s == 0)
+        self._join(cur)
+        return self.outputs()
+
+    def capture(self, xyz, normals, features):
+        """Capture one step over these input tensors into a hipGraph."""
         self._check_inputs(xyz, normals, features)
         self._static_in = (xyz, normals, features)
-        self.desc_steps = torch.empty((steps, self.b, self.c), dtype=torch.float32,
-                                      device=self.device)
         side = torch.cuda.Stream(device=self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(side):
@@ -156,11 +166,9 @@ class SphExtractor:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             cur = self._fork()
-            for s in range(steps):
-                self.enqueue(xyz, normals, features, desc=self.desc_steps[s], first=s == 0)
+            self.enqueue(xyz, normals, features)
             self._join(cur)
         self.graph = g
-        self.graph_steps = steps
         return g
 
     def replay(self):

@@ -25,10 +25,12 @@ for step in "$@"; do
     tests) run pytest_gpu 1200 python -m pytest tests -x -q -m gpu -p no:cacheprovider ;;
     tests_all) run pytest_gpu 1200 python -m pytest tests -q -m gpu -p no:cacheprovider ;;
     bench) run bench 600 python bench.py ;;
+    modes) run bench_graph 300 python bench.py --mode graph --no-cpu-baseline
+           run bench_eager 300 python bench.py --mode eager --no-cpu-baseline ;;
     prof) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
-          run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline ;;
-    pmc)  run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --kernel-iters 5 --no-cpu-baseline --no-graph
-          run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --kernel-iters 5 --no-cpu-baseline --no-graph
+          run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 50 --warmup 10 --no-cpu-baseline ;;
+    pmc)  run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --kernel-iters 5 --no-cpu-baseline --mode eager
+          run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --kernel-iters 5 --no-cpu-baseline --mode eager
           run pmc_json 60 python3 scripts/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc_traffic.json 32 1024 32 32 64 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

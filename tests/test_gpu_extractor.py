@@ -62,23 +62,23 @@ def test_extractor_graph_replay(dev):
 
 
 def test_extractor_pipelined_graph(dev):
-    """Several steps in one graph, no join between them (step i+1's KNN
-    overlaps step i's voxel stage): every step's descriptor and the final
-    outputs equal the single-step results."""
+    """Several steps with no join between them (step i+1's KNN overlaps step
+    i's voxel stage): every step's descriptor and the final outputs equal the
+    single-step results."""
     from pcr_amd.extractor import SphExtractor
     b, n, c, k, r = 8, 1024, 64, 32, 32
     xyz, nrm, feat = gaussian_clouds(b, n, seed=2, c=c)
     tx, tn, tf = T(xyz, dev), T(nrm, dev), T(feat, dev)
     ex = SphExtractor(b, n, c, k, r, device=dev)
     ref = {kk: v.clone() for kk, v in ex.forward(tx, tn, tf).items()}
-    ex.capture(tx, tn, tf, steps=4)
-    for _ in range(3):
-        out = ex.replay()
+    desc_steps = torch.empty((4, b, c), device=dev)
+    for _ in range(2):
+        out = ex.run_pipelined(tx, tn, tf, 4, desc_steps)
     torch.cuda.synchronize()
     for key, v in ref.items():
         assert torch.equal(out[key], v) or torch.allclose(out[key], v, equal_nan=True), key
     for s in range(4):
-        assert torch.equal(ex.desc_steps[s], ref["desc"]), s
+        assert torch.equal(desc_steps[s], ref["desc"]), s
 
 
 def test_extractor_full_size_properties(dev):
