@@ -583,6 +583,10 @@ __device__ inline float cand_dist(float qx, float qy, float qz, float sx, float 
 // two candidates at once (v_pk_add / v_pk_mul / v_pk_fma_f32); per element
 // the same operations and roundings as cand_dist
 __device__ inline pf2 cand_dist2(pf2 qx, pf2 qy, pf2 qz, pf2 sx, pf2 sy, pf2 sz) {
+#if defined(KNN_EXP) && KNN_EXP == 6
+  return pf2{cand_dist(qx[0], qy[0], qz[0], sx[0], sy[0], sz[0]),
+             cand_dist(qx[1], qy[1], qz[1], sx[1], sy[1], sz[1])};
+#endif
   const pf2 a = qx - sx, bq = qy - sy, c = qz - sz;
   pf2 d = a * a;
   d = __builtin_elementwise_fma(bq, bq, d);
@@ -611,6 +615,7 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
   __shared__ kkey buf_s[(kCap + 1) * kBlk];  // row kCap: sink of masked writes
   __shared__ unsigned dest_s[kBlk];
   __shared__ __align__(16) float cand_s[CL ? 3 * kSelCache : 4];  // x | y | z
+  __shared__ __align__(16) int cand_j[CL ? kSelCache : 4];
   const int b = blockIdx.y;
   const int qblk = blockIdx.x;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -631,22 +636,69 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     const int np = cs.npad;
     for (int i = threadIdx.x; i < np; i += NW * kBlk) {
       cand_s[i] = cs.x[cbase + i];
+      cand_j[i] = cs.j[cbase + i];
       cand_s[kSelCache + i] = cs.y[cbase + i];
       cand_s[2 * kSelCache + i] = cs.z[cbase + i];
     }
   }
-  // four candidates of block blk from position t (t % 4 == 0)
-  auto cand4 = [&](int blk, int t, float4& X, float4& Y, float4& Z) {
-    const int o = blk * kBlk + t;
+  // Visit every group of four candidates this wave owns: f(pos, d[4]), pos =
+  // sorted position of the group's first candidate.  Cached clouds: wave w
+  // owns candidates [64 b + w S, 64 b + w S + S) of every block b (S = 64 /
+  // NW), so the candidates near the queries -- the ones the collect pass
+  // keeps -- are spread over all waves; no pruning (at <= kSelCache points a
+  // 64-query block reaches nearly every candidate block).  The next group's
+  // LDS reads are issued before f runs, so their wait never covers the LDS
+  // atomics / stores f issues.  Larger clouds: whole blocks round-robin over
+  // the waves, skipped when no lane's box distance is below `lim`.
+  auto visit = [&](float lim, auto&& f) {
     if (CL) {
-      X = *(const float4*)(cand_s + o);
-      Y = *(const float4*)(cand_s + kSelCache + o);
-      Z = *(const float4*)(cand_s + 2 * kSelCache + o);
+      constexpr int S = kBlk / NW;
+      constexpr int GPB = S / 4;
+      static_assert(S % 4 == 0, "a wave owns whole groups of four");
+      const int ng = nblk * GPB;
+      auto off = [&](int g) { return (g / GPB) * kBlk + wv * S + (g % GPB) * 4; };
+      int o = off(0);
+      float4 X = *(const float4*)(cand_s + o);
+      float4 Y = *(const float4*)(cand_s + kSelCache + o);
+      float4 Z = *(const float4*)(cand_s + 2 * kSelCache + o);
+      for (int g = 0; g < ng; g++) {
+        const int on = off(g + 1 < ng ? g + 1 : g);
+        const float4 Xn = *(const float4*)(cand_s + on);
+        const float4 Yn = *(const float4*)(cand_s + kSelCache + on);
+        const float4 Zn = *(const float4*)(cand_s + 2 * kSelCache + on);
+        const pf2 d0 = cand_dist2(qx2, qy2, qz2, pf2{X.x, X.y}, pf2{Y.x, Y.y}, pf2{Z.x, Z.y});
+        const pf2 d1 = cand_dist2(qx2, qy2, qz2, pf2{X.z, X.w}, pf2{Y.z, Y.w}, pf2{Z.z, Z.w});
+        const float d[4] = {d0[0], d0[1], d1[0], d1[1]};
+        f(o, d);
+        o = on;
+        X = Xn;
+        Y = Yn;
+        Z = Zn;
+      }
     } else {
-      X = *(const float4*)(cs.x + cbase + o);
-      Y = *(const float4*)(cs.y + cbase + o);
-      Z = *(const float4*)(cs.z + cbase + o);
+      for (int blk = wv; blk < nblk; blk += NW) {
+        if (!__any(box_lb(qx, qy, qz, boxes + (size_t)blk * 8) < lim)) continue;
+        const float* bx = cs.x + cbase + (size_t)blk * kBlk;
+        const float* by = cs.y + cbase + (size_t)blk * kBlk;
+        const float* bz = cs.z + cbase + (size_t)blk * kBlk;
+#pragma unroll 4
+        for (int t = 0; t < kBlk; t += 4) {
+          const float4 X = *(const float4*)(bx + t);
+          const float4 Y = *(const float4*)(by + t);
+          const float4 Z = *(const float4*)(bz + t);
+          const pf2 d0 = cand_dist2(qx2, qy2, qz2, pf2{X.x, X.y}, pf2{Y.x, Y.y}, pf2{Z.x, Z.y});
+          const pf2 d1 = cand_dist2(qx2, qy2, qz2, pf2{X.z, X.w}, pf2{Y.z, Y.w}, pf2{Z.z, Z.w});
+          const float d[4] = {d0[0], d0[1], d1[0], d1[1]};
+          f(blk * kBlk + t, d);
+        }
+      }
     }
+  };
+  // original indices of the four candidates at sorted position pos
+  auto cand_idx4 = [&](int pos) {
+    if (CL) return *(const int4*)(cand_j + pos);
+    const int* bj = cs.j + cbase + pos;
+    return int4{bj[0], bj[1], bj[2], bj[3]};
   };
   __syncthreads();
   PCR_STAMP(0);
@@ -674,24 +726,25 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
   if (!fallback) {
     unsigned* hw = hist_s + (size_t)(wv / FPD) * (kNB + 1) * kBlk + lane;
     const unsigned inc = 1u << ((wv % FPD) * CB);
-    for (int blk = wv; blk < nblk; blk += NW) {
-      if (!__any(box_lb(qx, qy, qz, boxes + (size_t)blk * 8) < ftop)) continue;
-#pragma unroll 4
-      for (int t = 0; t < kBlk; t += 4) {
-        float4 X, Y, Z;
-        cand4(blk, t, X, Y, Z);
-        const pf2 d0 = cand_dist2(qx2, qy2, qz2, pf2{X.x, X.y}, pf2{Y.x, Y.y}, pf2{Z.x, Z.y});
-        const pf2 d1 = cand_dist2(qx2, qy2, qz2, pf2{X.z, X.w}, pf2{Y.z, Y.w}, pf2{Z.z, Z.w});
-        const float d[4] = {d0[0], d0[1], d1[0], d1[1]};
+#if defined(KNN_EXP) && KNN_EXP == 7
+    unsigned xacc = 0;
+#endif
+    visit(ftop, [&](int, const float (&d)[4]) {
 #pragma unroll
-        for (int h = 0; h < 4; h++) {
-          int bin = (int)(__float_as_uint(d[h]) >> 21) - ebase;
-          bin = bin < 0 ? 0 : (bin > kNB ? kNB : bin);  // kNB = not counted
-          __hip_atomic_fetch_add(hw + bin * kBlk, inc, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
+      for (int h = 0; h < 4; h++) {
+        int bin = (int)(__float_as_uint(d[h]) >> 21) - ebase;
+        bin = bin < 0 ? 0 : (bin > kNB ? kNB : bin);  // kNB = not counted
+#if defined(KNN_EXP) && KNN_EXP == 7
+        xacc += (unsigned)bin << (h * 5);
+#else
+        __hip_atomic_fetch_add(hw + bin * kBlk, inc, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
       }
-    }
+    });
+#if defined(KNN_EXP) && KNN_EXP == 7
+    if (xacc == 0x9e3779b9u) hw[0] = xacc;
+#endif
   }
   __syncthreads();
 
@@ -738,24 +791,21 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
   if (!fallback) {
     // 4. collect
     const float fcut = __uint_as_float(ucut);
-    for (int blk = wv; blk < nblk; blk += NW) {
-      if (!__any(box_lb(qx, qy, qz, boxes + (size_t)blk * 8) < fcut)) continue;
-      const int* bj = cs.j + cbase + (size_t)blk * kBlk;
-#pragma unroll 4
-      for (int t = 0; t < kBlk; t += 4) {
-        float4 X, Y, Z;
-        cand4(blk, t, X, Y, Z);
-        const pf2 d0 = cand_dist2(qx2, qy2, qz2, pf2{X.x, X.y}, pf2{Y.x, Y.y}, pf2{Z.x, Z.y});
-        const pf2 d1 = cand_dist2(qx2, qy2, qz2, pf2{X.z, X.w}, pf2{Y.z, Y.w}, pf2{Z.z, Z.w});
-        const float d[4] = {d0[0], d0[1], d1[0], d1[1]};
+    visit(fcut, [&](int pos, const float (&d)[4]) {
+      bool take[4];
+#pragma unroll
+      for (int h = 0; h < 4; h++) take[h] = __float_as_uint(d[h]) < ucut;
+      // most groups of four are taken by no lane: skip them uniformly
+      if (__any(take[0] | take[1] | take[2] | take[3])) {
+        const int4 jj = cand_idx4(pos);
+        const int j4[4] = {jj.x, jj.y, jj.z, jj.w};
 #pragma unroll
         for (int h = 0; h < 4; h++) {
-          const bool take = __float_as_uint(d[h]) < ucut;
-          buf_s[(take ? slot : kCap) * kBlk + lane] = make_key(d[h], bj[t + h]);
-          slot += take ? 1 : 0;
+          buf_s[(take[h] ? slot : kCap) * kBlk + lane] = make_key(d[h], j4[h]);
+          slot += take[h] ? 1 : 0;
         }
       }
-    }
+    });
     __syncthreads();
     PCR_STAMP(3);
 
@@ -780,6 +830,7 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
       for (int e = 0; e < kE; e++)
         if (e < ne) rank[e] += o < key[e] ? 1 : 0;
     }
+    PCR_STAMP(4);
     __syncthreads();  // all ranking reads of buf_s are done
 #pragma unroll
     for (int e = 0; e < kE; e++) {
@@ -787,6 +838,7 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
       if (e < ne && i < total && rank[e] < k) buf_s[rank[e] * kBlk + lane] = key[e];
     }
     __syncthreads();
+    PCR_STAMP(5);
     if (!qlive) return;
 
     // output slots wv, wv + NW, ...
@@ -835,7 +887,7 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
         }
       }
     }
-    PCR_STAMP(4);
+    PCR_STAMP(6);
     return;
   }
 
