@@ -31,6 +31,7 @@ namespace pcr {
 constexpr int kPrepThreads = kSortBlock;
 constexpr int kMaxSortN = kSortBlock * kMaxE;
 constexpr int kGridThreads = 256;
+constexpr int kDevoxThreads = 1024;
 constexpr int kMaxG = 8;
 
 enum PrepMode { kSphCoords = 0, kSphNormalize = 1, kCube = 2 };
@@ -367,8 +368,10 @@ __global__ __launch_bounds__(kPrepThreads) void vox_prep_kernel(
 // ------------------------------------------------------------ grid kernel
 // One workgroup per (cell tile, channel group, cloud).
 // PART: 1 = stream the grid (+cnt), 2 = devoxelise + descriptor, 3 = both.
-template <int PART>
-__global__ __launch_bounds__(kGridThreads) void vox_grid_kernel(
+// NT threads: 256 for the streaming parts; the devox-only part runs 1024
+// (one point per thread, so every corner load of a point is in flight at once).
+template <int PART, int NT>
+__global__ __launch_bounds__(NT) void vox_grid_kernel(
     const float* __restrict__ feat, int c, int n, int r3, int G, int tile_cells, VoxWs ws,
     float* __restrict__ out, int* __restrict__ cnt_out, const int* __restrict__ dinds,
     const float* __restrict__ dwgts, float* __restrict__ devox, float* __restrict__ desc) {
@@ -401,7 +404,7 @@ __global__ __launch_bounds__(kGridThreads) void vox_grid_kernel(
   unsigned* bm_s = (unsigned*)(scnt_s + n);
   int* pre_s = (int*)(bm_s + nw);
 
-  for (int w = tid; w < nw; w += kGridThreads) {
+  for (int w = tid; w < nw; w += NT) {
     bm_s[w] = gbm[wb + w];
     pre_s[w] = gpre[wb + w] - s_begin;
   }
@@ -411,11 +414,11 @@ __global__ __launch_bounds__(kGridThreads) void vox_grid_kernel(
     for (int g = 0; g < gcount; g++) {
       const float4* src = (const float4*)(fb + (size_t)g * n);
       float4* dst = (float4*)(feat_s + (size_t)g * n);
-      for (int i = tid; i < n4; i += kGridThreads) dst[i] = src[i];
+      for (int i = tid; i < n4; i += NT) dst[i] = src[i];
     }
   } else {
     for (int g = 0; g < gcount; g++)
-      for (int i = tid; i < n; i += kGridThreads) feat_s[(size_t)g * n + i] = fb[(size_t)g * n + i];
+      for (int i = tid; i < n; i += NT) feat_s[(size_t)g * n + i] = fb[(size_t)g * n + i];
   }
   __syncthreads();
 
@@ -425,7 +428,7 @@ __global__ __launch_bounds__(kGridThreads) void vox_grid_kernel(
   // this kernel both use ascending point order)
   const int* perm = ws.perm + (size_t)b * n;
   const int* seg_off = ws.seg_off + (size_t)b * (n + 1);
-  for (int si = tid; si < S; si += kGridThreads) {
+  for (int si = tid; si < S; si += NT) {
     const int s = s_begin + si;
     const int off = seg_off[s], end = seg_off[s + 1];
     const float inv = pcr_inv_count(end - off);
@@ -451,7 +454,7 @@ __global__ __launch_bounds__(kGridThreads) void vox_grid_kernel(
   int* cb = (cnt_out && grp == 0) ? cnt_out + (size_t)b * r3 : nullptr;
   if (!(PART & 1)) {
   } else if ((r3 & 3) == 0) {
-    for (int base = cell0 + tid * 4; base < cell1; base += kGridThreads * 4) {
+    for (int base = cell0 + tid * 4; base < cell1; base += NT * 4) {
       const int wl = (base >> 5) - wb;
       const unsigned word = bm_s[wl];
       const int pre = pre_s[wl];
@@ -481,7 +484,7 @@ __global__ __launch_bounds__(kGridThreads) void vox_grid_kernel(
       }
     }
   } else {
-    for (int cell = cell0 + tid; cell < cell1; cell += kGridThreads) {
+    for (int cell = cell0 + tid; cell < cell1; cell += NT) {
       const int wl = (cell >> 5) - wb;
       const unsigned word = bm_s[wl];
       const unsigned bit = 1u << (cell & 31);
@@ -502,7 +505,7 @@ __global__ __launch_bounds__(kGridThreads) void vox_grid_kernel(
     float vmax[kMaxG];
 #pragma unroll
     for (int g = 0; g < kMaxG; g++) vmax[g] = -__builtin_inff();
-    for (int i = tid; i < n; i += kGridThreads) {
+    for (int i = tid; i < n; i += NT) {
       int ci[8];
       float cw[8];
       int rk[8];
@@ -537,7 +540,7 @@ __global__ __launch_bounds__(kGridThreads) void vox_grid_kernel(
       }
     }
     if (desc) {
-      __shared__ float red[kGridThreads / kWave][kMaxG];
+      __shared__ float red[NT / kWave][kMaxG];
 #pragma unroll
       for (int g = 0; g < kMaxG; g++) {
         float m = wave_max(vmax[g]);
@@ -546,7 +549,7 @@ __global__ __launch_bounds__(kGridThreads) void vox_grid_kernel(
       __syncthreads();
       if (tid < gcount) {
         float m = red[0][tid];
-        for (int w = 1; w < kGridThreads / kWave; w++) m = fmaxf(m, red[w][tid]);
+        for (int w = 1; w < NT / kWave; w++) m = fmaxf(m, red[w][tid]);
         desc[(size_t)b * c + c0 + tid] = m;
       }
     }
@@ -685,22 +688,22 @@ static pcr_status run_voxelize(const float* features, const float* coords_f, con
     const int nw = (tile + 31) / 32 + 1;
     size_t smem = grid_smem_bytes(G, n, nw);
     PCR_REQUIRE(smem <= 150 * 1024, "%s: grid LDS %zu too large", name, smem);
-    allow_big_lds(vox_grid_kernel<1>, smem);
-    allow_big_lds(vox_grid_kernel<2>, smem);
-    allow_big_lds(vox_grid_kernel<3>, smem);
+    allow_big_lds(vox_grid_kernel<1, kGridThreads>, smem);
+    allow_big_lds(vox_grid_kernel<2, kDevoxThreads>, smem);
+    allow_big_lds(vox_grid_kernel<3, kGridThreads>, smem);
     if (do_dev) {
       PCR_REQUIRE(ntiles == 1, "%s: fused devoxelisation needs r^3 <= 65536", name);
       PCR_REQUIRE(c > 0, "%s: fused devoxelisation needs c > 0", name);
     }
     const dim3 grid(do_dev ? 1 : ntiles, ngrp, b);
     if (do_grid && do_dev)
-      hipLaunchKernelGGL(vox_grid_kernel<3>, grid, dim3(kGridThreads), smem, stream, features, c,
+      hipLaunchKernelGGL((vox_grid_kernel<3, kGridThreads>), grid, dim3(kGridThreads), smem, stream, features, c,
                          n, r3, G, tile, ws, out, cnt, dinds, dwgts, devox, desc);
     else if (do_dev)
-      hipLaunchKernelGGL(vox_grid_kernel<2>, grid, dim3(kGridThreads), smem, stream, features, c,
+      hipLaunchKernelGGL((vox_grid_kernel<2, kDevoxThreads>), grid, dim3(kDevoxThreads), smem, stream, features, c,
                          n, r3, G, tile, ws, nullptr, nullptr, dinds, dwgts, devox, desc);
     else if (c > 0 || cnt)
-      hipLaunchKernelGGL(vox_grid_kernel<1>, grid, dim3(kGridThreads), smem, stream, features, c,
+      hipLaunchKernelGGL((vox_grid_kernel<1, kGridThreads>), grid, dim3(kGridThreads), smem, stream, features, c,
                          n, r3, G, tile, ws, out, cnt, nullptr, nullptr, nullptr, nullptr);
   }
   return launch_status(name);

@@ -25,13 +25,20 @@ def N(t):
     return t.detach().cpu().numpy()
 
 
-def close(a, b, tol=TOL):
+def close(a, b, tol=TOL, rtol=0.0):
+    """|a - b| <= tol + rtol |b| elementwise, NaN where both are NaN."""
     a, b = np.asarray(a), np.asarray(b)
     assert a.shape == b.shape, (a.shape, b.shape)
     both_nan = np.isnan(a) & np.isnan(b)
     diff = np.abs(np.where(both_nan, 0, a - b))
     assert not np.isnan(diff).any(), "NaN mismatch"
-    assert diff.max(initial=0) <= tol, diff.max()
+    excess = diff - (tol + rtol * np.abs(np.where(both_nan, 0, b)))
+    assert excess.max(initial=0) <= 0, diff.max()
+
+
+# scatter-add backward passes sum in atomic (arbitrary) order, as the
+# reference's do: fp32 sum-order tolerance 1e-4 absolute + 1e-5 relative
+SCATTER_RTOL = 1e-5
 
 
 # --------------------------------------------------------------- voxelize
@@ -102,7 +109,7 @@ def test_sph_devox_backward(dev):
     gx = ops.spherical_trilinear_devoxelize_backward(
         T(g["sdevox_grad_y"], dev), T(g["sdevox_inds"], dev), T(g["sdevox_wgts"], dev),
         int(g["svox_r"]))
-    close(N(gx), g["sdevox_grad_x"], 1e-4)
+    close(N(gx), g["sdevox_grad_x"], 1e-4, SCATTER_RTOL)
 
 
 def test_cube_devox_golden(dev):
@@ -115,7 +122,7 @@ def test_cube_devox_golden(dev):
     assert np.array_equal(N(wgts), g["cdevox_wgts"])
     close(N(outs), g["cdevox_outs"])
     gx = ops.trilinear_devoxelize_backward(T(g["cdevox_grad_y"], dev), inds, wgts, rc)
-    close(N(gx), g["cdevox_grad_x"], 1e-4)
+    close(N(gx), g["cdevox_grad_x"], 1e-4, SCATTER_RTOL)
 
 
 @pytest.mark.parametrize("b,n,c,r", [(4, 1024, 64, 32), (2, 2048, 16, 16)])
@@ -199,7 +206,7 @@ def test_ball_query_grouping(dev):
     grp = ops.grouping_forward(pts, idx)
     assert np.array_equal(N(grp), g["bq_grouped"])
     gx = ops.grouping_backward(T(g["grp_grad_y"], dev), idx, pts.shape[2])
-    close(N(gx), g["grp_grad_x"], 1e-4)
+    close(N(gx), g["grp_grad_x"], 1e-4, SCATTER_RTOL)
 
 
 def test_ball_query_large(dev):
