@@ -93,6 +93,19 @@ pcr_status pcr_knn_local_ppf(const float *xyz, const float *normals, int b, int 
                              int relative, int *idx, float *dist, float *ppf, void *workspace,
                              size_t workspace_bytes, void *stream);
 
+/* The two launches of pcr_knn_local_ppf, separately, so a pipelined caller
+ * can sort step i+1 while step i selects (double-buffered workspaces):
+ * prepare = Morton sort of xyz into the workspace, prepared = selection +
+ * PPF from that workspace.  Both return PCR_ERR_UNSUPPORTED (nothing
+ * launched) where the sorted path does not apply (n > 4096); use
+ * pcr_knn_local_ppf there. */
+pcr_status pcr_knn_prepare(const float *xyz, int b, int n, void *workspace,
+                           size_t workspace_bytes, void *stream);
+pcr_status pcr_knn_local_ppf_prepared(const float *xyz, const float *normals, int b, int n, int k,
+                                      int relative, int *idx, float *dist, float *ppf,
+                                      const void *workspace, size_t workspace_bytes,
+                                      void *stream);
+
 /* ------------------------------------------------ ball query / grouping --
  * ball_query (ball_query/ball_query.cpp:6-30, kernel ball_query.cu:19-50):
  * centers [b,3,m], points [b,3,n] -> idx [b,m,u]. */

@@ -44,12 +44,14 @@ inline void allow_big_lds(K kernel, size_t bytes) {
 inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
 inline int64_t ceil_div64(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
-// knn_spatial.hip: Morton-sorted, box-pruned exact KNN.  Returns
-// PCR_ERR_UNSUPPORTED without launching anything when it does not apply.
+// knn_spatial.hip: Morton-sorted exact KNN.  Returns PCR_ERR_UNSUPPORTED
+// without launching anything when it does not apply.  stages: 1 = sort the
+// point sets into the workspace, 2 = select from an already sorted workspace,
+// 3 = both.
 pcr_status knn_spatial(const float* xyz1, const float* xyz2, int b, int n, int m, int k,
                        float* dist1, int* idx1, float* dist2, int* idx2, const float* nrm1,
                        const float* nrm2, int relative, float* ppf1, void* ws, size_t ws_bytes,
-                       bool self, hipStream_t st);
+                       bool self, hipStream_t st, int stages = 3);
 
 // ---------------------------------------------------------------- device
 constexpr int kWave = 64;

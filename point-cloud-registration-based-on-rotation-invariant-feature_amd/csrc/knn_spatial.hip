@@ -1017,15 +1017,18 @@ static pcr_status launch_block(const KnnSet& qs, const KnnSet& cs, int b, int k,
 pcr_status knn_spatial(const float* xyz1, const float* xyz2, int b, int n, int m, int k,
                        float* dist1, int* idx1, float* dist2, int* idx2, const float* nrm1,
                        const float* nrm2, int relative, float* ppf1, void* ws, size_t ws_bytes,
-                       bool self, hipStream_t st) {
+                       bool self, hipStream_t st, int stages) {
   if (ws == nullptr || n > kKnnMaxSortN || m > kKnnMaxSortN || n < 1 || m < 1 || k > 128)
     return PCR_ERR_UNSUPPORTED;
   if (ws_bytes < knn_ws_size(b, n, m)) return PCR_ERR_UNSUPPORTED;
   KnnSet s1, s2;
   size_t off = knn_set_layout(b, n, &s1, (char*)ws, 0);
   knn_set_layout(b, m, &s2, (char*)ws, off);
-  launch_sort(xyz1, b, n, s1, st);
-  if (!self) launch_sort(xyz2, b, m, s2, st);
+  if (stages & 1) {
+    launch_sort(xyz1, b, n, s1, st);
+    if (!self) launch_sort(xyz2, b, m, s2, st);
+  }
+  if (!(stages & 2)) return PCR_OK;
   const KnnSet& c1 = self ? s1 : s2;
   pcr_status rc;
   if (ppf1)

@@ -451,6 +451,38 @@ extern "C" pcr_status pcr_knn_local_ppf(const float* xyz, const float* normals, 
   return launch_status("knn_local_ppf");
 }
 
+extern "C" pcr_status pcr_knn_prepare(const float* xyz, int b, int n, void* workspace,
+                                      size_t workspace_bytes, void* stream) {
+  PCR_REQUIRE(b >= 0 && n >= 1, "knn_prepare: invalid sizes");
+  if (b == 0) return PCR_OK;
+  const pcr_status rc = knn_spatial(xyz, xyz, b, n, n, 1, nullptr, nullptr, nullptr, nullptr,
+                                    nullptr, nullptr, 0, nullptr, workspace, workspace_bytes, true,
+                                    as_stream(stream), 1);
+  if (rc == PCR_ERR_UNSUPPORTED) {
+    set_error("knn_prepare: no sorted path for n=%d (use pcr_knn_local_ppf)", n);
+    return rc;
+  }
+  return launch_status("knn_prepare");
+}
+
+extern "C" pcr_status pcr_knn_local_ppf_prepared(const float* xyz, const float* normals, int b,
+                                                 int n, int k, int relative, int* idx, float* dist,
+                                                 float* ppf, const void* workspace,
+                                                 size_t workspace_bytes, void* stream) {
+  PCR_REQUIRE(b >= 0 && n >= 1 && k >= 1 && k <= 128,
+              "knn_local_ppf_prepared: invalid sizes (k<=128)");
+  PCR_REQUIRE(ppf != nullptr && idx != nullptr, "knn_local_ppf_prepared: idx and ppf required");
+  if (b == 0) return PCR_OK;
+  const pcr_status rc = knn_spatial(xyz, xyz, b, n, n, k, dist, idx, nullptr, nullptr, normals,
+                                    normals, relative, ppf, const_cast<void*>(workspace),
+                                    workspace_bytes, true, as_stream(stream), 2);
+  if (rc == PCR_ERR_UNSUPPORTED) {
+    set_error("knn_local_ppf_prepared: no sorted path for n=%d, k=%d", n, k);
+    return rc;
+  }
+  return launch_status("knn_local_ppf_prepared");
+}
+
 extern "C" pcr_status pcr_spherical_ppf_forward(const float* coords, const float* center,
                                                 const float* normals, const float* center_normal,
                                                 int b, int n, float* feat, void* stream) {

@@ -28,6 +28,8 @@ SIGNATURES = {
     "pcr_spherical_ppf_forward": (ST, [P, P, P, P, I, I, P, P]),
     "pcr_local_ppf_forward": (ST, [P, P, P, P, P, I, I, I, I, I, I, P, P]),
     "pcr_knn_local_ppf": (ST, [P, P, I, I, I, I, P, P, P, P, SZ, P]),
+    "pcr_knn_prepare": (ST, [P, I, I, P, SZ, P]),
+    "pcr_knn_local_ppf_prepared": (ST, [P, P, I, I, I, I, P, P, P, P, SZ, P]),
     "pcr_ball_query": (ST, [P, P, I, I, I, F, I, P, P]),
     "pcr_grouping_forward": (ST, [P, P, I, I, I, I, I, P, P]),
     "pcr_grouping_backward": (ST, [P, P, I, I, I, I, I, P, P]),

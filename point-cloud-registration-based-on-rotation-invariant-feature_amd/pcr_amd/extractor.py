@@ -3,21 +3,22 @@
 One step over a batch of clouds (xyz [B,3,N], normals [B,3,N], point
 features [B,C,N], all resident on the GPU):
 
-  neighbour stage (stream A): self-KNN (k) -> local PPF [B,4,k,N]
+  front (stream P): Morton sort of the cloud for KNN; Spherical_Voxelization
+      normalisation (PVCNN/modules/spherical_vox.py:16-20) + voxel index /
+      occupancy / devox corners (prep)
+  neighbours (stream A): self-KNN (k) -> local PPF [B,4,k,N]
       = knn_forward_cuda + the model's local-PPF block
-        (PVCNN/models/pvcnn_classify.py:252-269), fused in one kernel
-  voxel stage (stream B): Spherical_Voxelization normalisation
-      (PVCNN/modules/spherical_vox.py:16-20) + voxel index / occupancy (prep),
-      then spherical_avg_voxelize's dense grid [B,C,r^3] + cnt (grid kernel),
-      and on stream C the spherical_trilinear_devoxelize of that grid
-      ([B,C,N] + inds/wgts) + per-cloud descriptor (max over points) [B,C]
-      (devox kernel; it re-forms the voxel means in LDS instead of re-reading
-      the grid, so it runs beside the grid kernel)
+        (PVCNN/models/pvcnn_classify.py:252-269), one kernel
+  grid (stream B): spherical_avg_voxelize's dense grid [B,C,r^3] + cnt
+  devox (stream C): spherical_trilinear_devoxelize of that grid ([B,C,N] +
+      inds/wgts) + per-cloud descriptor (max over points) [B,C]; it re-forms
+      the voxel means in LDS instead of re-reading the grid, so it runs beside
+      the grid kernel
 
-The stages run on HIP streams forked from and joined back to the caller's
-stream.  ``capture()`` records one step into a hipGraph; ``run_pipelined()``
-enqueues S consecutive steps with no join between them, so step i+1's
-neighbour stage overlaps step i's voxel stage.
+The streams are forked from and joined back to the caller's stream.
+``capture()`` records one step into a hipGraph; ``run_pipelined()`` enqueues
+S consecutive steps with no join between them on alternating buffer sets, so
+step i+1's front stage overlaps step i's back stages.
 """
 import torch
 
@@ -51,18 +52,56 @@ class SphExtractor:
                     device=dev)
         self.knn_ws = e(max(256, lib.pcr_knn_workspace_size(b, n, n)), dtype=torch.uint8,
                         device=dev)
+        self.s_pre = torch.cuda.Stream(device=dev)
         self.s_nbr = torch.cuda.Stream(device=dev)
         self.s_vox = torch.cuda.Stream(device=dev)
         self.s_dev = torch.cuda.Stream(device=dev)
         self.graph = None
         self._static_in = None
+        self._set1 = None
 
     # ---------------------------------------------------------------- stages
+    # Buffers a later stage of the same step reads (the two workspaces and the
+    # devox corners) come in two sets, so a pipelined caller can run step i+1's
+    # front stages while step i's back stages still read set i % 2.
+    def _set(self, slot):
+        if slot == 0:
+            return self.knn_ws, self.ws, self.dinds, self.dwgts
+        if self._set1 is None:
+            e = torch.empty_like
+            self._set1 = (e(self.knn_ws), e(self.ws), e(self.dinds), e(self.dwgts))
+        return self._set1
+
     def neighbor_stage(self, xyz, normals, stream):
+        """Sort + select + PPF in one call (the eager, unsplit path)."""
         _lib.check(_lib.load().pcr_knn_local_ppf(
             _ptr(xyz), _ptr(normals), self.b, self.n, self.k, int(self.relative),
             _ptr(self.knn_idx), _ptr(self.knn_dist), _ptr(self.local_ppf), _ptr(self.knn_ws),
             self.knn_ws.numel(), stream), "knn_local_ppf")
+
+    def knn_sort(self, xyz, stream, slot=0):
+        """Morton sort into workspace set `slot`; False when the sorted path
+        does not apply (then knn_select falls back to the one-call path)."""
+        kws = self._set(slot)[0]
+        rc = _lib.load().pcr_knn_prepare(_ptr(xyz), self.b, self.n, _ptr(kws), kws.numel(),
+                                         stream)
+        if rc == -3:  # PCR_ERR_UNSUPPORTED, nothing launched
+            return False
+        _lib.check(rc, "knn_prepare")
+        return True
+
+    def knn_select(self, xyz, normals, stream, slot=0, sorted_ok=True):
+        kws = self._set(slot)[0]
+        if not sorted_ok:
+            _lib.check(_lib.load().pcr_knn_local_ppf(
+                _ptr(xyz), _ptr(normals), self.b, self.n, self.k, int(self.relative),
+                _ptr(self.knn_idx), _ptr(self.knn_dist), _ptr(self.local_ppf), _ptr(kws),
+                kws.numel(), stream), "knn_local_ppf")
+            return
+        _lib.check(_lib.load().pcr_knn_local_ppf_prepared(
+            _ptr(xyz), _ptr(normals), self.b, self.n, self.k, int(self.relative),
+            _ptr(self.knn_idx), _ptr(self.knn_dist), _ptr(self.local_ppf), _ptr(kws),
+            kws.numel(), stream), "knn_local_ppf_prepared")
 
     def voxel_stage(self, xyz, features, stream):
         _lib.check(_lib.load().pcr_extractor_voxel_stage(
@@ -71,24 +110,25 @@ class SphExtractor:
             _ptr(self.dwgts), _ptr(self.desc), _ptr(self.ws), self.ws.numel(), stream),
             "extractor_voxel_stage")
 
-    def voxel_prep(self, xyz, stream):
+    def voxel_prep(self, xyz, stream, slot=0):
+        _, ws, dinds, dwgts = self._set(slot)
         _lib.check(_lib.load().pcr_extractor_voxel_prep(
             _ptr(xyz), self.b, self.n, self.r, _ptr(self.norm_coords), _ptr(self.ind),
-            _ptr(self.dinds), _ptr(self.dwgts), _ptr(self.ws), self.ws.numel(), stream),
-            "extractor_voxel_prep")
+            _ptr(dinds), _ptr(dwgts), _ptr(ws), ws.numel(), stream), "extractor_voxel_prep")
 
-    def voxel_grid(self, features, stream):
+    def voxel_grid(self, features, stream, slot=0):
         """The dominant kernel (vox_grid_kernel<1>: means -> dense grid + cnt)."""
+        ws = self._set(slot)[1]
         _lib.check(_lib.load().pcr_extractor_voxel_grid(
             _ptr(features), self.b, self.c, self.n, self.r, _ptr(self.cnt), _ptr(self.grid),
-            _ptr(self.ws), self.ws.numel(), stream), "extractor_voxel_grid")
+            _ptr(ws), ws.numel(), stream), "extractor_voxel_grid")
 
-    def voxel_devox(self, features, stream, desc=None):
+    def voxel_devox(self, features, stream, desc=None, slot=0):
+        _, ws, dinds, dwgts = self._set(slot)
         d = self.desc if desc is None else desc
         _lib.check(_lib.load().pcr_extractor_voxel_devox(
-            _ptr(features), self.b, self.c, self.n, self.r, _ptr(self.devox), _ptr(self.dinds),
-            _ptr(self.dwgts), _ptr(d), _ptr(self.ws), self.ws.numel(), stream),
-            "extractor_voxel_devox")
+            _ptr(features), self.b, self.c, self.n, self.r, _ptr(self.devox), _ptr(dinds),
+            _ptr(dwgts), _ptr(d), _ptr(ws), ws.numel(), stream), "extractor_voxel_devox")
 
     def _check_inputs(self, xyz, normals, features):
         for t, name in ((xyz, "xyz"), (normals, "normals"), (features, "features")):
@@ -98,31 +138,51 @@ class SphExtractor:
                                                                                   self.n):
             raise RuntimeError("input shape does not match the extractor configuration")
 
-    def enqueue(self, xyz, normals, features, desc=None, first=True):
-        """Enqueue one step on the extractor's own streams, no fork/join.
-        Stream order carries the step-to-step dependencies, so consecutive
-        steps pipeline: step i+1's neighbour stage runs beside step i's voxel
-        stage.  The only cross-stream edges: devox after prep (it reads the
-        prep results) and the next prep after devox (prep overwrites them);
-        `first` = nothing of this extractor is pending on the streams since
-        the last fork (no previous devox to wait for)."""
-        self.neighbor_stage(xyz, normals, self.s_nbr.cuda_stream)
-        if not first:
-            self.s_vox.wait_stream(self.s_dev)
-        self.voxel_prep(xyz, self.s_vox.cuda_stream)
-        self.s_dev.wait_stream(self.s_vox)
-        self.voxel_grid(features, self.s_vox.cuda_stream)
-        self.voxel_devox(features, self.s_dev.cuda_stream, desc)
+    def _streams(self):
+        return (self.s_pre, self.s_nbr, self.s_vox, self.s_dev)
 
     def _fork(self):
         cur = torch.cuda.current_stream(self.device)
-        for st in (self.s_nbr, self.s_vox, self.s_dev):
+        for st in self._streams():
             st.wait_stream(cur)
         return cur
 
     def _join(self, cur):
-        for st in (self.s_nbr, self.s_vox, self.s_dev):
+        for st in self._streams():
             cur.wait_stream(st)
+
+    def enqueue(self, xyz, normals, features, desc=None, slot=0, reuse=None, events=False):
+        """Enqueue one step on the extractor's streams, no fork/join:
+          s_pre: KNN Morton sort, voxel prep (both small, one workgroup per cloud)
+          s_nbr: KNN selection + local PPF      (after the sort)
+          s_vox: voxel grid                     (after prep)
+          s_dev: devoxelisation + descriptor    (after prep)
+        `reuse` = events after which the previous users of buffer set `slot`
+        are done (s_pre waits for them before overwriting it).  With
+        `events`, returns this step's events on buffer set `slot`."""
+        if reuse:
+            for ev in reuse:
+                self.s_pre.wait_event(ev)
+        sorted_ok = self.knn_sort(xyz, self.s_pre.cuda_stream, slot)
+        e_sort = torch.cuda.Event()
+        e_sort.record(self.s_pre)
+        self.voxel_prep(xyz, self.s_pre.cuda_stream, slot)
+        e_prep = torch.cuda.Event()
+        e_prep.record(self.s_pre)
+        self.s_nbr.wait_event(e_sort)
+        self.knn_select(xyz, normals, self.s_nbr.cuda_stream, slot, sorted_ok)
+        self.s_vox.wait_event(e_prep)
+        self.voxel_grid(features, self.s_vox.cuda_stream, slot)
+        self.s_dev.wait_event(e_prep)
+        self.voxel_devox(features, self.s_dev.cuda_stream, desc, slot)
+        if not events:
+            return None
+        evs = []
+        for st in (self.s_nbr, self.s_vox, self.s_dev):
+            ev = torch.cuda.Event()
+            ev.record(st)
+            evs.append(ev)
+        return evs
 
     def forward(self, xyz, normals, features):
         """Enqueue one step, forked from and joined back to the current stream."""
@@ -132,26 +192,31 @@ class SphExtractor:
         self._join(cur)
         return self.outputs()
 
-    def outputs(self):
+    def outputs(self, slot=0):
+        _, _, dinds, dwgts = self._set(slot)
         return {
             "knn_idx": self.knn_idx, "local_ppf": self.local_ppf, "norm_coords": self.norm_coords,
             "ind": self.ind, "cnt": self.cnt, "grid": self.grid, "devox": self.devox,
-            "dinds": self.dinds, "dwgts": self.dwgts, "desc": self.desc,
+            "dinds": dinds, "dwgts": dwgts, "desc": self.desc,
         }
 
     def run_pipelined(self, xyz, normals, features, steps, desc_steps=None):
-        """Enqueue `steps` consecutive steps with no join between them (step
-        i+1's neighbour stage overlaps step i's voxel stage), forked from and
-        joined back to the current stream once.  Step s writes its descriptor
-        to desc_steps[s] when given.  Eager launches: ROCm's stream capture
-        does not take the prep-after-devox edge between two steps."""
+        """Enqueue `steps` consecutive steps with no join between them: step
+        i+1's sort and prep run while step i selects and voxelises, on
+        alternating buffer sets; forked from and joined back to the current
+        stream once.  Step s writes its descriptor to desc_steps[s] when
+        given.  Eager launches (ROCm's stream capture rejects the cross-step
+        edges)."""
         self._check_inputs(xyz, normals, features)
         cur = self._fork()
+        pending = [None, None]
         for s in range(steps):
+            slot = s & 1
             d = None if desc_steps is None else desc_steps[s]
-            self.enqueue(xyz, normals, features, desc=d, first=s == 0)
+            pending[slot] = self.enqueue(xyz, normals, features, desc=d, slot=slot,
+                                         reuse=pending[slot], events=True)
         self._join(cur)
-        return self.outputs()
+        return self.outputs(slot=(steps - 1) & 1)
 
     def capture(self, xyz, normals, features):
         """Capture one step over these input tensors into a hipGraph."""
