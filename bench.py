@@ -48,7 +48,8 @@ def parse():
     ap.add_argument("--kernel-iters", type=int, default=50)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--mode", choices=("pipelined", "graph", "eager"), default="pipelined",
+    ap.add_argument("--mode", choices=("pipelined", "pipelined4", "graph", "eager"),
+                    default="pipelined",
                     help="pipelined: S steps enqueued with no join between them; graph: one "
                          "hipGraph replay per step; eager: fork/join launches per step")
     ap.add_argument("--steps-per-launch", type=int, default=10,
@@ -128,7 +129,7 @@ def main():
 
     # S pipelined steps per graph launch (one launch = S batches); S must
     # divide the step counts so exactly --steps steps are timed
-    S = max(1, args.steps_per_launch) if args.mode == "pipelined" else 1
+    S = max(1, args.steps_per_launch) if args.mode.startswith("pipelined") else 1
     if args.steps % S or (args.warmup and args.warmup % S):
         S = 1
     comm = torch.cuda.Stream(device=dev) if world > 1 else None
@@ -142,8 +143,9 @@ def main():
 
     def launch(i):
         """Steps i*S .. i*S+S-1."""
-        if args.mode == "pipelined":
-            ex.run_pipelined(xyz, nrm, feat, S, desc_steps)
+        if args.mode.startswith("pipelined"):
+            ex.run_pipelined(xyz, nrm, feat, S, desc_steps,
+                             mode="four" if args.mode == "pipelined4" else "two")
             src = desc_steps.view(S * b, c)
         elif args.mode == "graph":
             ex.replay()

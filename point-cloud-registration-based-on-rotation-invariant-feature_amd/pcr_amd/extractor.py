@@ -200,15 +200,30 @@ class SphExtractor:
             "dinds": dinds, "dwgts": dwgts, "desc": self.desc,
         }
 
-    def run_pipelined(self, xyz, normals, features, steps, desc_steps=None):
-        """Enqueue `steps` consecutive steps with no join between them: step
-        i+1's sort and prep run while step i selects and voxelises, on
-        alternating buffer sets; forked from and joined back to the current
-        stream once.  Step s writes its descriptor to desc_steps[s] when
-        given.  Eager launches (ROCm's stream capture rejects the cross-step
-        edges)."""
+    def run_pipelined(self, xyz, normals, features, steps, desc_steps=None, mode="two"):
+        """Enqueue `steps` consecutive steps with no join between them, forked
+        from and joined back to the current stream once.  Step s writes its
+        descriptor to desc_steps[s] when given.
+
+        mode "two": two independent streams and no cross-stream edge at all --
+        s_nbr runs sort + select of every step, s_vox prep + grid + devox of
+        every step (each stream reuses its own buffers in stream order).
+        mode "four": the four-stream schedule of enqueue() on alternating
+        buffer sets (front stages of step i+1 overlap step i's back stages).
+        Eager launches (ROCm's stream capture rejects the cross-step edges)."""
         self._check_inputs(xyz, normals, features)
         cur = self._fork()
+        if mode == "two":
+            sn, sv = self.s_nbr.cuda_stream, self.s_vox.cuda_stream
+            for s in range(steps):
+                d = None if desc_steps is None else desc_steps[s]
+                ok = self.knn_sort(xyz, sn)
+                self.knn_select(xyz, normals, sn, 0, ok)
+                self.voxel_prep(xyz, sv)
+                self.voxel_grid(features, sv)
+                self.voxel_devox(features, sv, d)
+            self._join(cur)
+            return self.outputs()
         pending = [None, None]
         for s in range(steps):
             slot = s & 1

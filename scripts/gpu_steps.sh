@@ -25,7 +25,8 @@ for step in "$@"; do
     tests) run pytest_gpu 1200 python -m pytest tests -x -q -m gpu -p no:cacheprovider ;;
     tests_all) run pytest_gpu 1200 python -m pytest tests -q -m gpu -p no:cacheprovider ;;
     bench) run bench 600 python bench.py ;;
-    modes) run bench_graph 300 python bench.py --mode graph --no-cpu-baseline
+    modes) run bench_p4 300 python bench.py --mode pipelined4 --no-cpu-baseline
+           run bench_graph 300 python bench.py --mode graph --no-cpu-baseline
            run bench_eager 300 python bench.py --mode eager --no-cpu-baseline ;;
     prof) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
           run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 50 --warmup 10 --no-cpu-baseline ;;

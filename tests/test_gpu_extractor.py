@@ -71,14 +71,16 @@ def test_extractor_pipelined_graph(dev):
     tx, tn, tf = T(xyz, dev), T(nrm, dev), T(feat, dev)
     ex = SphExtractor(b, n, c, k, r, device=dev)
     ref = {kk: v.clone() for kk, v in ex.forward(tx, tn, tf).items()}
-    desc_steps = torch.empty((4, b, c), device=dev)
-    for _ in range(2):
-        out = ex.run_pipelined(tx, tn, tf, 4, desc_steps)
-    torch.cuda.synchronize()
-    for key, v in ref.items():
-        assert torch.equal(out[key], v) or torch.allclose(out[key], v, equal_nan=True), key
-    for s in range(4):
-        assert torch.equal(desc_steps[s], ref["desc"]), s
+    for mode in ("two", "four"):
+        desc_steps = torch.empty((5, b, c), device=dev)
+        for _ in range(2):
+            out = ex.run_pipelined(tx, tn, tf, 5, desc_steps, mode=mode)
+        torch.cuda.synchronize()
+        for key, v in ref.items():
+            assert torch.equal(out[key], v) or torch.allclose(out[key], v, equal_nan=True), \
+                (mode, key)
+        for s in range(5):
+            assert torch.equal(desc_steps[s], ref["desc"]), (mode, s)
 
 
 def test_extractor_full_size_properties(dev):
