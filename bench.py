@@ -48,7 +48,7 @@ def parse():
     ap.add_argument("--kernel-iters", type=int, default=50)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--mode", choices=("pipelined", "pipelined4", "graph", "eager"),
+    ap.add_argument("--mode", choices=("pipelined", "pipelined2", "pipelined4", "graph", "eager"),
                     default="pipelined",
                     help="pipelined: S steps enqueued with no join between them; graph: one "
                          "hipGraph replay per step; eager: fork/join launches per step")
@@ -145,7 +145,8 @@ def main():
         """Steps i*S .. i*S+S-1."""
         if args.mode.startswith("pipelined"):
             ex.run_pipelined(xyz, nrm, feat, S, desc_steps,
-                             mode="four" if args.mode == "pipelined4" else "two")
+                             mode={"pipelined": "three", "pipelined2": "two",
+                                   "pipelined4": "four"}[args.mode])
             src = desc_steps.view(S * b, c)
         elif args.mode == "graph":
             ex.replay()

@@ -200,11 +200,14 @@ class SphExtractor:
             "dinds": dinds, "dwgts": dwgts, "desc": self.desc,
         }
 
-    def run_pipelined(self, xyz, normals, features, steps, desc_steps=None, mode="two"):
+    def run_pipelined(self, xyz, normals, features, steps, desc_steps=None, mode="three"):
         """Enqueue `steps` consecutive steps with no join between them, forked
         from and joined back to the current stream once.  Step s writes its
         descriptor to desc_steps[s] when given.
 
+        mode "three" (default): s_nbr runs sort + select of every step, s_vox
+        prep + grid, s_dev devox after its step's prep, on alternating buffer
+        sets (prep waits only for the devox two steps back).
         mode "two": two independent streams and no cross-stream edge at all --
         s_nbr runs sort + select of every step, s_vox prep + grid + devox of
         every step (each stream reuses its own buffers in stream order).
@@ -213,18 +216,27 @@ class SphExtractor:
         Eager launches (ROCm's stream capture rejects the cross-step edges)."""
         self._check_inputs(xyz, normals, features)
         cur = self._fork()
-        if mode == "two":
-            sn, sv = self.s_nbr.cuda_stream, self.s_vox.cuda_stream
+        if mode == "three":
+            sn, sv, sd = self.s_nbr.cuda_stream, self.s_vox.cuda_stream, self.s_dev.cuda_stream
+            dev_done = [None, None]
             for s in range(steps):
+                slot = s & 1
                 d = None if desc_steps is None else desc_steps[s]
                 ok = self.knn_sort(xyz, sn)
                 self.knn_select(xyz, normals, sn, 0, ok)
-                self.voxel_prep(xyz, sv)
-                self.voxel_grid(features, sv)
-                self.voxel_devox(features, sv, d)
+                if dev_done[slot] is not None:  # step s-2's devox read this set
+                    self.s_vox.wait_event(dev_done[slot])
+                self.voxel_prep(xyz, sv, slot)
+                e_prep = torch.cuda.Event()
+                e_prep.record(self.s_vox)
+                self.voxel_grid(features, sv, slot)
+                self.s_dev.wait_event(e_prep)
+                self.voxel_devox(features, sd, d, slot)
+                dev_done[slot] = torch.cuda.Event()
+                dev_done[slot].record(self.s_dev)
             self._join(cur)
-            return self.outputs()
-        pending = [None, None]
+            return self.outputs(slot=(steps - 1) & 1)
+        if mode == "two":        pending = [None, None]
         for s in range(steps):
             slot = s & 1
             d = None if desc_steps is None else desc_steps[s]
