@@ -236,7 +236,18 @@ class SphExtractor:
                 dev_done[slot].record(self.s_dev)
             self._join(cur)
             return self.outputs(slot=(steps - 1) & 1)
-        if mode == "two":        pending = [None, None]
+        if mode == "two":
+            sn, sv = self.s_nbr.cuda_stream, self.s_vox.cuda_stream
+            for s in range(steps):
+                d = None if desc_steps is None else desc_steps[s]
+                ok = self.knn_sort(xyz, sn)
+                self.knn_select(xyz, normals, sn, 0, ok)
+                self.voxel_prep(xyz, sv)
+                self.voxel_grid(features, sv)
+                self.voxel_devox(features, sv, d)
+            self._join(cur)
+            return self.outputs()
+        pending = [None, None]
         for s in range(steps):
             slot = s & 1
             d = None if desc_steps is None else desc_steps[s]
