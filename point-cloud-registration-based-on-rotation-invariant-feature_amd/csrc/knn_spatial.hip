@@ -555,7 +555,7 @@ __global__ __launch_bounds__(KnnNW<KMAX>::wg * 64) void knn_block_kernel(
 // reference's result: the k lexicographically smallest (d, index) with
 // d < 10000, unfilled slots (10000, 0).
 constexpr int kNB = 24;
-constexpr int kCap = 96;
+constexpr int kCap = 88;
 constexpr int kSelCache = 1024;  // candidates staged in LDS per workgroup
 constexpr int kSelMaxK = 32;
 
@@ -611,8 +611,12 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     float* __restrict__ ppf) {
   constexpr int FPD = 32 / CB;              // wave fields per counter dword
   constexpr int NG = (NW + FPD - 1) / FPD;  // counter dwords per (bin, lane)
-  __shared__ unsigned hist_s[NG * (kNB + 1) * kBlk];
-  __shared__ kkey buf_s[(kCap + 1) * kBlk];  // row kCap: sink of masked writes
+  // the histogram is dead once the cut is chosen: the collected keys reuse it
+  constexpr int kHistBytes = NG * (kNB + 1) * kBlk * 4;
+  constexpr int kBufBytes = (kCap + 1) * kBlk * 8;  // row kCap: sink of masked writes
+  __shared__ __align__(16) unsigned char sel_u[kHistBytes > kBufBytes ? kHistBytes : kBufBytes];
+  unsigned* hist_s = (unsigned*)sel_u;
+  kkey* buf_s = (kkey*)sel_u;
   __shared__ unsigned dest_s[kBlk];
   __shared__ __align__(16) float cand_s[CL ? 3 * kSelCache : 4];  // x | y | z
   __shared__ __align__(16) int cand_j[CL ? kSelCache : 4];
@@ -781,6 +785,7 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     for (int g = 0; g < NG; g++)
       slot += (int)field_sum<CB>(g < mg ? cut[g] : (g == mg ? (cut[g] & below) : 0u));
   }
+  __syncthreads();  // histogram reads done: buf_s overwrites it
 #ifdef PCR_DIAG
   if (threadIdx.x == 0 && PCR_WG_LINEAR < 1024) {
     pcr_diag_stamps[PCR_WG_LINEAR][8] = fallback ? 1 : 0;

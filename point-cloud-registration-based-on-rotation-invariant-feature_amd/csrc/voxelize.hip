@@ -637,12 +637,11 @@ __global__ __launch_bounds__(kPrepThreads) void sph_normalize_kernel(
 }
 
 // ------------------------------------------------------------- launchers
-static int pick_groups(int c, int n, int* G_out) {
-  // LDS per grid WG ~ (2*G + 1) * n * 4 + bitmap; keep <= 64 KB so two
-  // workgroups co-reside per CU (one computes means while the other streams)
+static int pick_groups(int c, int n, int max_g, int* G_out) {
+  // LDS per grid WG ~ (2*G + 1) * n * 4 + bitmap: at most max_g channels
   int G = kMaxG;
   while (G > 1 && ((size_t)(2 * G + 1) * n * 4 + 8192) > 65536) G >>= 1;
-  if (G > 4) G = 4;
+  if (G > max_g) G = max_g;
   *G_out = G;
   return ceil_div(c, G);
 }
@@ -679,32 +678,43 @@ static pcr_status run_voxelize(const float* features, const float* coords_f, con
   }
   const bool do_grid = (what & 2) != 0;
   const bool do_dev = (what & 4) != 0 && devox != nullptr;
-  if (do_grid || do_dev) {
+  // one tile covers the whole grid when its bitmap fits comfortably
+  const int tile = r3 <= 65536 ? ((r3 + 31) / 32) * 32 : 32768;
+  const int ntiles = ceil_div(r3, tile);
+  const int nw = (tile + 31) / 32 + 1;
+  if (do_dev) {
+    PCR_REQUIRE(ntiles == 1, "%s: fused devoxelisation needs r^3 <= 65536", name);
+    PCR_REQUIRE(c > 0, "%s: fused devoxelisation needs c > 0", name);
+  }
+  if (do_grid && do_dev) {
     int G = 1;
-    const int ngrp = c > 0 ? pick_groups(c, n, &G) : 1;
-    // one tile covers the whole grid when its bitmap fits comfortably
-    const int tile = r3 <= 65536 ? ((r3 + 31) / 32) * 32 : 32768;
-    const int ntiles = ceil_div(r3, tile);
-    const int nw = (tile + 31) / 32 + 1;
-    size_t smem = grid_smem_bytes(G, n, nw);
+    const int ngrp = pick_groups(c, n, 4, &G);
+    const size_t smem = grid_smem_bytes(G, n, nw);
+    PCR_REQUIRE(smem <= 150 * 1024, "%s: grid LDS %zu too large", name, smem);
+    allow_big_lds(vox_grid_kernel<3, kGridThreads>, smem);
+    hipLaunchKernelGGL((vox_grid_kernel<3, kGridThreads>), dim3(1, ngrp, b), dim3(kGridThreads),
+                       smem, stream, features, c, n, r3, G, tile, ws, out, cnt, dinds, dwgts,
+                       devox, desc);
+  } else if (do_dev) {
+    int G = 1;
+    const int ngrp = pick_groups(c, n, 4, &G);
+    const size_t smem = grid_smem_bytes(G, n, nw);
+    PCR_REQUIRE(smem <= 150 * 1024, "%s: grid LDS %zu too large", name, smem);
+    allow_big_lds(vox_grid_kernel<2, kDevoxThreads>, smem);
+    hipLaunchKernelGGL((vox_grid_kernel<2, kDevoxThreads>), dim3(1, ngrp, b),
+                       dim3(kDevoxThreads), smem, stream, features, c, n, r3, G, tile, ws, nullptr,
+                       nullptr, dinds, dwgts, devox, desc);
+  } else if (do_grid && (c > 0 || cnt)) {
+    // streaming part: two channels per workgroup keep its LDS small (~29 KB
+    // at n = 1024), so its workgroups fit beside the KNN selection's
+    int G = 1;
+    const int ngrp = c > 0 ? pick_groups(c, n, 2, &G) : 1;
+    const size_t smem = grid_smem_bytes(G, n, nw);
     PCR_REQUIRE(smem <= 150 * 1024, "%s: grid LDS %zu too large", name, smem);
     allow_big_lds(vox_grid_kernel<1, kGridThreads>, smem);
-    allow_big_lds(vox_grid_kernel<2, kDevoxThreads>, smem);
-    allow_big_lds(vox_grid_kernel<3, kGridThreads>, smem);
-    if (do_dev) {
-      PCR_REQUIRE(ntiles == 1, "%s: fused devoxelisation needs r^3 <= 65536", name);
-      PCR_REQUIRE(c > 0, "%s: fused devoxelisation needs c > 0", name);
-    }
-    const dim3 grid(do_dev ? 1 : ntiles, ngrp, b);
-    if (do_grid && do_dev)
-      hipLaunchKernelGGL((vox_grid_kernel<3, kGridThreads>), grid, dim3(kGridThreads), smem, stream, features, c,
-                         n, r3, G, tile, ws, out, cnt, dinds, dwgts, devox, desc);
-    else if (do_dev)
-      hipLaunchKernelGGL((vox_grid_kernel<2, kDevoxThreads>), grid, dim3(kDevoxThreads), smem, stream, features, c,
-                         n, r3, G, tile, ws, nullptr, nullptr, dinds, dwgts, devox, desc);
-    else if (c > 0 || cnt)
-      hipLaunchKernelGGL((vox_grid_kernel<1, kGridThreads>), grid, dim3(kGridThreads), smem, stream, features, c,
-                         n, r3, G, tile, ws, out, cnt, nullptr, nullptr, nullptr, nullptr);
+    hipLaunchKernelGGL((vox_grid_kernel<1, kGridThreads>), dim3(ntiles, ngrp, b),
+                       dim3(kGridThreads), smem, stream, features, c, n, r3, G, tile, ws, out, cnt,
+                       nullptr, nullptr, nullptr, nullptr);
   }
   return launch_status(name);
 }
