@@ -96,7 +96,9 @@ pcr_status pcr_knn_local_ppf(const float *xyz, const float *normals, int b, int 
 /* The two launches of pcr_knn_local_ppf, separately, so a pipelined caller
  * can sort step i+1 while step i selects (double-buffered workspaces):
  * prepare = Morton sort of xyz into the workspace, prepared = selection +
- * PPF from that workspace.  Both return PCR_ERR_UNSUPPORTED (nothing
+ * PPF from that workspace (ppf == NULL: selection only; the PPF can then
+ * come from pcr_local_ppf_forward with idx_kmajor = 1, one thread per
+ * output, coalesced).  Both return PCR_ERR_UNSUPPORTED (nothing
  * launched) where the sorted path does not apply (n > 4096); use
  * pcr_knn_local_ppf there. */
 pcr_status pcr_knn_prepare(const float *xyz, int b, int n, void *workspace,

@@ -471,7 +471,7 @@ extern "C" pcr_status pcr_knn_local_ppf_prepared(const float* xyz, const float* 
                                                  size_t workspace_bytes, void* stream) {
   PCR_REQUIRE(b >= 0 && n >= 1 && k >= 1 && k <= 128,
               "knn_local_ppf_prepared: invalid sizes (k<=128)");
-  PCR_REQUIRE(ppf != nullptr && idx != nullptr, "knn_local_ppf_prepared: idx and ppf required");
+  PCR_REQUIRE(idx != nullptr, "knn_local_ppf_prepared: idx required");
   if (b == 0) return PCR_OK;
   const pcr_status rc = knn_spatial(xyz, xyz, b, n, n, k, dist, idx, nullptr, nullptr, normals,
                                     normals, relative, ppf, const_cast<void*>(workspace),

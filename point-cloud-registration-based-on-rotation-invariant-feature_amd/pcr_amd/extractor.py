@@ -28,9 +28,10 @@ from .ops import _ptr
 
 class SphExtractor:
     def __init__(self, batch, npoints, channels, k, resolution, device="cuda", relative=True,
-                 with_dist=False):
+                 with_dist=False, split_ppf=True):
         self.b, self.n, self.c, self.k, self.r = batch, npoints, channels, k, resolution
         self.relative = relative
+        self.split_ppf = split_ppf
         self.device = torch.device(device)
         b, n, c, r = batch, npoints, channels, resolution
         r3 = r * r * r
@@ -98,10 +99,17 @@ class SphExtractor:
                 _ptr(self.knn_idx), _ptr(self.knn_dist), _ptr(self.local_ppf), _ptr(kws),
                 kws.numel(), stream), "knn_local_ppf")
             return
-        _lib.check(_lib.load().pcr_knn_local_ppf_prepared(
+        lib = _lib.load()
+        _lib.check(lib.pcr_knn_local_ppf_prepared(
             _ptr(xyz), _ptr(normals), self.b, self.n, self.k, int(self.relative),
-            _ptr(self.knn_idx), _ptr(self.knn_dist), _ptr(self.local_ppf), _ptr(kws),
-            kws.numel(), stream), "knn_local_ppf_prepared")
+            _ptr(self.knn_idx), _ptr(self.knn_dist), None if self.split_ppf else
+            _ptr(self.local_ppf), _ptr(kws), kws.numel(), stream), "knn_local_ppf_prepared")
+        if self.split_ppf:
+            # PPF as its own launch: one thread per (slot, point), coalesced
+            _lib.check(lib.pcr_local_ppf_forward(
+                _ptr(xyz), _ptr(normals), _ptr(xyz), _ptr(normals), _ptr(self.knn_idx), self.b,
+                self.n, self.n, self.k, 1, int(self.relative), _ptr(self.local_ppf), stream),
+                "local_ppf_forward")
 
     def voxel_stage(self, xyz, features, stream):
         _lib.check(_lib.load().pcr_extractor_voxel_stage(
