@@ -661,23 +661,36 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
       static_assert(S % 4 == 0, "a wave owns whole groups of four");
       const int ng = nblk * GPB;
       auto off = [&](int g) { return (g / GPB) * kBlk + wv * S + (g % GPB) * 4; };
-      int o = off(0);
-      float4 X = *(const float4*)(cand_s + o);
-      float4 Y = *(const float4*)(cand_s + kSelCache + o);
-      float4 Z = *(const float4*)(cand_s + 2 * kSelCache + o);
-      for (int g = 0; g < ng; g++) {
-        const int on = off(g + 1 < ng ? g + 1 : g);
-        const float4 Xn = *(const float4*)(cand_s + on);
-        const float4 Yn = *(const float4*)(cand_s + kSelCache + on);
-        const float4 Zn = *(const float4*)(cand_s + 2 * kSelCache + on);
+      // two groups per iteration, the next two groups' reads in flight
+      auto rd = [&](int g, float4& X, float4& Y, float4& Z) {
+        const int o = off(g);
+        X = *(const float4*)(cand_s + o);
+        Y = *(const float4*)(cand_s + kSelCache + o);
+        Z = *(const float4*)(cand_s + 2 * kSelCache + o);
+      };
+      auto eval = [&](int g, const float4& X, const float4& Y, const float4& Z) {
         const pf2 d0 = cand_dist2(qx2, qy2, qz2, pf2{X.x, X.y}, pf2{Y.x, Y.y}, pf2{Z.x, Z.y});
         const pf2 d1 = cand_dist2(qx2, qy2, qz2, pf2{X.z, X.w}, pf2{Y.z, Y.w}, pf2{Z.z, Z.w});
         const float d[4] = {d0[0], d0[1], d1[0], d1[1]};
-        f(o, d);
-        o = on;
-        X = Xn;
-        Y = Yn;
-        Z = Zn;
+        f(off(g), d);
+      };
+      // ping-pong register sets A / B, no copies: B's reads are issued
+      // before A's evaluation (and its LDS atomics / stores) and vice versa
+      auto cl = [&](int g) { return g < ng ? g : ng - 1; };
+      float4 AX0, AY0, AZ0, AX1, AY1, AZ1, BX0, BY0, BZ0, BX1, BY1, BZ1;
+      rd(cl(0), AX0, AY0, AZ0);
+      rd(cl(1), AX1, AY1, AZ1);
+      for (int g = 0; g < ng; g += 4) {
+        rd(cl(g + 2), BX0, BY0, BZ0);
+        rd(cl(g + 3), BX1, BY1, BZ1);
+        __builtin_amdgcn_sched_barrier(0);  // reads first, then A's (older) data is waited on
+        eval(g, AX0, AY0, AZ0);
+        if (g + 1 < ng) eval(g + 1, AX1, AY1, AZ1);
+        rd(cl(g + 4), AX0, AY0, AZ0);
+        rd(cl(g + 5), AX1, AY1, AZ1);
+        __builtin_amdgcn_sched_barrier(0);
+        if (g + 2 < ng) eval(g + 2, BX0, BY0, BZ0);
+        if (g + 3 < ng) eval(g + 3, BX1, BY1, BZ1);
       }
     } else {
       for (int blk = wv; blk < nblk; blk += NW) {
@@ -733,15 +746,18 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
 #if defined(KNN_EXP) && KNN_EXP == 7
     unsigned xacc = 0;
 #endif
+    // counter of bin e (clamped to [ebase, ebase + kNB]; the last = not
+    // counted, also NaN) at hwb + e * kBlk
+    unsigned* hwb = hw - ebase * kBlk;
     visit(ftop, [&](int, const float (&d)[4]) {
 #pragma unroll
       for (int h = 0; h < 4; h++) {
-        int bin = (int)(__float_as_uint(d[h]) >> 21) - ebase;
-        bin = bin < 0 ? 0 : (bin > kNB ? kNB : bin);  // kNB = not counted
+        int e = (int)(__float_as_uint(d[h]) >> 21);
+        e = max(ebase, min(e, ebase + kNB));
 #if defined(KNN_EXP) && KNN_EXP == 7
-        xacc += (unsigned)bin << (h * 5);
+        xacc += (unsigned)e << (h * 5);
 #else
-        __hip_atomic_fetch_add(hw + bin * kBlk, inc, __ATOMIC_RELAXED,
+        __hip_atomic_fetch_add(hwb + e * kBlk, inc, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_WORKGROUP);
 #endif
       }
