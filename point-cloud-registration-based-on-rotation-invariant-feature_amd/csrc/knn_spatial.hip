@@ -289,11 +289,6 @@ __device__ inline void merge_batch(kkey (&key)[KMAX], kkey (&q)[kQ]) {
   }
 }
 
-// value of lane l - 1 (lane 0 gets lane 63): DPP wave_ror:1
-__device__ inline float ror1(float v) {
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x13C, 0xF, 0xF, false));
-}
-
 __device__ inline float readlane_f(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
@@ -716,26 +711,6 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
       }
     }
   };
-  // Cached clouds: the 64 candidates of block blk through the lanes -- lane l
-  // starts with candidate l and the block rotates one lane per step (DPP
-  // wave_ror:1, plain VALU, no LDS traffic), so at step r lane l holds
-  // candidate (l - r) & 63; f(r, d of steps r and r + 1).
-  auto rotate_block = [&](int blk, auto&& f) {
-    const int p0 = blk * kBlk + lane;
-    float cx = cand_s[p0], cy = cand_s[kSelCache + p0], cz = cand_s[2 * kSelCache + p0];
-#pragma unroll
-    for (int r = 0; r < kBlk; r += 2) {
-      const float x0 = cx, y0 = cy, z0 = cz;
-      cx = ror1(cx);
-      cy = ror1(cy);
-      cz = ror1(cz);
-      const pf2 d = cand_dist2(qx2, qy2, qz2, pf2{x0, cx}, pf2{y0, cy}, pf2{z0, cz});
-      cx = ror1(cx);
-      cy = ror1(cy);
-      cz = ror1(cz);
-      f(r, d);
-    }
-  };
   // original indices of the four candidates at sorted position pos
   auto cand_idx4 = [&](int pos) {
     if (CL) return *(const int4*)(cand_j + pos);
@@ -774,27 +749,19 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     // counter of bin e (clamped to [ebase, ebase + kNB]; the last = not
     // counted, also NaN) at hwb + e * kBlk
     unsigned* hwb = hw - ebase * kBlk;
-    auto count = [&](float d) {
-      int e = (int)(__float_as_uint(d) >> 21);
-      e = max(ebase, min(e, ebase + kNB));
-#if defined(KNN_EXP) && KNN_EXP == 7
-      xacc += (unsigned)e;
-#else
-      __hip_atomic_fetch_add(hwb + e * kBlk, inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#endif
-    };
-    if (CL) {
-      for (int blk = wv; blk < nblk; blk += NW)
-        rotate_block(blk, [&](int, pf2 d) {
-          count(d[0]);
-          count(d[1]);
-        });
-    } else {
-      visit(ftop, [&](int, const float (&d)[4]) {
+    visit(ftop, [&](int, const float (&d)[4]) {
 #pragma unroll
-        for (int h = 0; h < 4; h++) count(d[h]);
-      });
-    }
+      for (int h = 0; h < 4; h++) {
+        int e = (int)(__float_as_uint(d[h]) >> 21);
+        e = max(ebase, min(e, ebase + kNB));
+#if defined(KNN_EXP) && KNN_EXP == 7
+        xacc += (unsigned)e << (h * 5);
+#else
+        __hip_atomic_fetch_add(hwb + e * kBlk, inc, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
+      }
+    });
 #if defined(KNN_EXP) && KNN_EXP == 7
     if (xacc == 0x9e3779b9u) hw[0] = xacc;
 #endif
@@ -845,45 +812,6 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
   if (!fallback) {
     // 4. collect
     const float fcut = __uint_as_float(ucut);
-    if (CL) {
-      // take bits (block slot bb, rotation step r), then gather the taken
-      // candidates lane by lane: at step r lane l held candidate (l - r) & 63
-      static_assert(kSelCache / kBlk <= 2 * NW, "at most two blocks per wave");
-      unsigned tm[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-      for (int bb = 0; bb < 2; bb++) {
-        const int blk = wv + bb * NW;
-        if (blk < nblk)
-          rotate_block(blk, [&](int r, pf2 d) {
-            const unsigned t0 = __float_as_uint(d[0]) < ucut ? 1u : 0u;
-            const unsigned t1 = __float_as_uint(d[1]) < ucut ? 1u : 0u;
-            tm[2 * bb + (r >> 5)] |= (t0 << (r & 31)) | (t1 << ((r + 1) & 31));
-          });
-      }
-      const int mine = __popc(tm[0]) + __popc(tm[1]) + __popc(tm[2]) + __popc(tm[3]);
-      int iters = mine;
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) iters = max(iters, __shfl_xor(iters, off, kWave));
-      iters = __builtin_amdgcn_readfirstlane(iters);
-      for (int it = 0; it < iters; it++) {
-        const int wsel = tm[0] ? 0 : (tm[1] ? 1 : (tm[2] ? 2 : 3));
-        const unsigned w = wsel == 0 ? tm[0] : (wsel == 1 ? tm[1] : (wsel == 2 ? tm[2] : tm[3]));
-        const int bit = w ? __builtin_ctz(w) : 0;
-        const unsigned clr = w & (w - 1u);
-        tm[0] = wsel == 0 ? clr : tm[0];
-        tm[1] = wsel == 1 ? clr : tm[1];
-        tm[2] = wsel == 2 ? clr : tm[2];
-        tm[3] = wsel == 3 ? clr : tm[3];
-        const int r = (wsel & 1) * 32 + bit;
-        const int p = (wv + (wsel >> 1) * NW) * kBlk + ((lane - r) & (kBlk - 1));
-        const float d = cand_dist(qx, qy, qz, cand_s[p], cand_s[kSelCache + p],
-                                  cand_s[2 * kSelCache + p]);
-        if (it < mine) {
-          buf_s[slot * kBlk + lane] = make_key(d, cand_j[p]);
-          slot++;
-        }
-      }
-    } else
     visit(fcut, [&](int pos, const float (&d)[4]) {
       bool take[4];
 #pragma unroll
