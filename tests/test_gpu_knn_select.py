@@ -1,0 +1,95 @@
+"""Parity of the KNN selection kernel's special paths against the oracle
+(bit-exact): the histogram / cut / collect / rank path, the exact LDS
+insertion fallback (too many collected keys, no finite bound), ties,
+unfilled slots, NaN and far-away points, ragged sizes, k = 1 .. 32."""
+import numpy as np
+import pytest
+
+import oracle
+from clouds import edge_clouds_for_knn, gaussian_clouds
+
+pytestmark = pytest.mark.gpu
+
+
+def T(a, dev):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def N(t):
+    return t.detach().cpu().numpy()
+
+
+def check_self(dev, xyz, k):
+    """knn_forward_cuda(xyz, xyz, k) and the fused knn_local_ppf vs the oracle."""
+    from pcr_amd import ops
+    xyz = np.ascontiguousarray(xyz, dtype=np.float32)
+    d1, d2, i1, i2 = ops.knn_forward_cuda(T(xyz, dev), T(xyz, dev), k)
+    e = oracle.knn_forward(xyz, xyz, k)
+    for name, got, exp in zip(("d1", "d2", "i1", "i2"), (d1, d2, i1, i2), e):
+        assert np.array_equal(N(got), exp, equal_nan=True), name
+    nrm = np.ascontiguousarray(np.roll(xyz, 1, axis=1))
+    idx, ppf, dist = ops.knn_local_ppf(T(xyz, dev), T(nrm, dev), k, want_dist=True)
+    assert np.array_equal(N(idx), e[2])
+    assert np.array_equal(N(dist), e[0])
+    ep = oracle.local_ppf(xyz, nrm, xyz, nrm, e[2], kmajor=True, relative=True)
+    assert np.array_equal(N(ppf), ep, equal_nan=True)
+
+
+@pytest.mark.parametrize("k", [1, 7, 16, 31, 32])
+def test_select_k_values(dev, k):
+    xyz, _, _ = gaussian_clouds(3, 1024, seed=20 + k)
+    check_self(dev, xyz, k)
+
+
+@pytest.mark.parametrize("n", [1000, 65, 129, 700])
+def test_select_ragged_sizes(dev, n):
+    xyz, _, _ = gaussian_clouds(2, n, seed=n)
+    check_self(dev, xyz, 32)
+
+
+def test_select_lattice_ties(dev):
+    """Integer lattice: many equal distances, ties broken by index."""
+    check_self(dev, edge_clouds_for_knn(2, 1024, seed=5), 32)
+
+
+def test_select_heavy_duplicates_fallback(dev):
+    """200 copies of one point: more than the collection capacity lands in one
+    bin, so those query blocks take the exact insertion fallback."""
+    xyz, _, _ = gaussian_clouds(2, 1024, seed=31)
+    xyz[:, :, 100:300] = xyz[:, :, 100:101]
+    check_self(dev, xyz, 32)
+
+
+def test_select_fewer_points_than_k(dev):
+    """n < k: unfilled slots stay (10000, 0)."""
+    xyz, _, _ = gaussian_clouds(2, 20, seed=3)
+    check_self(dev, xyz, 32)
+
+
+def test_select_far_points_unfilled(dev):
+    """Squared distances beyond 10000 are never selected (knn.cu:33-45):
+    a cloud of two far-apart clusters leaves slots unfilled."""
+    rng = np.random.default_rng(7)
+    xyz = rng.standard_normal((2, 3, 1024)).astype(np.float32)
+    xyz[:, :, 1000:] += np.float32(500.0)  # 24 points far away: their lists stay short
+    check_self(dev, xyz, 32)
+
+
+def test_select_nan_points(dev):
+    """A NaN point never enters any list; its own list stays unfilled."""
+    xyz, _, _ = gaussian_clouds(2, 1024, seed=9)
+    xyz[0, :, 17] = np.nan
+    xyz[1, 1, 400] = np.nan
+    check_self(dev, xyz, 32)
+
+
+def test_select_two_sets(dev):
+    """Non-self query/candidate sets of different sizes, both directions."""
+    from pcr_amd import ops
+    rng = np.random.default_rng(11)
+    x1 = rng.standard_normal((2, 3, 1024)).astype(np.float32)
+    x2 = (rng.standard_normal((2, 3, 900)) * 0.5 + 0.3).astype(np.float32)
+    got = ops.knn_forward_cuda(T(x1, dev), T(x2, dev), 32)
+    for a, b in zip(got, oracle.knn_forward(x1, x2, 32)):
+        assert np.array_equal(N(a), b)
