@@ -172,6 +172,32 @@ PCR_HD double pcr_atan_d(double x) {
 
 /* float acos/atan of the reference (CUDA float overloads), rounded once */
 PCR_HD float pcr_acosf(float x) { return (float)pcr_acos_d((double)x); }
+
+/* Faithful fp32 acos (error <= ~2 ulp, checked against float64 acos in
+ * tests/test_oracle_kat.py) for the local PPF: the reference evaluates it
+ * with torch.acos on fp32 tensors (pvcnn_classify.py:264-266), itself not
+ * correctly rounded, and the PPF angles carry a 1e-5 tolerance; the voxel
+ * bins keep the correctly rounded pcr_acosf.  asin(s) = s + s z P(z), z = s^2,
+ * |s| <= 0.5 (cephes asinf coefficients); the same three ranges as
+ * pcr_acos_d, without branches; pi/2 and pi split into hi + lo. */
+PCR_HD float pcr_asinf_core(float s) {
+  float z = s * s;
+  float p = __builtin_fmaf(4.2163199048e-2f, z, 2.4181311049e-2f);
+  p = __builtin_fmaf(p, z, 4.5470025998e-2f);
+  p = __builtin_fmaf(p, z, 7.4953002686e-2f);
+  p = __builtin_fmaf(p, z, 1.6666752422e-1f);
+  return __builtin_fmaf(s * z, p, s);
+}
+
+PCR_HD float pcr_acosf_fast(float x) {
+  const float pio2_hi = 1.57079637e+00f, pio2_lo = -4.37113883e-08f;
+  const float pi_hi = 3.14159274e+00f, pi_lo = -8.74227766e-08f;
+  float ax = __builtin_fabsf(x);
+  int mid = ax <= 0.5f;
+  float s = mid ? x : __builtin_sqrtf((1.0f - ax) * 0.5f);
+  float p = pcr_asinf_core(s);
+  return mid ? pio2_hi - (p - pio2_lo) : (x > 0.0f ? 2.0f * p : pi_hi - (2.0f * p - pi_lo));
+}
 PCR_HD float pcr_atanf(float x) { return (float)pcr_atan_d((double)x); }
 
 /* ---- spherical coordinates of a normalised point (spherical_vox.cu:34-56,
@@ -346,9 +372,9 @@ PCR_HD void pcr_local_ppf(float cx, float cy, float cz, float cnx, float cny, fl
   float dx = cx - gx, dy = cy - gy, dz = cz - gz;
   float dn = __builtin_sqrtf(pcr_sumsq3f(dx, dy, dz));
   float ux = dx / dn, uy = dy / dn, uz = dz / dn;
-  out[0] = pcr_acosf(pcr_clamp1f(pcr_dot3f(pnx, pny, pnz, ux, uy, uz)));
-  out[1] = pcr_acosf(pcr_clamp1f(pcr_dot3f(cnx, cny, cnz, ux, uy, uz)));
-  out[2] = pcr_acosf(pcr_clamp1f(pcr_dot3f(pnx, pny, pnz, cnx, cny, cnz)));
+  out[0] = pcr_acosf_fast(pcr_clamp1f(pcr_dot3f(pnx, pny, pnz, ux, uy, uz)));
+  out[1] = pcr_acosf_fast(pcr_clamp1f(pcr_dot3f(cnx, cny, cnz, ux, uy, uz)));
+  out[2] = pcr_acosf_fast(pcr_clamp1f(pcr_dot3f(pnx, pny, pnz, cnx, cny, cnz)));
   out[3] = dn;
 }
 

@@ -45,6 +45,7 @@ _SIGS = {
     "orc_local_ppf": [_i, _i, _i, _i, _f32p, _f32p, _f32p, _f32p, _i32p, _i, _i, _f32p],
     "orc_normalize_sph": [_i, _i, _f32p, _f32p],
     "orc_acosf_v": [_i, _f32p, _f32p],
+    "orc_acosf_fast_v": [_i, _f32p, _f32p],
     "orc_atanf_v": [_i, _f32p, _f32p],
     "orc_acos_d_v": [_i, _f64p, _f64p],
     "orc_sph_index_v": [_i, _f32p, _i, _i, _i32p],
@@ -247,6 +248,14 @@ def acosf(x):
     x = _f32(x).ravel()
     y = np.empty_like(x)
     lib().orc_acosf_v(x.size, x, y)
+    return y
+
+
+def acosf_fast(x):
+    """The local PPF's faithful fp32 acos (pcr_math.h pcr_acosf_fast)."""
+    x = _f32(x).ravel()
+    y = np.empty_like(x)
+    lib().orc_acosf_fast_v(x.size, x, y)
     return y
 
 

@@ -477,6 +477,11 @@ void orc_normalize_sph(int b, int n, const float *coords, float *norm_coords) {
 }
 
 /* -------------------------------------------------- math self-test hooks */
+void orc_acosf_fast_v(int n, const float *x, float *y) {
+  int i;
+  for (i = 0; i < n; i++) y[i] = pcr_acosf_fast(x[i]);
+}
+
 void orc_acosf_v(int n, const float *x, float *y) {
   int i;
   for (i = 0; i < n; i++) y[i] = pcr_acosf(x[i]);

@@ -26,6 +26,18 @@ def same(a, b):
     return np.array_equal(np.asarray(a), np.asarray(b), equal_nan=True)
 
 
+def same_lppf(a, b):
+    """Local PPF: the oracle's angles use the faithful fp32 acos of the
+    kernels (pcr_acosf_fast, <= 1.15 ulp), the NumPy restatement float64
+    arccos rounded once: angles within 2.5e-7, |d| bit-exact."""
+    a, b = np.asarray(a), np.asarray(b)
+    if not np.array_equal(np.isnan(a), np.isnan(b)):
+        return False
+    ok = ~np.isnan(a)
+    return (np.abs(a[:, :3] - b[:, :3])[ok[:, :3]].max(initial=0) <= 2.5e-7
+            and np.array_equal(a[:, 3:], b[:, 3:], equal_nan=True))
+
+
 def main():
     g = {}
     # ---- spherical voxelization on edge + random normalised coords (r=16, C=4)
@@ -92,11 +104,11 @@ def main():
     g["grp_grad_x"] = oracle.grouping_backward(gy, bq, pts.shape[2])
     # ---- local PPF (ball-query layout, model's relative quirk) and KNN layout
     lp = oracle.local_ppf(pts, pn, pts, pn, bq, kmajor=False, relative=True)
-    assert same(lp, R.local_ppf(pts, pn, pts, pn, bq, False, True))
+    assert same_lppf(lp, R.local_ppf(pts, pn, pts, pn, bq, False, True))
     g["lppf_ball"] = lp
     _, ki = oracle.knn_dir(pts, pts, 16)
     lk = oracle.local_ppf(pts, pn, pts, pn, ki, kmajor=True, relative=True)
-    assert same(lk, R.local_ppf(pts, pn, pts, pn, ki, True, True))
+    assert same_lppf(lk, R.local_ppf(pts, pn, pts, pn, ki, True, True))
     g.update(lppf_knn_idx=ki, lppf_knn=lk)
     # ---- global PPF with zero normals / coincident centre
     cen = np.repeat(pts.mean(axis=2, keepdims=True), pts.shape[2], axis=2)

@@ -132,3 +132,25 @@ def test_local_ppf_close_to_torch_model_block():
                      (nb * c).sum(1, keepdim=True)), 1).clamp(-1, 1).numpy()
     assert np.abs(np.cos(lp[:, :3]) - cos).max() < 2e-6
     assert np.abs(lp[:, 3:] - dn.numpy()).max() < 1e-6
+
+
+def test_acosf_fast_faithful():
+    """The local PPF's fp32 acos (pcr_acosf_fast) against float64 arccos:
+    <= 1.2 ulp everywhere on [-1, 1] (dense sweep + both range seams), exact
+    at -1, 0, 1, NaN in -> NaN out."""
+    rng = np.random.default_rng(0)
+    step = np.float32(6e-8)
+    x = np.concatenate([np.linspace(-1, 1, 400_001, dtype=np.float32),
+                        rng.uniform(-1, 1, 400_000).astype(np.float32),
+                        np.float32(0.5) + np.arange(-2000, 2000, dtype=np.float32) * step,
+                        np.float32(-0.5) + np.arange(-2000, 2000, dtype=np.float32) * step,
+                        np.float32(1) - np.arange(0, 20000, dtype=np.float32) * step,
+                        np.float32(-1) + np.arange(0, 20000, dtype=np.float32) * step])
+    x = np.clip(x, -1, 1).astype(np.float32)
+    y = oracle.acosf_fast(x).astype(np.float64)
+    ref = np.arccos(x.astype(np.float64))
+    ulp = np.spacing(ref.astype(np.float32)).astype(np.float64)
+    assert (np.abs(y - ref) / ulp).max() <= 1.2
+    e = oracle.acosf_fast(np.array([-1, 0, 1, np.nan], np.float32))
+    assert e[0] == np.float32(np.pi) and e[1] == np.float32(np.pi / 2) and e[2] == 0
+    assert np.isnan(e[3])
