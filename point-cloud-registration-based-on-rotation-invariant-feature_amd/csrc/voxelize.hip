@@ -636,6 +636,133 @@ __global__ __launch_bounds__(kPrepThreads) void sph_normalize_kernel(
   }
 }
 
+// ------------------------------------------------- clouds of > 4096 points
+// The reference algorithm as such (spherical_vox.cu:19-125, vox.cu:18-73):
+// per-point voxel index + count (global atomics), then every valid point adds
+// feature * (1 / count) to its voxel with global atomics.  The summation
+// order inside a voxel is arbitrary, as in the reference (parity within the
+// fp32 sum-order tolerance); indices and counts are exact.
+template <int MODE>
+__global__ __launch_bounds__(256) void vox_index_big_kernel(const float* __restrict__ coords_f,
+                                                            const int* __restrict__ coords_i,
+                                                            int n, int r, int* __restrict__ ind,
+                                                            int* __restrict__ cnt) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (i >= n) return;
+  const int r3 = r * r * r;
+  int v;
+  bool valid;
+  if (MODE == kCube) {
+    const int* x = coords_i + (size_t)b * 3 * n;
+    v = x[i] * r * r + x[i + n] * r + x[i + 2 * n];
+    valid = v >= 0 && v < r3;
+  } else {
+    const float* x = coords_f + (size_t)b * 3 * n;
+    v = pcr_sph_index(x[i], x[i + n], x[i + 2 * n], r);
+    valid = v >= 0;
+  }
+  ind[(size_t)b * n + i] = v;
+  if (valid) atomicAdd(&cnt[(size_t)b * r3 + v], 1);
+}
+
+__global__ __launch_bounds__(256) void vox_scatter_big_kernel(const float* __restrict__ feat,
+                                                              const int* __restrict__ ind,
+                                                              const int* __restrict__ cnt, int c,
+                                                              int n, int r3, int cg,
+                                                              float* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = blockIdx.z;
+  if (i >= n) return;
+  const int v = ind[(size_t)b * n + i];
+  if (v < 0 || v >= r3) return;
+  const float inv = pcr_inv_count(cnt[(size_t)b * r3 + v]);
+  const int c0 = blockIdx.y * cg, c1 = min(c, c0 + cg);
+  for (int j = c0; j < c1; j++)
+    atomicAdd(&out[((size_t)b * c + j) * r3 + v], feat[((size_t)b * c + j) * n + i] * inv);
+}
+
+// Fixed-order normalisation for any n (same order as cloud_mean: thread t
+// sums points t, t + 1024, ... ascending in double; wave halving trees).
+__global__ __launch_bounds__(kPrepThreads) void sph_normalize_big_kernel(
+    const float* __restrict__ coords, int n, float* __restrict__ out) {
+  __shared__ double red[48];
+  __shared__ float s_stat[4];
+  __shared__ float wm[kPrepThreads / kWave];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const float* x = coords + (size_t)b * 3 * n;
+  float* o = out + (size_t)b * 3 * n;
+  double s[3] = {0.0, 0.0, 0.0};
+  for (int i = tid; i < n; i += kPrepThreads) {
+    s[0] += (double)x[i];
+    s[1] += (double)x[i + n];
+    s[2] += (double)x[i + 2 * n];
+  }
+#pragma unroll
+  for (int a = 0; a < 3; a++) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const double v = __shfl_down(s[a], off, kWave);
+      if (lane < off) s[a] += v;
+    }
+    if (lane == 0) red[a * 16 + w] = s[a];
+  }
+  __syncthreads();
+  if (tid < 3) {
+    double v[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) v[i] = red[tid * 16 + i];
+#pragma unroll
+    for (int off = 8; off > 0; off >>= 1)
+#pragma unroll
+      for (int i = 0; i < off; i++) v[i] += v[i + off];
+    s_stat[tid] = (float)(v[0] / (double)n);
+  }
+  __syncthreads();
+  const float m0 = s_stat[0], m1 = s_stat[1], m2 = s_stat[2];
+  float mx = 0.0f;
+  for (int i = tid; i < n; i += kPrepThreads)
+    mx = fmaxf(mx, __builtin_sqrtf(pcr_sumsq3f(x[i] - m0, x[i + n] - m1, x[i + 2 * n] - m2)));
+  mx = wave_max(mx);
+  if (lane == 0) wm[w] = mx;
+  __syncthreads();
+  if (tid == 0) {
+    float m = 0.0f;
+    for (int k = 0; k < kPrepThreads / kWave; k++) m = fmaxf(m, wm[k]);
+    s_stat[3] = m + 1e-20f;
+  }
+  __syncthreads();
+  const float den = s_stat[3];
+  for (int i = tid; i < n; i += kPrepThreads) {
+    o[i] = (x[i] - m0) / den;
+    o[i + n] = (x[i + n] - m1) / den;
+    o[i + 2 * n] = (x[i + 2 * n] - m2) / den;
+  }
+}
+
+template <int MODE>
+static pcr_status run_voxelize_big(const float* features, const float* coords_f,
+                                   const int* coords_i, int b, int c, int n, int r, float* out,
+                                   int* ind, int* cnt, hipStream_t stream, const char* name) {
+  const int r3 = r * r * r;
+  PCR_REQUIRE(cnt != nullptr && ind != nullptr, "%s: ind and cnt required", name);
+  if (hipMemsetAsync(cnt, 0, (size_t)b * r3 * sizeof(int), stream) != hipSuccess ||
+      (c > 0 && out &&
+       hipMemsetAsync(out, 0, (size_t)b * c * r3 * sizeof(float), stream) != hipSuccess)) {
+    set_error("%s: memset failed", name);
+    return PCR_ERR_LAUNCH;
+  }
+  hipLaunchKernelGGL(vox_index_big_kernel<MODE>, dim3(ceil_div(n, 256), b), dim3(256), 0, stream,
+                     coords_f, coords_i, n, r, ind, cnt);
+  if (c > 0 && out) {
+    const int cg = 8;
+    hipLaunchKernelGGL(vox_scatter_big_kernel, dim3(ceil_div(n, 256), ceil_div(c, cg), b),
+                       dim3(256), 0, stream, features, ind, cnt, c, n, r3, cg, out);
+  }
+  return launch_status(name);
+}
+
 // ------------------------------------------------------------- launchers
 static int pick_groups(int c, int n, int max_g, int* G_out) {
   // LDS per grid WG ~ (2*G + 1) * n * 4 + bitmap: at most max_g channels
@@ -661,8 +788,11 @@ static pcr_status run_voxelize(const float* features, const float* coords_f, con
               b, c, n, r);
   PCR_REQUIRE((int64_t)r * r * r <= (1 << 24), "%s: resolution %d too large", name, r);
   if (b == 0) return PCR_OK;
+  if (n > kMaxSortN && MODE != kSphNormalize && what == 3 && devox == nullptr)
+    return run_voxelize_big<MODE>(features, coords_f, coords_i, b, c, n, r, out, ind, cnt, stream,
+                                  name);
   PCR_REQUIRE(n >= 1 && n <= kMaxSortN,
-              "%s: n=%d points per cloud unsupported (1..%d in this build)", name, n, kMaxSortN);
+              "%s: n=%d points per cloud unsupported on this path (1..%d)", name, n, kMaxSortN);
   const int r3 = r * r * r;
   VoxWs ws;
   size_t need = vox_ws_layout(b, n, r, &ws, workspace);
@@ -761,7 +891,11 @@ extern "C" pcr_status pcr_spherical_normalize(const float* coords, int b, int n,
                                               float* norm_coords, void* stream) {
   PCR_REQUIRE(b >= 0 && n >= 1, "spherical_normalize: invalid sizes b=%d n=%d", b, n);
   if (b == 0) return PCR_OK;
-  PCR_REQUIRE(n <= kMaxSortN, "spherical_normalize: n=%d > %d unsupported", n, kMaxSortN);
+  if (n > kMaxSortN) {
+    hipLaunchKernelGGL(sph_normalize_big_kernel, dim3(b), dim3(kPrepThreads), 0,
+                       as_stream(stream), coords, n, norm_coords);
+    return launch_status("spherical_normalize");
+  }
   const int E = next_pow2(n < kPrepThreads ? kPrepThreads : n) / kPrepThreads;
   hipLaunchKernelGGL(sph_normalize_kernel, dim3(b), dim3(kPrepThreads), 0, as_stream(stream),
                      coords, n, E, norm_coords);

@@ -1,0 +1,111 @@
+"""Clouds beyond the 4096-point single-workgroup paths (BASELINE c5: 8 x
+65,536 points, k = 64, r = 64): normalisation, spherical / cube
+voxelisation on the global-atomic path, devoxelisation and KNN, against the
+oracle at sizes it finishes in seconds, plus size-independent properties at
+the full c5 cloud size."""
+import numpy as np
+import pytest
+
+import oracle
+from clouds import gaussian_clouds
+
+pytestmark = pytest.mark.gpu
+
+# voxel means summed in atomic (arbitrary) order, as the reference does
+SUM_ORDER_TOL = 1e-5
+
+
+def T(a, dev):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def N(t):
+    return t.detach().cpu().numpy()
+
+
+def test_normalize_large(dev):
+    from pcr_amd import ops
+    xyz, _, _ = gaussian_clouds(2, 20000, seed=41)
+    xyz = xyz * np.float32(2.5) + np.float32(0.7)
+    got = ops.spherical_normalize(T(xyz, dev))
+    assert np.array_equal(N(got), oracle.normalize_sph(xyz))
+
+
+def test_sph_vox_large(dev):
+    from pcr_amd import ops
+    xyz, _, feat = gaussian_clouds(2, 20000, seed=42, c=8)
+    nc = oracle.normalize_sph(xyz)
+    out, ind, cnt = ops.spherical_avg_voxelize_forward(T(feat, dev), T(nc, dev), 64)
+    eo, ei, ec = oracle.spherical_avg_voxelize_forward(feat, nc, 64)
+    assert np.array_equal(N(ind), ei)
+    assert np.array_equal(N(cnt), ec.reshape(N(cnt).shape))
+    assert np.abs(N(out).reshape(eo.shape) - eo).max() <= SUM_ORDER_TOL
+
+
+def test_cube_vox_large(dev):
+    from pcr_amd import ops
+    rng = np.random.default_rng(43)
+    b, n, c, r = 2, 12000, 5, 32
+    coords = rng.integers(0, r, size=(b, 3, n)).astype(np.int32)
+    coords[:, :, :7] = -1  # out-of-range voxel coordinates
+    feat = rng.standard_normal((b, c, n)).astype(np.float32)
+    out, ind, cnt = ops.avg_voxelize_forward(T(feat, dev), T(coords, dev), r)
+    eo, ei, ec = oracle.avg_voxelize_forward(feat, coords, r)
+    assert np.array_equal(N(ind), ei)
+    assert np.array_equal(N(cnt), ec.reshape(N(cnt).shape))
+    assert np.abs(N(out).reshape(eo.shape) - eo).max() <= SUM_ORDER_TOL
+
+
+def test_sph_devox_large(dev):
+    from pcr_amd import ops
+    xyz, _, feat = gaussian_clouds(2, 20000, seed=44, c=4)
+    nc = oracle.normalize_sph(xyz)
+    grid, gind, _ = oracle.spherical_avg_voxelize_forward(feat, nc, 64)
+    outs, inds, wgts = ops.spherical_trilinear_devoxelize_forward(
+        64, False, T(nc, dev), T(grid.reshape(2, 4, -1), dev), T(gind, dev))
+    eo, ei, ew = oracle.spherical_trilinear_devoxelize_forward(64, nc, grid, gind)
+    assert np.array_equal(N(inds), ei)
+    assert np.array_equal(N(wgts), ew)
+    assert np.abs(N(outs) - eo).max() <= SUM_ORDER_TOL
+
+
+def test_knn_large_k64(dev):
+    from pcr_amd import ops
+    xyz, nrm, _ = gaussian_clouds(1, 8192, seed=45)
+    d1, d2, i1, i2 = ops.knn_forward_cuda(T(xyz, dev), T(xyz, dev), 64)
+    e = oracle.knn_forward(xyz, xyz, 64)
+    for got, exp in zip((d1, d2, i1, i2), e):
+        assert np.array_equal(N(got), exp)
+    idx, ppf, _ = ops.knn_local_ppf(T(xyz, dev), T(nrm, dev), 64)
+    assert np.array_equal(N(idx), e[2])
+    ep = oracle.local_ppf(xyz, nrm, xyz, nrm, e[2], kmajor=True, relative=True)
+    assert np.array_equal(N(ppf), ep, equal_nan=True)
+
+
+def test_c5_cloud_properties(dev):
+    """One c5-sized cloud (65,536 points, k = 64, r = 64, C = 64):
+    size-independent properties of the whole path."""
+    import torch
+    from pcr_amd import ops
+    n, k, r, c = 65536, 64, 64, 64
+    xyz, nrm, feat = gaussian_clouds(1, n, seed=46, c=c)
+    tx, tn, tf = T(xyz, dev), T(nrm, dev), T(feat, dev)
+    idx, ppf, dist = ops.knn_local_ppf(tx, tn, k, want_dist=True)
+    i, d = N(idx), N(dist)
+    assert ((i >= 0) & (i < n)).all()
+    assert (np.diff(d, axis=1) >= 0).all()                      # ascending per point
+    assert (d[:, 0] == 0).all()                                 # self (or a duplicate)
+    samp = np.random.default_rng(0).choice(n, 64, replace=False)
+    ref_d, ref_i = oracle.knn_dir(np.ascontiguousarray(xyz[:, :, samp]), xyz, k)
+    assert np.array_equal(d[0][:, samp], ref_d[0])             # spot-check exact lists
+    assert np.array_equal(i[0][:, samp], ref_i[0])
+    nc = ops.spherical_normalize(tx)
+    out, ind, cnt = ops.spherical_avg_voxelize_forward(tf, nc, r)
+    ind_, cnt_ = N(ind), N(cnt).reshape(1, -1)
+    valid = ind_ >= 0
+    assert cnt_.sum() == valid.sum()
+    assert np.array_equal(np.bincount(ind_[valid], minlength=r ** 3), cnt_[0])
+    grid = N(out).reshape(1, c, -1)
+    assert (grid[:, :, cnt_[0] == 0] == 0).all()
+    torch.cuda.synchronize()
