@@ -48,7 +48,8 @@ def parse():
     ap.add_argument("--kernel-iters", type=int, default=50)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--mode", choices=("pipelined", "pipelined2", "pipelined4", "graph", "eager"),
+    ap.add_argument("--mode", choices=("pipelined", "pipelined2", "pipelined4", "pipelined_sv",
+                                       "graph", "eager"),
                     default="pipelined",
                     help="pipelined: S steps enqueued with no join between them; graph: one "
                          "hipGraph replay per step; eager: fork/join launches per step")
@@ -146,7 +147,7 @@ def main():
         if args.mode.startswith("pipelined"):
             ex.run_pipelined(xyz, nrm, feat, S, desc_steps,
                              mode={"pipelined": "three", "pipelined2": "two",
-                                   "pipelined4": "four"}[args.mode])
+                                   "pipelined4": "four", "pipelined_sv": "sortvox"}[args.mode])
             src = desc_steps.view(S * b, c)
         elif args.mode == "graph":
             ex.replay()

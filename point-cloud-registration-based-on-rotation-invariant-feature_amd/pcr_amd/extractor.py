@@ -244,6 +244,34 @@ class SphExtractor:
                 dev_done[slot].record(self.s_dev)
             self._join(cur)
             return self.outputs(slot=(steps - 1) & 1)
+        if mode == "sortvox":
+            # the Morton sort moves to the voxel stream, ahead of prep: s_nbr
+            # only selects (+ PPF); sorted / voxel buffers alternate per step
+            sn, sv, sd = self.s_nbr.cuda_stream, self.s_vox.cuda_stream, self.s_dev.cuda_stream
+            sel_done, dev_done = [None, None], [None, None]
+            for s in range(steps):
+                slot = s & 1
+                d = None if desc_steps is None else desc_steps[s]
+                for ev in (sel_done[slot], dev_done[slot]):  # step s-2's readers
+                    if ev is not None:
+                        self.s_vox.wait_event(ev)
+                ok = self.knn_sort(xyz, sv, slot)
+                e_sort = torch.cuda.Event()
+                e_sort.record(self.s_vox)
+                self.voxel_prep(xyz, sv, slot)
+                e_prep = torch.cuda.Event()
+                e_prep.record(self.s_vox)
+                self.voxel_grid(features, sv, slot)
+                self.s_nbr.wait_event(e_sort)
+                self.knn_select(xyz, normals, sn, slot, ok)
+                sel_done[slot] = torch.cuda.Event()
+                sel_done[slot].record(self.s_nbr)
+                self.s_dev.wait_event(e_prep)
+                self.voxel_devox(features, sd, d, slot)
+                dev_done[slot] = torch.cuda.Event()
+                dev_done[slot].record(self.s_dev)
+            self._join(cur)
+            return self.outputs(slot=(steps - 1) & 1)
         if mode == "two":
             sn, sv = self.s_nbr.cuda_stream, self.s_vox.cuda_stream
             for s in range(steps):
