@@ -48,11 +48,12 @@ def parse():
     ap.add_argument("--kernel-iters", type=int, default=50)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--mode", choices=("pipelined", "pipelined2", "pipelined4", "pipelined_sv",
+    ap.add_argument("--mode", choices=("pipelined", "pipelined3", "pipelined4", "pipelined_sv",
                                        "graph", "eager"),
                     default="pipelined",
-                    help="pipelined: S steps enqueued with no join between them; graph: one "
-                         "hipGraph replay per step; eager: fork/join launches per step")
+                    help="pipelined: S steps on two independent streams (KNN / voxel) with "
+                         "no join between them; pipelined3/4/_sv: schedules with cross-stream "
+                         "events; graph: one hipGraph replay per step; eager: fork/join per step")
     ap.add_argument("--steps-per-launch", type=int, default=10,
                     help="pipelined steps per launch group (must divide --steps and --warmup)")
     return ap.parse_args()
@@ -146,7 +147,7 @@ def main():
         """Steps i*S .. i*S+S-1."""
         if args.mode.startswith("pipelined"):
             ex.run_pipelined(xyz, nrm, feat, S, desc_steps,
-                             mode={"pipelined": "three", "pipelined2": "two",
+                             mode={"pipelined": "two", "pipelined3": "three",
                                    "pipelined4": "four", "pipelined_sv": "sortvox"}[args.mode])
             src = desc_steps.view(S * b, c)
         elif args.mode == "graph":

@@ -208,17 +208,18 @@ class SphExtractor:
             "dinds": dinds, "dwgts": dwgts, "desc": self.desc,
         }
 
-    def run_pipelined(self, xyz, normals, features, steps, desc_steps=None, mode="three"):
+    def run_pipelined(self, xyz, normals, features, steps, desc_steps=None, mode="two"):
         """Enqueue `steps` consecutive steps with no join between them, forked
         from and joined back to the current stream once.  Step s writes its
         descriptor to desc_steps[s] when given.
 
-        mode "three" (default): s_nbr runs sort + select of every step, s_vox
+        mode "two" (default, fastest measured: fewest cross-stream edges):
+        s_nbr runs sort + select + PPF of every step, s_vox prep + grid +
+        devox, two independent streams joined once at the end ("two_dg":
+        devox before grid).
+        mode "three": s_nbr runs sort + select of every step, s_vox
         prep + grid, s_dev devox after its step's prep, on alternating buffer
         sets (prep waits only for the devox two steps back).
-        mode "two": two independent streams and no cross-stream edge at all --
-        s_nbr runs sort + select of every step, s_vox prep + grid + devox of
-        every step (each stream reuses its own buffers in stream order).
         mode "four": the four-stream schedule of enqueue() on alternating
         buffer sets (front stages of step i+1 overlap step i's back stages).
         Eager launches (ROCm's stream capture rejects the cross-step edges)."""
@@ -272,15 +273,19 @@ class SphExtractor:
                 dev_done[slot].record(self.s_dev)
             self._join(cur)
             return self.outputs(slot=(steps - 1) & 1)
-        if mode == "two":
+        if mode in ("two", "two_dg"):
             sn, sv = self.s_nbr.cuda_stream, self.s_vox.cuda_stream
             for s in range(steps):
                 d = None if desc_steps is None else desc_steps[s]
                 ok = self.knn_sort(xyz, sn)
                 self.knn_select(xyz, normals, sn, 0, ok)
                 self.voxel_prep(xyz, sv)
-                self.voxel_grid(features, sv)
-                self.voxel_devox(features, sv, d)
+                if mode == "two":
+                    self.voxel_grid(features, sv)
+                    self.voxel_devox(features, sv, d)
+                else:
+                    self.voxel_devox(features, sv, d)
+                    self.voxel_grid(features, sv)
             self._join(cur)
             return self.outputs()
         pending = [None, None]

@@ -26,9 +26,9 @@ for step in "$@"; do
     tests_all) run pytest_gpu 1200 python -m pytest tests -q -m gpu -p no:cacheprovider ;;
     bench) run bench 600 python bench.py ;;
     modes) run bench_psv 300 python bench.py --mode pipelined_sv --no-cpu-baseline
-           run bench_p3 300 python bench.py --mode pipelined --no-cpu-baseline
+           run bench_p3 300 python bench.py --mode pipelined3 --no-cpu-baseline
            run bench_p4 300 python bench.py --mode pipelined4 --no-cpu-baseline
-           run bench_p2 300 python bench.py --mode pipelined2 --no-cpu-baseline
+
            run bench_graph 300 python bench.py --mode graph --no-cpu-baseline
            run bench_eager 300 python bench.py --mode eager --no-cpu-baseline ;;
     prof) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
