@@ -43,6 +43,7 @@ struct VoxWs {
   int* nseg;         // [b]
   unsigned* bitmap;  // [b][W] occupancy bits
   int* wprefix;      // [b][W] occupied voxels before word w
+  int* dseg;         // [b][8][n] segment of each devox corner (-1: empty / none)
   int W;             // words per cloud = ceil(r^3 / 32)
 };
 
@@ -64,7 +65,9 @@ static size_t vox_ws_layout(int b, int n, int r, VoxWs* ws, void* base) {
   int* nseg = (int*)take((size_t)b * 4);
   unsigned* bitmap = (unsigned*)take((size_t)b * W * 4);
   int* wprefix = (int*)take((size_t)b * W * 4);
+  int* dseg = (int*)take((size_t)b * 8 * n * 4);
   if (ws) {
+    ws->dseg = dseg;
     ws->perm = perm;
     ws->seg_off = seg_off;
     ws->seg_vox = seg_vox;
@@ -286,6 +289,30 @@ __global__ __launch_bounds__(kPrepThreads) void vox_prep_kernel(
   }
   __syncthreads();
   const int nseg = __float_as_int(s_stat[0]);
+  // devox corners -> their voxel's segment (the grid kernel's devox part
+  // gathers the voxel means by segment without a bitmap lookup); this
+  // thread wrote the corners above, so it reads them back itself
+  if (MODE == kSphNormalize && dinds) {
+    const int* I = dinds + (size_t)b * 8 * n;
+    int* D = ws.dseg + (size_t)b * 8 * n;
+#pragma unroll
+    for (int e = 0; e < kMaxE; e++) {
+      const int i = e * nt + tid;
+      if (e < E && i < n) {
+        const bool skip = I[i] == -1;
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+          const int cell = I[i + (size_t)q * n];
+          int sg = -1;
+          if (!skip && cell >= 0 && cell < r3) {
+            const unsigned word = bm[cell >> 5], bit = 1u << (cell & 31);
+            if (word & bit) sg = pre_l[cell >> 5] + __popc(word & (bit - 1u));
+          }
+          D[i + (size_t)q * n] = sg;
+        }
+      }
+    }
+  }
   // 3. counts per segment; arrival slot within the segment (unstable)
   int seg_of[kMaxE], slot_of[kMaxE];
 #pragma unroll
@@ -505,24 +532,17 @@ __global__ __launch_bounds__(NT) void vox_grid_kernel(
     float vmax[kMaxG];
 #pragma unroll
     for (int g = 0; g < kMaxG; g++) vmax[g] = -__builtin_inff();
+    // corner -> segment map from prep (ws.dseg): the segment ids are the
+    // rows of mean_s (one tile: s_begin = 0)
+    const int* Dg = ws.dseg + (size_t)b * 8 * n;
     for (int i = tid; i < n; i += NT) {
-      int ci[8];
       float cw[8];
       int rk[8];
       const bool skip = I[i] == -1;
 #pragma unroll
       for (int q = 0; q < 8; q++) {
-        ci[q] = I[i + (size_t)q * n];
         cw[q] = Wt[i + (size_t)q * n];
-        int cell = ci[q];
-        int rr = -1;
-        if (!skip && cell >= 0 && cell < r3) {
-          const int wl = (cell >> 5) - wb;
-          const unsigned word = bm_s[wl];
-          const unsigned bit = 1u << (cell & 31);
-          if (word & bit) rr = pre_s[wl] + __popc(word & (bit - 1u));
-        }
-        rk[q] = rr;
+        rk[q] = Dg[i + (size_t)q * n];
       }
 #pragma unroll
       for (int g = 0; g < kMaxG; g++) {
@@ -817,8 +837,11 @@ static pcr_status run_voxelize(const float* features, const float* coords_f, con
     PCR_REQUIRE(c > 0, "%s: fused devoxelisation needs c > 0", name);
   }
   if (do_grid && do_dev) {
+    // streaming + devox from the same LDS means: two channels per workgroup
+    // as in the streaming-only part; the devox tail gathers by prep's
+    // corner -> segment map
     int G = 1;
-    const int ngrp = pick_groups(c, n, 4, &G);
+    const int ngrp = pick_groups(c, n, 2, &G);
     const size_t smem = grid_smem_bytes(G, n, nw);
     PCR_REQUIRE(smem <= 150 * 1024, "%s: grid LDS %zu too large", name, smem);
     allow_big_lds(vox_grid_kernel<3, kGridThreads>, smem);

@@ -111,11 +111,13 @@ class SphExtractor:
                 self.n, self.n, self.k, 1, int(self.relative), _ptr(self.local_ppf), stream),
                 "local_ppf_forward")
 
-    def voxel_stage(self, xyz, features, stream):
+    def voxel_stage(self, xyz, features, stream, desc=None):
+        """prep + the fused grid / devox / descriptor kernel, one call."""
+        d = self.desc if desc is None else desc
         _lib.check(_lib.load().pcr_extractor_voxel_stage(
             _ptr(xyz), _ptr(features), self.b, self.c, self.n, self.r, _ptr(self.norm_coords),
             _ptr(self.ind), _ptr(self.cnt), _ptr(self.grid), _ptr(self.devox), _ptr(self.dinds),
-            _ptr(self.dwgts), _ptr(self.desc), _ptr(self.ws), self.ws.numel(), stream),
+            _ptr(self.dwgts), _ptr(d), _ptr(self.ws), self.ws.numel(), stream),
             "extractor_voxel_stage")
 
     def voxel_prep(self, xyz, stream, slot=0):
@@ -273,6 +275,16 @@ class SphExtractor:
                 dev_done[slot].record(self.s_dev)
             self._join(cur)
             return self.outputs(slot=(steps - 1) & 1)
+        if mode == "two_fused":
+            # voxel stream: prep, then one kernel for grid + devox + descriptor
+            sn, sv = self.s_nbr.cuda_stream, self.s_vox.cuda_stream
+            for s in range(steps):
+                d = None if desc_steps is None else desc_steps[s]
+                ok = self.knn_sort(xyz, sn)
+                self.knn_select(xyz, normals, sn, 0, ok)
+                self.voxel_stage(xyz, features, sv, d)
+            self._join(cur)
+            return self.outputs()
         if mode in ("two", "two_dg"):
             sn, sv = self.s_nbr.cuda_stream, self.s_vox.cuda_stream
             for s in range(steps):
