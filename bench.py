@@ -13,7 +13,7 @@ GPU (torch.distributed, RCCL), the batch is sharded by cloud (weak scaling:
 (registration matching), overlapped on a side stream.
 
 Prints ONE JSON line (rank 0).  `roofline` prices the dominant kernel (the
-voxel-grid kernel, vox_grid_kernel<1>: dense [B,C,r^3] grid + cnt) from its HIP-event-timed average duration;
+voxel kernel of the step, vox_grid_kernel<3>: dense [B,C,r^3] grid + cnt, devox + descriptor) from its HIP-event-timed average duration;
 `cpu_baseline` times the CPU restatement (oracle/, the "port") on a bounded
 sample of the same workload on this box's host cores.
 """
@@ -48,11 +48,12 @@ def parse():
     ap.add_argument("--kernel-iters", type=int, default=50)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--mode", choices=("pipelined", "pipelined3", "pipelined4", "pipelined_sv",
-                                       "graph", "eager"),
+    ap.add_argument("--mode", choices=("pipelined", "pipelined_split", "pipelined3", "pipelined4",
+                                       "pipelined_sv", "graph", "eager"),
                     default="pipelined",
-                    help="pipelined: S steps on two independent streams (KNN / voxel) with "
-                         "no join between them; pipelined3/4/_sv: schedules with cross-stream "
+                    help="pipelined: S steps on two independent streams (KNN / voxel, fused "
+                         "grid+devox kernel) with no join between them; pipelined_split: "
+                         "separate grid and devox launches; pipelined3/4/_sv: schedules with cross-stream "
                          "events; graph: one hipGraph replay per step; eager: fork/join per step")
     ap.add_argument("--steps-per-launch", type=int, default=10,
                     help="pipelined steps per launch group (must divide --steps and --warmup)")
@@ -124,7 +125,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from pcr_amd.extractor import (SphExtractor, algorithmic_bytes_per_cloud,
-                                   grid_kernel_bytes_per_cloud)
+                                   fused_grid_kernel_bytes_per_cloud)
     b, n, c, k, r = args.batch, args.points, args.channels, args.k, args.res
     xyz, nrm, feat = synthetic_inputs(b, n, c, dev, seed=1234 + rank)
     ex = SphExtractor(b, n, c, k, r, device=dev)
@@ -147,7 +148,8 @@ def main():
         """Steps i*S .. i*S+S-1."""
         if args.mode.startswith("pipelined"):
             ex.run_pipelined(xyz, nrm, feat, S, desc_steps,
-                             mode={"pipelined": "two", "pipelined3": "three",
+                             mode={"pipelined": "two_fused", "pipelined_split": "two",
+                                   "pipelined3": "three",
                                    "pipelined4": "four", "pipelined_sv": "sortvox"}[args.mode])
             src = desc_steps.view(S * b, c)
         elif args.mode == "graph":
@@ -201,12 +203,12 @@ def main():
         for e0, e1 in ev:
             ex.voxel_prep(xyz, s_k.cuda_stream)
             e0.record(s_k)
-            ex.voxel_grid(feat, s_k.cuda_stream)
+            ex.voxel_grid_devox(feat, s_k.cuda_stream)
             e1.record(s_k)
     torch.cuda.synchronize(dev)
     grid_ms = sorted(e0.elapsed_time(e1) for e0, e1 in ev)
     grid_avg_ms = sum(grid_ms) / len(grid_ms)
-    grid_bytes = grid_kernel_bytes_per_cloud(n, r, c) * b
+    grid_bytes = fused_grid_kernel_bytes_per_cloud(n, r, c) * b
     achieved = grid_bytes / (grid_avg_ms * 1e-3) / 1e9
 
     total_clouds = b * world * args.steps
@@ -245,7 +247,8 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic,
-                     "kernel": "vox_grid_kernel<1> (sph-vox dense grid + cnt)",
+                     "kernel": "vox_grid_kernel<3> (sph-vox dense grid + cnt, sph-devox + "
+                               "descriptor)",
                      "kernel_avg_ms": round(grid_avg_ms, 5),
                      "kernel_bytes_per_launch": grid_bytes},
         "step_algorithmic_GBps": round(step_bytes * world * args.steps / elapsed / 1e9, 1),

@@ -218,6 +218,13 @@ pcr_status pcr_extractor_voxel_devox(const float *features, int b, int c, int n,
                                      float *devox, const int *dinds, const float *dwgts,
                                      float *desc, void *workspace, size_t workspace_bytes,
                                      void *stream);
+/* grid + devox + descriptor in one launch after prep (the devox tail gathers
+ * the voxel means the workgroup already holds in LDS, through prep's corner
+ * -> segment map): what pcr_extractor_voxel_stage launches after prep. */
+pcr_status pcr_extractor_voxel_grid_devox(const float *features, int b, int c, int n, int r,
+                                          int *cnt, float *grid, float *devox, const int *dinds,
+                                          const float *dwgts, float *desc, void *workspace,
+                                          size_t workspace_bytes, void *stream);
 
 /* ------------------------------------------------------ self tests ------
  * Device evaluation of the shared bit-exact math (include/pcr_math.h) for

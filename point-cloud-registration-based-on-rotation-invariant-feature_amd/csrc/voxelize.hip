@@ -962,6 +962,19 @@ extern "C" pcr_status pcr_extractor_voxel_devox(const float* features, int b, in
                                      desc, "extractor_voxel_devox", 4);
 }
 
+extern "C" pcr_status pcr_extractor_voxel_grid_devox(const float* features, int b, int c, int n,
+                                                     int r, int* cnt, float* grid, float* devox,
+                                                     const int* dinds, const float* dwgts,
+                                                     float* desc, void* workspace,
+                                                     size_t workspace_bytes, void* stream) {
+  PCR_REQUIRE(grid != nullptr && devox != nullptr && dinds != nullptr && dwgts != nullptr,
+              "extractor_voxel_grid_devox: grid, devox, dinds, dwgts required");
+  return run_voxelize<kSphNormalize>(features, nullptr, nullptr, b, c, n, r, grid, nullptr, cnt,
+                                     workspace, workspace_bytes, as_stream(stream), nullptr,
+                                     devox, const_cast<int*>(dinds), const_cast<float*>(dwgts),
+                                     desc, "extractor_voxel_grid_devox", 6);
+}
+
 extern "C" pcr_status pcr_extractor_voxel_stage(const float* xyz, const float* features, int b,
                                                 int c, int n, int r, float* norm_coords, int* ind,
                                                 int* cnt, float* grid, float* devox, int* dinds,

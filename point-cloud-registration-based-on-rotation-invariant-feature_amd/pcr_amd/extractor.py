@@ -133,6 +133,15 @@ class SphExtractor:
             _ptr(features), self.b, self.c, self.n, self.r, _ptr(self.cnt), _ptr(self.grid),
             _ptr(ws), ws.numel(), stream), "extractor_voxel_grid")
 
+    def voxel_grid_devox(self, features, stream, desc=None):
+        """The dominant kernel of the default step (vox_grid_kernel<3>: dense
+        grid + cnt, devox + descriptor from the same LDS means)."""
+        d = self.desc if desc is None else desc
+        _lib.check(_lib.load().pcr_extractor_voxel_grid_devox(
+            _ptr(features), self.b, self.c, self.n, self.r, _ptr(self.cnt), _ptr(self.grid),
+            _ptr(self.devox), _ptr(self.dinds), _ptr(self.dwgts), _ptr(d), _ptr(self.ws),
+            self.ws.numel(), stream), "extractor_voxel_grid_devox")
+
     def voxel_devox(self, features, stream, desc=None, slot=0):
         _, ws, dinds, dwgts = self._set(slot)
         d = self.desc if desc is None else desc
@@ -210,14 +219,15 @@ class SphExtractor:
             "dinds": dinds, "dwgts": dwgts, "desc": self.desc,
         }
 
-    def run_pipelined(self, xyz, normals, features, steps, desc_steps=None, mode="two"):
+    def run_pipelined(self, xyz, normals, features, steps, desc_steps=None, mode="two_fused"):
         """Enqueue `steps` consecutive steps with no join between them, forked
         from and joined back to the current stream once.  Step s writes its
         descriptor to desc_steps[s] when given.
 
-        mode "two" (default, fastest measured: fewest cross-stream edges):
-        s_nbr runs sort + select + PPF of every step, s_vox prep + grid +
-        devox, two independent streams joined once at the end ("two_dg":
+        mode "two_fused" (default, fastest measured): two independent streams
+        joined once at the end -- s_nbr runs sort + select + PPF of every
+        step, s_vox prep + the fused grid / devox / descriptor kernel.
+        mode "two": the same with separate grid and devox launches ("two_dg":
         devox before grid).
         mode "three": s_nbr runs sort + select of every step, s_vox
         prep + grid, s_dev devox after its step's prep, on alternating buffer
@@ -340,6 +350,16 @@ def grid_kernel_bytes_per_cloud(n, r, c):
     point order 8N) is not counted: it is an artefact of this design."""
     r3 = r ** 3
     return 4 * c * n + 4 * c * r3 + 4 * r3
+
+
+def fused_grid_kernel_bytes_per_cloud(n, r, c):
+    """Algorithmic HBM bytes of the step's voxel kernel (vox_grid_kernel<3>:
+    spherical_avg_voxelize output + spherical_trilinear_devoxelize of it +
+    descriptor) per cloud: features read 4CN, grid written
+    4C r^3, cnt 4 r^3, devox written 4CN, corner inds + wgts read 64N,
+    descriptor 4C.  Prep's corner -> segment map (32N) and the occupancy
+    metadata are artefacts of this design and not counted."""
+    return grid_kernel_bytes_per_cloud(n, r, c) + 4 * c * n + 64 * n + 4 * c
 
 
 def algorithmic_bytes_per_cloud(n, k, r, c):
