@@ -214,9 +214,11 @@ __global__ __launch_bounds__(kPrepThreads) void vox_prep_kernel(
   PCR_STAMP(2);
   // voxel index, devox corners, sort keys
   unsigned long long kv[kMaxE];
+  bool corner_ok[kMaxE];  // the reference interpolates this point (else outputs stay 0)
 #pragma unroll
   for (int e = 0; e < kMaxE; e++) {
     kv[e] = ~0ull;
+    corner_ok[e] = false;
     const int i = e * nt + tid;
     if (e < E && i < n) {
       int v;
@@ -239,6 +241,7 @@ __global__ __launch_bounds__(kPrepThreads) void vox_prep_kernel(
           int* I = dinds + (size_t)b * 8 * n;
           float* Wt = dwgts + (size_t)b * 8 * n;
           const bool ok = valid && pcr_sph_corners(px[e], py[e], pz[e], v, r, cidx, cw);
+          corner_ok[e] = ok;
 #pragma unroll
           for (int q = 0; q < 8; q++) {
             I[i + (size_t)q * n] = ok ? cidx[q] : ((q == 0 && !valid) ? -1 : 0);
@@ -299,7 +302,9 @@ __global__ __launch_bounds__(kPrepThreads) void vox_prep_kernel(
     for (int e = 0; e < kMaxE; e++) {
       const int i = e * nt + tid;
       if (e < E && i < n) {
-        const bool skip = I[i] == -1;
+        // dropped or not interpolated (spherical_trilinear_devox.cu:41-65
+        // `continue`): every corner -1, so the output is +0 as untouched
+        const bool skip = !corner_ok[e];
 #pragma unroll
         for (int q = 0; q < 8; q++) {
           const int cell = I[i + (size_t)q * n];
@@ -533,29 +538,40 @@ __global__ __launch_bounds__(NT) void vox_grid_kernel(
 #pragma unroll
     for (int g = 0; g < kMaxG; g++) vmax[g] = -__builtin_inff();
     // corner -> segment map from prep (ws.dseg): the segment ids are the
-    // rows of mean_s (one tile: s_begin = 0)
+    // rows of mean_s (one tile: s_begin = 0).  A dropped point has every
+    // corner at -1 and zero weights, so its wsum8 is +0 like the
+    // reference's untouched output.  PB points per thread with all their
+    // corner loads in flight before any gather.
+    (void)I;
     const int* Dg = ws.dseg + (size_t)b * 8 * n;
-    for (int i = tid; i < n; i += NT) {
-      float cw[8];
-      int rk[8];
-      const bool skip = I[i] == -1;
+    constexpr int PB = 4;
+    for (int i0 = tid; i0 < n; i0 += NT * PB) {
+      float cw[PB][8];
+      int rk[PB][8];
 #pragma unroll
-      for (int q = 0; q < 8; q++) {
-        cw[q] = Wt[i + (size_t)q * n];
-        rk[q] = Dg[i + (size_t)q * n];
+      for (int u = 0; u < PB; u++) {
+        const int i = i0 + u * NT;
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+          cw[u][q] = i < n ? Wt[i + (size_t)q * n] : 0.0f;
+          rk[u][q] = i < n ? Dg[i + (size_t)q * n] : -1;
+        }
       }
 #pragma unroll
-      for (int g = 0; g < kMaxG; g++) {
-        if (g < gcount) {
-          float v = 0.0f;
-          if (!skip) {
+      for (int u = 0; u < PB; u++) {
+        const int i = i0 + u * NT;
+        if (i >= n) break;
+#pragma unroll
+        for (int g = 0; g < kMaxG; g++) {
+          if (g < gcount) {
             float fv[8];
 #pragma unroll
-            for (int q = 0; q < 8; q++) fv[q] = rk[q] >= 0 ? mean_s[(size_t)g * n + rk[q]] : 0.0f;
-            v = pcr_wsum8(cw, fv);
+            for (int q = 0; q < 8; q++)
+              fv[q] = rk[u][q] >= 0 ? mean_s[(size_t)g * n + rk[u][q]] : 0.0f;
+            const float v = pcr_wsum8(cw[u], fv);
+            ov[(size_t)g * n + i] = v;
+            vmax[g] = fmaxf(vmax[g], v);
           }
-          ov[(size_t)g * n + i] = v;
-          vmax[g] = fmaxf(vmax[g], v);
         }
       }
     }
