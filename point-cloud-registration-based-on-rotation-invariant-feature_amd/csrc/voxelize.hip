@@ -215,6 +215,7 @@ __global__ __launch_bounds__(kPrepThreads) void vox_prep_kernel(
   // voxel index, devox corners, sort keys
   unsigned long long kv[kMaxE];
   bool corner_ok[kMaxE];  // the reference interpolates this point (else outputs stay 0)
+  int corner_cell[MODE == kSphNormalize ? kMaxE : 1][8];
 #pragma unroll
   for (int e = 0; e < kMaxE; e++) {
     kv[e] = ~0ull;
@@ -242,6 +243,8 @@ __global__ __launch_bounds__(kPrepThreads) void vox_prep_kernel(
           float* Wt = dwgts + (size_t)b * 8 * n;
           const bool ok = valid && pcr_sph_corners(px[e], py[e], pz[e], v, r, cidx, cw);
           corner_ok[e] = ok;
+#pragma unroll
+          for (int q = 0; q < 8; q++) corner_cell[MODE == kSphNormalize ? e : 0][q] = cidx[q];
 #pragma unroll
           for (int q = 0; q < 8; q++) {
             I[i + (size_t)q * n] = ok ? cidx[q] : ((q == 0 && !valid) ? -1 : 0);
@@ -293,10 +296,9 @@ __global__ __launch_bounds__(kPrepThreads) void vox_prep_kernel(
   __syncthreads();
   const int nseg = __float_as_int(s_stat[0]);
   // devox corners -> their voxel's segment (the grid kernel's devox part
-  // gathers the voxel means by segment without a bitmap lookup); this
-  // thread wrote the corners above, so it reads them back itself
+  // gathers the voxel means by segment without a bitmap lookup); the corner
+  // cells are still in this thread's registers
   if (MODE == kSphNormalize && dinds) {
-    const int* I = dinds + (size_t)b * 8 * n;
     int* D = ws.dseg + (size_t)b * 8 * n;
 #pragma unroll
     for (int e = 0; e < kMaxE; e++) {
@@ -307,7 +309,7 @@ __global__ __launch_bounds__(kPrepThreads) void vox_prep_kernel(
         const bool skip = !corner_ok[e];
 #pragma unroll
         for (int q = 0; q < 8; q++) {
-          const int cell = I[i + (size_t)q * n];
+          const int cell = corner_cell[MODE == kSphNormalize ? e : 0][q];
           int sg = -1;
           if (!skip && cell >= 0 && cell < r3) {
             const unsigned word = bm[cell >> 5], bit = 1u << (cell & 31);
@@ -399,7 +401,8 @@ __global__ __launch_bounds__(kPrepThreads) void vox_prep_kernel(
 
 // ------------------------------------------------------------ grid kernel
 // One workgroup per (cell tile, channel group, cloud).
-// PART: 1 = stream the grid (+cnt), 2 = devoxelise + descriptor, 3 = both.
+// PART: 1 = stream the grid (+cnt), 2 = devoxelise + descriptor, 3 = both,
+// 4 = both as separate workgroups of one launch.
 // NT threads: 256 for the streaming parts; the devox-only part runs 1024
 // (one point per thread, so every corner load of a point is in flight at once).
 template <int PART, int NT>
@@ -409,7 +412,12 @@ __global__ __launch_bounds__(NT) void vox_grid_kernel(
     const float* __restrict__ dwgts, float* __restrict__ devox, float* __restrict__ desc) {
   extern __shared__ __align__(16) unsigned char smem_raw[];
   const int tile = blockIdx.x;
-  const int grp = blockIdx.y;
+  // PART 4: the first half of blockIdx.y streams the grid (role 1), the
+  // second half devoxelises the same channel groups (role 2) -- both in one
+  // launch, so the devox work overlaps the HBM-bound streaming
+  const int ngy = PART == 4 ? (int)gridDim.y / 2 : (int)gridDim.y;
+  const int role = PART == 4 ? ((int)blockIdx.y < ngy ? 1 : 2) : PART;
+  const int grp = (int)blockIdx.y % ngy;
   const int b = blockIdx.z;
   const int tid = threadIdx.x;
   const int W = ws.W;
@@ -484,7 +492,7 @@ __global__ __launch_bounds__(NT) void vox_grid_kernel(
   // stream the [gcount, cell0..cell1) slab once; zeros included
   float* ob = out + ((size_t)b * c + c0) * r3;
   int* cb = (cnt_out && grp == 0) ? cnt_out + (size_t)b * r3 : nullptr;
-  if (!(PART & 1)) {
+  if (!(role & 1)) {
   } else if ((r3 & 3) == 0) {
     for (int base = cell0 + tid * 4; base < cell1; base += NT * 4) {
       const int wl = (base >> 5) - wb;
@@ -528,7 +536,7 @@ __global__ __launch_bounds__(NT) void vox_grid_kernel(
   }
 
   PCR_STAMP(11);
-  if (PART & 2) {
+  if (role & 2) {
     // spherical devoxelisation of this grid (spherical_trilinear_devox.cu:127-134)
     // evaluated from the LDS-resident means; requires one tile per cloud.
     const int* I = dinds + (size_t)b * 8 * n;
@@ -860,10 +868,10 @@ static pcr_status run_voxelize(const float* features, const float* coords_f, con
     const int ngrp = pick_groups(c, n, 2, &G);
     const size_t smem = grid_smem_bytes(G, n, nw);
     PCR_REQUIRE(smem <= 150 * 1024, "%s: grid LDS %zu too large", name, smem);
-    allow_big_lds(vox_grid_kernel<3, kGridThreads>, smem);
-    hipLaunchKernelGGL((vox_grid_kernel<3, kGridThreads>), dim3(1, ngrp, b), dim3(kGridThreads),
-                       smem, stream, features, c, n, r3, G, tile, ws, out, cnt, dinds, dwgts,
-                       devox, desc);
+    allow_big_lds(vox_grid_kernel<4, kGridThreads>, smem);
+    hipLaunchKernelGGL((vox_grid_kernel<4, kGridThreads>), dim3(1, 2 * ngrp, b),
+                       dim3(kGridThreads), smem, stream, features, c, n, r3, G, tile, ws, out, cnt,
+                       dinds, dwgts, devox, desc);
   } else if (do_dev) {
     int G = 1;
     const int ngrp = pick_groups(c, n, 4, &G);

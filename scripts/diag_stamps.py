@@ -32,6 +32,7 @@ s = torch.cuda.current_stream().cuda_stream
 for name, fn, reader, nwg in (("vox_prep", lambda: ex.voxel_prep(xyz, s), lib.pcr_diag_read_vox, b),
                               ("vox_grid", lambda: ex.voxel_grid(feat, s), lib.pcr_diag_read_vox, 512),
                               ("vox_devox", lambda: ex.voxel_devox(feat, s), lib.pcr_diag_read_vox, 512),
+                              ("vox_fused", lambda: ex.voxel_grid_devox(feat, s), lib.pcr_diag_read_vox, 1024),
                               ("knn", lambda: ex.neighbor_stage(xyz, nrm, s), lib.pcr_diag_read_knn,
                                b * n // 64)):
     fn()
@@ -44,7 +45,7 @@ for name, fn, reader, nwg in (("vox_prep", lambda: ex.voxel_prep(xyz, s), lib.pc
         ok = (a[:, p] > 0) & (a[:, p - 1] > 0)
         if ok.any():
             print("  phase %d->%d: median %d  max %d cycles" % (p - 1, p, np.median(d[ok]), d[ok].max()))
-    if name in ("vox_grid", "vox_devox"):
+    if name in ("vox_grid", "vox_devox", "vox_fused"):
         t0 = a[:, 8][a[:, 8] > 0]
         t1 = a[:, 12][a[:, 12] > 0]
         print("  kernel span %d cycles; WG durations median %d" % (t1.max() - t0.min(), np.median(t1 - t0)))
