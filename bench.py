@@ -247,7 +247,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic,
-                     "kernel": "vox_grid_kernel<4> (sph-vox dense grid + cnt; sph-devox + "
+                     "kernel": "vox_grid_kernel<3> (sph-vox dense grid + cnt, sph-devox + "
                                "descriptor)",
                      "kernel_avg_ms": round(grid_avg_ms, 5),
                      "kernel_bytes_per_launch": grid_bytes},

@@ -401,8 +401,9 @@ __global__ __launch_bounds__(kPrepThreads) void vox_prep_kernel(
 
 // ------------------------------------------------------------ grid kernel
 // One workgroup per (cell tile, channel group, cloud).
-// PART: 1 = stream the grid (+cnt), 2 = devoxelise + descriptor, 3 = both,
-// 4 = both as separate workgroups of one launch.
+// PART: 1 = stream the grid (+cnt), 2 = devoxelise + descriptor, 3 = both
+// (a variant with the two as separate workgroups of one launch measured
+// slower: 68 vs 60 us).
 // NT threads: 256 for the streaming parts; the devox-only part runs 1024
 // (one point per thread, so every corner load of a point is in flight at once).
 template <int PART, int NT>
@@ -412,12 +413,8 @@ __global__ __launch_bounds__(NT) void vox_grid_kernel(
     const float* __restrict__ dwgts, float* __restrict__ devox, float* __restrict__ desc) {
   extern __shared__ __align__(16) unsigned char smem_raw[];
   const int tile = blockIdx.x;
-  // PART 4: the first half of blockIdx.y streams the grid (role 1), the
-  // second half devoxelises the same channel groups (role 2) -- both in one
-  // launch, so the devox work overlaps the HBM-bound streaming
-  const int ngy = PART == 4 ? (int)gridDim.y / 2 : (int)gridDim.y;
-  const int role = PART == 4 ? ((int)blockIdx.y < ngy ? 1 : 2) : PART;
-  const int grp = (int)blockIdx.y % ngy;
+  const int role = PART;
+  const int grp = blockIdx.y;
   const int b = blockIdx.z;
   const int tid = threadIdx.x;
   const int W = ws.W;
@@ -868,10 +865,10 @@ static pcr_status run_voxelize(const float* features, const float* coords_f, con
     const int ngrp = pick_groups(c, n, 2, &G);
     const size_t smem = grid_smem_bytes(G, n, nw);
     PCR_REQUIRE(smem <= 150 * 1024, "%s: grid LDS %zu too large", name, smem);
-    allow_big_lds(vox_grid_kernel<4, kGridThreads>, smem);
-    hipLaunchKernelGGL((vox_grid_kernel<4, kGridThreads>), dim3(1, 2 * ngrp, b),
-                       dim3(kGridThreads), smem, stream, features, c, n, r3, G, tile, ws, out, cnt,
-                       dinds, dwgts, devox, desc);
+    allow_big_lds(vox_grid_kernel<3, kGridThreads>, smem);
+    hipLaunchKernelGGL((vox_grid_kernel<3, kGridThreads>), dim3(1, ngrp, b), dim3(kGridThreads),
+                       smem, stream, features, c, n, r3, G, tile, ws, out, cnt, dinds, dwgts,
+                       devox, desc);
   } else if (do_dev) {
     int G = 1;
     const int ngrp = pick_groups(c, n, 4, &G);

@@ -17,7 +17,7 @@ import os
 import sys
 from collections import defaultdict
 
-KERNEL = "vox_grid_kernel<4,"
+KERNEL = "vox_grid_kernel<3,"
 
 
 def per_dispatch(d, counter):
