@@ -285,6 +285,26 @@ class SphExtractor:
                 dev_done[slot].record(self.s_dev)
             self._join(cur)
             return self.outputs(slot=(steps - 1) & 1)
+        if mode == "two_sv":
+            # as two_fused, with the Morton sort on the voxel stream ahead of
+            # prep (KNN workspace alternates; two events per step)
+            sn, sv = self.s_nbr.cuda_stream, self.s_vox.cuda_stream
+            sel_done = [None, None]
+            for s in range(steps):
+                slot = s & 1
+                d = None if desc_steps is None else desc_steps[s]
+                if sel_done[slot] is not None:
+                    self.s_vox.wait_event(sel_done[slot])
+                ok = self.knn_sort(xyz, sv, slot)
+                e_sort = torch.cuda.Event()
+                e_sort.record(self.s_vox)
+                self.voxel_stage(xyz, features, sv, d)
+                self.s_nbr.wait_event(e_sort)
+                self.knn_select(xyz, normals, sn, slot, ok)
+                sel_done[slot] = torch.cuda.Event()
+                sel_done[slot].record(self.s_nbr)
+            self._join(cur)
+            return self.outputs()
         if mode == "two_fused":
             # voxel stream: prep, then one kernel for grid + devox + descriptor
             sn, sv = self.s_nbr.cuda_stream, self.s_vox.cuda_stream
