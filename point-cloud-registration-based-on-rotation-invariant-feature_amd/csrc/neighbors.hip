@@ -228,26 +228,39 @@ __global__ __launch_bounds__(256) void global_ppf_kernel(const float* __restrict
 }
 
 // pvcnn_classify.py:258-269 with explicit neighbour indices; out [b,4,u,m]
+// buffer resource over [p, p + bytes): raw buffer loads / stores take a
+// 32-bit byte offset (no 64-bit address arithmetic per access)
+__device__ inline __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes,
+                                           0x00020000);
+}
+__device__ inline float bld(__amdgpu_buffer_rsrc_t r, unsigned i) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)(i * 4u), 0, 0));
+}
+
 __global__ __launch_bounds__(256) void local_ppf_kernel(
     const float* __restrict__ pts, const float* __restrict__ nrm, const float* __restrict__ ctr,
     const float* __restrict__ cnrm, const int* __restrict__ idx, int n, int m, int u, int kmajor,
     int relative, float* __restrict__ out) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  const int q = blockIdx.y;
-  const int b = blockIdx.z;
-  if (j >= m) return;
-  const float* P = pts + (size_t)b * 3 * n;
-  const float* Nn = nrm + (size_t)b * 3 * n;
-  const float* C = ctr + (size_t)b * 3 * m;
-  const float* Cn = cnrm + (size_t)b * 3 * m;
-  const int* I = idx + (size_t)b * m * u;
-  int s = kmajor ? I[(size_t)q * m + j] : I[(size_t)j * u + q];
-  if (s < 0 || s >= n) s = 0;
+  const unsigned j = blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned q = blockIdx.y;
+  const unsigned b = blockIdx.z;
+  if (j >= (unsigned)m) return;
+  const unsigned un = (unsigned)n, um = (unsigned)m, uu = (unsigned)u;
+  const auto P = buf_rsrc(pts + (size_t)b * 3 * un, 12u * un);
+  const auto Nn = buf_rsrc(nrm + (size_t)b * 3 * un, 12u * un);
+  const auto C = buf_rsrc(ctr + (size_t)b * 3 * um, 12u * um);
+  const auto Cn = buf_rsrc(cnrm + (size_t)b * 3 * um, 12u * um);
+  const int* I = idx + (size_t)b * um * uu;
+  const int si = kmajor ? I[q * um + j] : I[j * uu + q];
+  const unsigned s = (si < 0 || si >= n) ? 0u : (unsigned)si;
   float o[4];
-  pcr_local_ppf(C[j], C[j + m], C[j + 2 * m], Cn[j], Cn[j + m], Cn[j + 2 * m], P[s], P[s + n],
-                P[s + 2 * n], Nn[s], Nn[s + n], Nn[s + 2 * n], relative, o);
+  pcr_local_ppf(bld(C, j), bld(C, j + um), bld(C, j + 2 * um), bld(Cn, j), bld(Cn, j + um),
+                bld(Cn, j + 2 * um), bld(P, s), bld(P, s + un), bld(P, s + 2 * un), bld(Nn, s),
+                bld(Nn, s + un), bld(Nn, s + 2 * un), relative, o);
+  float* O = out + (size_t)b * 4 * uu * um;
 #pragma unroll
-  for (int ch = 0; ch < 4; ch++) out[(((size_t)b * 4 + ch) * u + q) * m + j] = o[ch];
+  for (unsigned ch = 0; ch < 4; ch++) O[(ch * uu + q) * um + j] = o[ch];
 }
 
 // ball_query.cu:30-49: points staged through LDS tiles; per-centre early exit
