@@ -406,7 +406,7 @@ __global__ __launch_bounds__(kPrepThreads) void vox_prep_kernel(
 // slower: 68 vs 60 us).
 // NT threads: 256 for the streaming parts; the devox-only part runs 1024
 // (one point per thread, so every corner load of a point is in flight at once).
-template <int PART, int NT>
+template <int PART, int NT, int MG>
 __global__ __launch_bounds__(NT) void vox_grid_kernel(
     const float* __restrict__ feat, int c, int n, int r3, int G, int tile_cells, VoxWs ws,
     float* __restrict__ out, int* __restrict__ cnt_out, const int* __restrict__ dinds,
@@ -469,17 +469,17 @@ __global__ __launch_bounds__(NT) void vox_grid_kernel(
     const int s = s_begin + si;
     const int off = seg_off[s], end = seg_off[s + 1];
     const float inv = pcr_inv_count(end - off);
-    float acc[kMaxG];
+    float acc[MG];
 #pragma unroll
-    for (int g = 0; g < kMaxG; g++) acc[g] = 0.0f;
+    for (int g = 0; g < MG; g++) acc[g] = 0.0f;
     for (int p = off; p < end; p++) {
       const int pt = perm[p];
 #pragma unroll
-      for (int g = 0; g < kMaxG; g++)
+      for (int g = 0; g < MG; g++)
         if (g < gcount) acc[g] = acc[g] + feat_s[(size_t)g * n + pt] * inv;
     }
 #pragma unroll
-    for (int g = 0; g < kMaxG; g++)
+    for (int g = 0; g < MG; g++)
       if (g < gcount) mean_s[(size_t)g * n + si] = acc[g];
     scnt_s[si] = end - off;
   }
@@ -489,7 +489,87 @@ __global__ __launch_bounds__(NT) void vox_grid_kernel(
   // stream the [gcount, cell0..cell1) slab once; zeros included
   float* ob = out + ((size_t)b * c + c0) * r3;
   int* cb = (cnt_out && grp == 0) ? cnt_out + (size_t)b * r3 : nullptr;
+  // fused devox (role 3): each thread's PB points' corner data is loaded
+  // before the streaming loop, and one point is devoxelised every few
+  // streaming iterations, so the VALU / LDS work of the devox hides under the
+  // outstanding grid stores instead of running after them
+  constexpr int PB = 4;
+  const bool interleave = role == 3 && (r3 & 3) == 0 && n <= PB * NT;
+  float dv_w[PB][8];
+  int dv_s[PB][8];
+  float vmax[MG];
+#pragma unroll
+  for (int g = 0; g < MG; g++) vmax[g] = -__builtin_inff();
+  auto devox_point = [&](int u) {
+    const int i = tid + u * NT;
+    if (i >= n) return;
+    float* ov = devox + ((size_t)b * c + c0) * n;
+#pragma unroll
+    for (int g = 0; g < MG; g++) {
+      if (g < gcount) {
+        float fv[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++)
+          fv[q] = dv_s[u][q] >= 0 ? mean_s[(size_t)g * n + dv_s[u][q]] : 0.0f;
+        const float v = pcr_wsum8(dv_w[u], fv);
+        ov[(size_t)g * n + i] = v;
+        vmax[g] = fmaxf(vmax[g], v);
+      }
+    }
+  };
+  if (interleave) {
+    const float* Wt = dwgts + (size_t)b * 8 * n;
+    const int* Dg = ws.dseg + (size_t)b * 8 * n;
+#pragma unroll
+    for (int u = 0; u < PB; u++) {
+      const int i = tid + u * NT;
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        dv_w[u][q] = i < n ? Wt[i + (size_t)q * n] : 0.0f;
+        dv_s[u][q] = i < n ? Dg[i + (size_t)q * n] : -1;
+      }
+    }
+  }
   if (!(role & 1)) {
+  } else if (interleave) {
+    // the streaming iterations in PB chunks, one devox point after each
+    const int iters = (cell1 - cell0 + NT * 4 - 1) / (NT * 4);
+#pragma unroll
+    for (int u = 0; u < PB; u++) {
+      const int it1 = (u + 1) * iters / PB;
+      for (int it = u * iters / PB; it < it1; it++) {
+        const int base = cell0 + tid * 4 + it * NT * 4;
+        if (base >= cell1) continue;
+        const int wl = (base >> 5) - wb;
+        const unsigned word = bm_s[wl];
+        const int pre = pre_s[wl];
+        const int sh = base & 31;
+        int rk[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const unsigned bit = 1u << (sh + j);
+          rk[j] = (word & bit) ? pre + __popc(word & (bit - 1u)) : -1;
+        }
+        for (int g = 0; g < gcount; g++) {
+          const float* ms = mean_s + (size_t)g * n;
+          float4 v;
+          v.x = rk[0] >= 0 ? ms[rk[0]] : 0.0f;
+          v.y = rk[1] >= 0 ? ms[rk[1]] : 0.0f;
+          v.z = rk[2] >= 0 ? ms[rk[2]] : 0.0f;
+          v.w = rk[3] >= 0 ? ms[rk[3]] : 0.0f;
+          *(float4*)(ob + (size_t)g * r3 + base) = v;
+        }
+        if (cb) {
+          int4 cv;
+          cv.x = rk[0] >= 0 ? scnt_s[rk[0]] : 0;
+          cv.y = rk[1] >= 0 ? scnt_s[rk[1]] : 0;
+          cv.z = rk[2] >= 0 ? scnt_s[rk[2]] : 0;
+          cv.w = rk[3] >= 0 ? scnt_s[rk[3]] : 0;
+          *(int4*)(cb + base) = cv;
+        }
+      }
+      devox_point(u);
+    }
   } else if ((r3 & 3) == 0) {
     for (int base = cell0 + tid * 4; base < cell1; base += NT * 4) {
       const int wl = (base >> 5) - wb;
@@ -536,54 +616,48 @@ __global__ __launch_bounds__(NT) void vox_grid_kernel(
   if (role & 2) {
     // spherical devoxelisation of this grid (spherical_trilinear_devox.cu:127-134)
     // evaluated from the LDS-resident means; requires one tile per cloud.
-    const int* I = dinds + (size_t)b * 8 * n;
-    const float* Wt = dwgts + (size_t)b * 8 * n;
-    float* ov = devox + ((size_t)b * c + c0) * n;
-    float vmax[kMaxG];
-#pragma unroll
-    for (int g = 0; g < kMaxG; g++) vmax[g] = -__builtin_inff();
-    // corner -> segment map from prep (ws.dseg): the segment ids are the
+    // Corner -> segment map from prep (ws.dseg): the segment ids are the
     // rows of mean_s (one tile: s_begin = 0).  A dropped point has every
     // corner at -1 and zero weights, so its wsum8 is +0 like the
-    // reference's untouched output.  PB points per thread with all their
-    // corner loads in flight before any gather.
-    (void)I;
-    const int* Dg = ws.dseg + (size_t)b * 8 * n;
-    constexpr int PB = 4;
-    for (int i0 = tid; i0 < n; i0 += NT * PB) {
-      float cw[PB][8];
-      int rk[PB][8];
+    // reference's untouched output.
+    if (!interleave) {
+      const float* Wt = dwgts + (size_t)b * 8 * n;
+      const int* Dg = ws.dseg + (size_t)b * 8 * n;
+      for (int i0 = 0; i0 < n; i0 += NT * PB) {
+        // PB points per thread with all their corner loads in flight
 #pragma unroll
-      for (int u = 0; u < PB; u++) {
-        const int i = i0 + u * NT;
+        for (int u = 0; u < PB; u++) {
+          const int i = i0 + tid + u * NT;
 #pragma unroll
-        for (int q = 0; q < 8; q++) {
-          cw[u][q] = i < n ? Wt[i + (size_t)q * n] : 0.0f;
-          rk[u][q] = i < n ? Dg[i + (size_t)q * n] : -1;
+          for (int q = 0; q < 8; q++) {
+            dv_w[u][q] = i < n ? Wt[i + (size_t)q * n] : 0.0f;
+            dv_s[u][q] = i < n ? Dg[i + (size_t)q * n] : -1;
+          }
         }
-      }
+        float* ov = devox + ((size_t)b * c + c0) * n;
 #pragma unroll
-      for (int u = 0; u < PB; u++) {
-        const int i = i0 + u * NT;
-        if (i >= n) break;
+        for (int u = 0; u < PB; u++) {
+          const int i = i0 + tid + u * NT;
+          if (i >= n) break;
 #pragma unroll
-        for (int g = 0; g < kMaxG; g++) {
-          if (g < gcount) {
-            float fv[8];
+          for (int g = 0; g < MG; g++) {
+            if (g < gcount) {
+              float fv[8];
 #pragma unroll
-            for (int q = 0; q < 8; q++)
-              fv[q] = rk[u][q] >= 0 ? mean_s[(size_t)g * n + rk[u][q]] : 0.0f;
-            const float v = pcr_wsum8(cw[u], fv);
-            ov[(size_t)g * n + i] = v;
-            vmax[g] = fmaxf(vmax[g], v);
+              for (int q = 0; q < 8; q++)
+                fv[q] = dv_s[u][q] >= 0 ? mean_s[(size_t)g * n + dv_s[u][q]] : 0.0f;
+              const float v = pcr_wsum8(dv_w[u], fv);
+              ov[(size_t)g * n + i] = v;
+              vmax[g] = fmaxf(vmax[g], v);
+            }
           }
         }
       }
     }
     if (desc) {
-      __shared__ float red[NT / kWave][kMaxG];
+      __shared__ float red[NT / kWave][MG];
 #pragma unroll
-      for (int g = 0; g < kMaxG; g++) {
+      for (int g = 0; g < MG; g++) {
         float m = wave_max(vmax[g]);
         if ((tid & 63) == 0) red[tid >> 6][g] = m;
       }
@@ -865,8 +939,8 @@ static pcr_status run_voxelize(const float* features, const float* coords_f, con
     const int ngrp = pick_groups(c, n, 2, &G);
     const size_t smem = grid_smem_bytes(G, n, nw);
     PCR_REQUIRE(smem <= 150 * 1024, "%s: grid LDS %zu too large", name, smem);
-    allow_big_lds(vox_grid_kernel<3, kGridThreads>, smem);
-    hipLaunchKernelGGL((vox_grid_kernel<3, kGridThreads>), dim3(1, ngrp, b), dim3(kGridThreads),
+    allow_big_lds(vox_grid_kernel<3, kGridThreads, 2>, smem);
+    hipLaunchKernelGGL((vox_grid_kernel<3, kGridThreads, 2>), dim3(1, ngrp, b), dim3(kGridThreads),
                        smem, stream, features, c, n, r3, G, tile, ws, out, cnt, dinds, dwgts,
                        devox, desc);
   } else if (do_dev) {
@@ -874,8 +948,8 @@ static pcr_status run_voxelize(const float* features, const float* coords_f, con
     const int ngrp = pick_groups(c, n, 4, &G);
     const size_t smem = grid_smem_bytes(G, n, nw);
     PCR_REQUIRE(smem <= 150 * 1024, "%s: grid LDS %zu too large", name, smem);
-    allow_big_lds(vox_grid_kernel<2, kDevoxThreads>, smem);
-    hipLaunchKernelGGL((vox_grid_kernel<2, kDevoxThreads>), dim3(1, ngrp, b),
+    allow_big_lds(vox_grid_kernel<2, kDevoxThreads, 4>, smem);
+    hipLaunchKernelGGL((vox_grid_kernel<2, kDevoxThreads, 4>), dim3(1, ngrp, b),
                        dim3(kDevoxThreads), smem, stream, features, c, n, r3, G, tile, ws, nullptr,
                        nullptr, dinds, dwgts, devox, desc);
   } else if (do_grid && (c > 0 || cnt)) {
@@ -885,8 +959,8 @@ static pcr_status run_voxelize(const float* features, const float* coords_f, con
     const int ngrp = c > 0 ? pick_groups(c, n, 2, &G) : 1;
     const size_t smem = grid_smem_bytes(G, n, nw);
     PCR_REQUIRE(smem <= 150 * 1024, "%s: grid LDS %zu too large", name, smem);
-    allow_big_lds(vox_grid_kernel<1, kGridThreads>, smem);
-    hipLaunchKernelGGL((vox_grid_kernel<1, kGridThreads>), dim3(ntiles, ngrp, b),
+    allow_big_lds(vox_grid_kernel<1, kGridThreads, 2>, smem);
+    hipLaunchKernelGGL((vox_grid_kernel<1, kGridThreads, 2>), dim3(ntiles, ngrp, b),
                        dim3(kGridThreads), smem, stream, features, c, n, r3, G, tile, ws, out, cnt,
                        nullptr, nullptr, nullptr, nullptr);
   }
