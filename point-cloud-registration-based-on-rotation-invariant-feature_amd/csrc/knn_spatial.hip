@@ -636,8 +636,8 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
   float qx, qy, qz;
   int qj;
   if (SS) {
-    qj = qblk * kBlk + lane;  // non-self: queries in their original order
-    if (qj < qs.n && !(qxyz == cxyz && qs.n == cs.n)) {
+    qj = qblk * kBlk + lane;
+    if (qj < qs.n) {
       const float* Q = qxyz + (size_t)b * 3 * qs.n;
       qx = Q[qj];
       qy = Q[qj + qs.n];
@@ -653,11 +653,12 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     qz = qs.z[qb];
     qj = qs.j[qb];
   }
+  const bool qlive = qj >= 0;
   const int m = cs.n;
   const int nblk = cs.nblk;
   const float* boxes = SS ? box_s : cs.box + (size_t)b * nblk * 8;
   const size_t cbase = (size_t)b * cs.npad;
-  const bool self_q = SS && qxyz == cxyz && qs.n == m;
+  const pf2 qx2 = {qx, qx}, qy2 = {qy, qy}, qz2 = {qz, qz};
 
   if (SS) {
     constexpr int NT = NW * 64;
@@ -759,36 +760,6 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
       cand_j[pos] = -1;
     }
     __syncthreads();
-    // points inside a cell by ascending index: the sorted order is then the
-    // same in every workgroup of the cloud, so self queries can be taken in
-    // it (64 Morton-consecutive queries per workgroup)
-    for (int c = threadIdx.x; c < 4096; c += NT) {
-      const int o0 = chist[c], o1 = c + 1 < 4096 ? chist[c + 1] : m;
-      for (int x = o0 + 1; x < o1; x++) {
-        const int vj = cand_j[x];
-        const float vx = cand_s[x], vy = cand_s[kSelCache + x], vz = cand_s[2 * kSelCache + x];
-        int y = x - 1;
-        while (y >= o0 && cand_j[y] > vj) {
-          cand_j[y + 1] = cand_j[y];
-          cand_s[y + 1] = cand_s[y];
-          cand_s[kSelCache + y + 1] = cand_s[kSelCache + y];
-          cand_s[2 * kSelCache + y + 1] = cand_s[2 * kSelCache + y];
-          y--;
-        }
-        cand_j[y + 1] = vj;
-        cand_s[y + 1] = vx;
-        cand_s[kSelCache + y + 1] = vy;
-        cand_s[2 * kSelCache + y + 1] = vz;
-      }
-    }
-    __syncthreads();
-    if (self_q) {
-      const int p = qblk * kBlk + lane;
-      qj = p < m ? cand_j[p] : -1;
-      qx = p < m ? cand_s[p] : __builtin_nanf("");
-      qy = p < m ? cand_s[kSelCache + p] : __builtin_nanf("");
-      qz = p < m ? cand_s[2 * kSelCache + p] : __builtin_nanf("");
-    }
     // block boxes: wave w takes blocks w, w + NW, ...
     for (int blk = wv; blk < nblk; blk += NW) {
       const int pos = blk * kBlk + lane;
@@ -811,9 +782,6 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     }
     __syncthreads();
   }
-
-  const bool qlive = qj >= 0;
-  const pf2 qx2 = {qx, qx}, qy2 = {qy, qy}, qz2 = {qz, qz};
 
   for (int i = threadIdx.x; i < NG * (kNB + 1) * kBlk; i += NW * kBlk) hist_s[i] = 0u;
   if (wv == 0) dest_s[lane] = 0x7F800000u;  // +inf
