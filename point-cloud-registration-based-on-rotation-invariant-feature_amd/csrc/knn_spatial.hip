@@ -603,189 +603,40 @@ __device__ inline unsigned field_sum(unsigned v) {
   return (v & 0xFFFFu) + (v >> 16);
 }
 
-template <int NW, int CB, bool CL, bool PPF, bool SS>
+template <int NW, int CB, bool CL, bool PPF>
 __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     KnnSet qs, KnnSet cs, int k, float* __restrict__ dist, int* __restrict__ idx,
     const float* __restrict__ qxyz, const float* __restrict__ qnrm,
     const float* __restrict__ cxyz, const float* __restrict__ cnrm, int relative,
     float* __restrict__ ppf) {
-  // SS (self-sorting, cached clouds only): no prepared workspace.  The
-  // workgroup Morton-sorts the candidate cloud itself into LDS (the order
-  // inside a cell is arbitrary, which only moves the bound D_q, never the
-  // result) and takes its 64 queries in their original order
-  // (qs.x/y/z/j unused; qs.n = query count).
-  static_assert(!SS || CL, "self-sorting needs the LDS candidate cache");
   constexpr int FPD = 32 / CB;              // wave fields per counter dword
   constexpr int NG = (NW + FPD - 1) / FPD;  // counter dwords per (bin, lane)
   // the histogram is dead once the cut is chosen: the collected keys reuse it
   constexpr int kHistBytes = NG * (kNB + 1) * kBlk * 4;
   constexpr int kBufBytes = (kCap + 1) * kBlk * 8;  // row kCap: sink of masked writes
-  constexpr int kSortBytes = 4096 * 4 + 64;        // SS: cell histogram + scan scratch
-  constexpr int kU0 = kHistBytes > kBufBytes ? kHistBytes : kBufBytes;
-  __shared__ __align__(16) unsigned char sel_u[kU0 > kSortBytes ? kU0 : kSortBytes];
+  __shared__ __align__(16) unsigned char sel_u[kHistBytes > kBufBytes ? kHistBytes : kBufBytes];
   unsigned* hist_s = (unsigned*)sel_u;
   kkey* buf_s = (kkey*)sel_u;
   __shared__ unsigned dest_s[kBlk];
   __shared__ __align__(16) float cand_s[CL ? 3 * kSelCache : 4];  // x | y | z
   __shared__ __align__(16) int cand_j[CL ? kSelCache : 4];
-  __shared__ float box_s[SS ? (kSelCache / kBlk) * 8 : 8];
   const int b = blockIdx.y;
   const int qblk = blockIdx.x;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  float qx, qy, qz;
-  int qj;
-  if (SS) {
-    qj = qblk * kBlk + lane;
-    if (qj < qs.n) {
-      const float* Q = qxyz + (size_t)b * 3 * qs.n;
-      qx = Q[qj];
-      qy = Q[qj + qs.n];
-      qz = Q[qj + 2 * qs.n];
-    } else {
-      qj = -1;
-      qx = qy = qz = __builtin_nanf("");
-    }
-  } else {
-    const size_t qb = (size_t)b * qs.npad + (size_t)qblk * kBlk + lane;
-    qx = qs.x[qb];
-    qy = qs.y[qb];
-    qz = qs.z[qb];
-    qj = qs.j[qb];
-  }
+  const size_t qb = (size_t)b * qs.npad + (size_t)qblk * kBlk + lane;
+  const float qx = qs.x[qb], qy = qs.y[qb], qz = qs.z[qb];
+  const int qj = qs.j[qb];
   const bool qlive = qj >= 0;
   const int m = cs.n;
   const int nblk = cs.nblk;
-  const float* boxes = SS ? box_s : cs.box + (size_t)b * nblk * 8;
+  const float* boxes = cs.box + (size_t)b * nblk * 8;
   const size_t cbase = (size_t)b * cs.npad;
   const pf2 qx2 = {qx, qx}, qy2 = {qy, qy}, qz2 = {qz, qz};
 
-  if (SS) {
-    constexpr int NT = NW * 64;
-    constexpr int E = kSelCache / NT;  // points per thread
-    int* chist = (int*)sel_u;          // [4096] cell counts -> starts
-    int* scan_b = chist + 4096;        // [NW + 1]
-    __shared__ float red_s[6][NW];
-    const float* C = cxyz + (size_t)b * 3 * m;
-    float px[E], py[E], pz[E];
-    float mn[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
-    float mx[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
-#pragma unroll
-    for (int e = 0; e < E; e++) {
-      const int i = e * NT + threadIdx.x;
-      const bool ok = i < m;
-      px[e] = ok ? C[i] : __builtin_nanf("");
-      py[e] = ok ? C[i + m] : __builtin_nanf("");
-      pz[e] = ok ? C[i + 2 * m] : __builtin_nanf("");
-      mn[0] = fminf(mn[0], px[e]);  // fminf / fmaxf ignore NaN
-      mn[1] = fminf(mn[1], py[e]);
-      mn[2] = fminf(mn[2], pz[e]);
-      mx[0] = fmaxf(mx[0], px[e]);
-      mx[1] = fmaxf(mx[1], py[e]);
-      mx[2] = fmaxf(mx[2], pz[e]);
-    }
-    for (int i = threadIdx.x; i < 4096; i += NT) chist[i] = 0;
-#pragma unroll
-    for (int a2 = 0; a2 < 3; a2++) {
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) {
-        mn[a2] = fminf(mn[a2], __shfl_xor(mn[a2], off, kWave));
-        mx[a2] = fmaxf(mx[a2], __shfl_xor(mx[a2], off, kWave));
-      }
-    }
-    if (lane == 0) {
-#pragma unroll
-      for (int a2 = 0; a2 < 3; a2++) {
-        red_s[a2][wv] = mn[a2];
-        red_s[3 + a2][wv] = mx[a2];
-      }
-    }
-    __syncthreads();
-    float lo[3], sc[3];
-#pragma unroll
-    for (int a2 = 0; a2 < 3; a2++) {
-      float l = red_s[a2][0], h = red_s[3 + a2][0];
-      for (int w = 1; w < NW; w++) {
-        l = fminf(l, red_s[a2][w]);
-        h = fmaxf(h, red_s[3 + a2][w]);
-      }
-      lo[a2] = l;
-      const float ext = h - l;
-      sc[a2] = (ext > 0.0f && ext < __builtin_inff()) ? 1023.0f / ext : 0.0f;
-    }
-    // coarse counting sort on the top 12 Morton bits (16^3 cells)
-    int cell[E], slot[E];
-#pragma unroll
-    for (int e = 0; e < E; e++) {
-      const int i = e * NT + threadIdx.x;
-      cell[e] = -1;
-      if (i < m) {
-        const unsigned code = spread10(quant10(px[e], lo[0], sc[0])) |
-                              (spread10(quant10(py[e], lo[1], sc[1])) << 1) |
-                              (spread10(quant10(pz[e], lo[2], sc[2])) << 2);
-        cell[e] = (int)(code >> 18);
-        slot[e] = atomicAdd(&chist[cell[e]], 1);
-      }
-    }
-    __syncthreads();
-    {
-      constexpr int CPT = 4096 / NT;  // cells per thread
-      int h[CPT], sum = 0;
-#pragma unroll
-      for (int q = 0; q < CPT; q++) {
-        h[q] = chist[threadIdx.x * CPT + q];
-        sum += h[q];
-      }
-      const int incl = block_inclusive_scan(sum, scan_b);
-      int run = incl - sum;
-#pragma unroll
-      for (int q = 0; q < CPT; q++) {
-        chist[threadIdx.x * CPT + q] = run;
-        run += h[q];
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int e = 0; e < E; e++) {
-      if (cell[e] >= 0) {
-        const int pos = chist[cell[e]] + slot[e];
-        cand_s[pos] = px[e];
-        cand_s[kSelCache + pos] = py[e];
-        cand_s[2 * kSelCache + pos] = pz[e];
-        cand_j[pos] = e * NT + threadIdx.x;
-      }
-    }
-    for (int pos = m + threadIdx.x; pos < nblk * kBlk; pos += NT) {
-      cand_s[pos] = cand_s[kSelCache + pos] = cand_s[2 * kSelCache + pos] = __builtin_nanf("");
-      cand_j[pos] = -1;
-    }
-    __syncthreads();
-    // block boxes: wave w takes blocks w, w + NW, ...
-    for (int blk = wv; blk < nblk; blk += NW) {
-      const int pos = blk * kBlk + lane;
-      float v[3] = {cand_s[pos], cand_s[kSelCache + pos], cand_s[2 * kSelCache + pos]};
-      float bmn[3], bmx[3];
-#pragma unroll
-      for (int a2 = 0; a2 < 3; a2++) {
-        const bool real = pos < m && v[a2] == v[a2];
-        bmn[a2] = real ? v[a2] : __builtin_inff();
-        bmx[a2] = real ? v[a2] : -__builtin_inff();
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {
-          bmn[a2] = fminf(bmn[a2], __shfl_xor(bmn[a2], off, kWave));
-          bmx[a2] = fmaxf(bmx[a2], __shfl_xor(bmx[a2], off, kWave));
-        }
-      }
-      const float bv = lane == 0 ? bmn[0] : lane == 1 ? bmn[1] : lane == 2 ? bmn[2]
-                     : lane == 3 ? bmx[0] : lane == 4 ? bmx[1] : bmx[2];
-      if (lane < 6) box_s[blk * 8 + lane] = bv;
-    }
-    __syncthreads();
-  }
-
   for (int i = threadIdx.x; i < NG * (kNB + 1) * kBlk; i += NW * kBlk) hist_s[i] = 0u;
   if (wv == 0) dest_s[lane] = 0x7F800000u;  // +inf
-  if (CL && !SS) {
+  if (CL) {
     const int np = cs.npad;
     for (int i = threadIdx.x; i < np; i += NW * kBlk) {
       cand_s[i] = cs.x[cbase + i];
@@ -1067,10 +918,10 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
   for (int s2 = 0; s2 < k; s2++) buf_s[s2 * kBlk + lane] = undef;
   kkey kth = undef;
   for (int blk = 0; blk < nblk; blk++) {
-    const float* bx = CL ? cand_s + blk * kBlk : cs.x + cbase + (size_t)blk * kBlk;
-    const float* by = CL ? cand_s + kSelCache + blk * kBlk : cs.y + cbase + (size_t)blk * kBlk;
-    const float* bz = CL ? cand_s + 2 * kSelCache + blk * kBlk : cs.z + cbase + (size_t)blk * kBlk;
-    const int* bj = CL ? cand_j + blk * kBlk : cs.j + cbase + (size_t)blk * kBlk;
+    const float* bx = cs.x + cbase + (size_t)blk * kBlk;
+    const float* by = cs.y + cbase + (size_t)blk * kBlk;
+    const float* bz = cs.z + cbase + (size_t)blk * kBlk;
+    const int* bj = cs.j + cbase + (size_t)blk * kBlk;
     for (int t = 0; t < kBlk; t++) {
       const kkey x = make_key(cand_dist(qx, qy, qz, bx[t], by[t], bz[t]), bj[t]);
       if (x < kth) {
@@ -1120,33 +971,14 @@ static void launch_select(const KnnSet& qs, const KnnSet& cs, int b, int k, floa
   const int per_wave = ceil_div(cs.nblk, NW) * kBlk;
   const dim3 grid(qs.nblk, b), blk(NW * 64);
   if (per_wave <= 255 && cs.npad <= kSelCache)
-    hipLaunchKernelGGL((knn_select_kernel<NW, 8, true, PPF, false>), grid, blk, 0, st, qs, cs, k,
-                       dist, idx, qxyz, qnrm, cxyz, cnrm, relative, ppf);
+    hipLaunchKernelGGL((knn_select_kernel<NW, 8, true, PPF>), grid, blk, 0, st, qs, cs, k, dist,
+                       idx, qxyz, qnrm, cxyz, cnrm, relative, ppf);
   else if (per_wave <= 255)
-    hipLaunchKernelGGL((knn_select_kernel<NW, 8, false, PPF, false>), grid, blk, 0, st, qs, cs, k,
-                       dist, idx, qxyz, qnrm, cxyz, cnrm, relative, ppf);
+    hipLaunchKernelGGL((knn_select_kernel<NW, 8, false, PPF>), grid, blk, 0, st, qs, cs, k, dist,
+                       idx, qxyz, qnrm, cxyz, cnrm, relative, ppf);
   else
-    hipLaunchKernelGGL((knn_select_kernel<NW, 16, false, PPF, false>), grid, blk, 0, st, qs, cs,
-                       k, dist, idx, qxyz, qnrm, cxyz, cnrm, relative, ppf);
-}
-
-// Self-sorting selection (no workspace, no sort launch): candidate clouds
-// of <= kSelCache points, k <= kSelMaxK.  Queries in their original order.
-template <bool PPF>
-static void launch_select_ss(const float* qxyz, int n, const float* cxyz, int m, int b, int k,
-                             float* dist, int* idx, const float* qnrm, const float* cnrm,
-                             int relative, float* ppf, hipStream_t st) {
-  constexpr int NW = 8;
-  KnnSet qs{}, cs{};
-  qs.n = n;
-  qs.nblk = ceil_div(n, kBlk);
-  qs.npad = qs.nblk * kBlk;
-  cs.n = m;
-  cs.nblk = ceil_div(m, kBlk);
-  cs.npad = cs.nblk * kBlk;
-  hipLaunchKernelGGL((knn_select_kernel<NW, 8, true, PPF, true>), dim3(qs.nblk, b),
-                     dim3(NW * 64), 0, st, qs, cs, k, dist, idx, qxyz, qnrm, cxyz, cnrm, relative,
-                     ppf);
+    hipLaunchKernelGGL((knn_select_kernel<NW, 16, false, PPF>), grid, blk, 0, st, qs, cs, k, dist,
+                       idx, qxyz, qnrm, cxyz, cnrm, relative, ppf);
 }
 
 size_t knn_ws_size(int b, int n, int m) {
@@ -1210,19 +1042,6 @@ pcr_status knn_spatial(const float* xyz1, const float* xyz2, int b, int n, int m
   if (ws == nullptr || n > kKnnMaxSortN || m > kKnnMaxSortN || n < 1 || m < 1 || k > 128)
     return PCR_ERR_UNSUPPORTED;
   if (ws_bytes < knn_ws_size(b, n, m)) return PCR_ERR_UNSUPPORTED;
-  // small clouds, k <= 32: the selection sorts its candidates itself
-  if (k <= kSelMaxK && n <= kSelCache && m <= kSelCache) {
-    if (!(stages & 2)) return PCR_OK;
-    if (ppf1)
-      launch_select_ss<true>(xyz1, n, xyz2, m, b, k, dist1, idx1, nrm1, nrm2, relative, ppf1, st);
-    else
-      launch_select_ss<false>(xyz1, n, xyz2, m, b, k, dist1, idx1, nullptr, nullptr, 0, nullptr,
-                              st);
-    if (idx2)
-      launch_select_ss<false>(xyz2, m, xyz1, n, b, k, dist2, idx2, nullptr, nullptr, 0, nullptr,
-                              st);
-    return PCR_OK;
-  }
   KnnSet s1, s2;
   size_t off = knn_set_layout(b, n, &s1, (char*)ws, 0);
   knn_set_layout(b, m, &s2, (char*)ws, off);
