@@ -160,15 +160,16 @@ def main():
             src = ex.desc
         if world > 1:
             # descriptor all-gather of the S batches (registration matching),
-            # overlapped with the next launch on a side stream; double-buffered
+            # overlapped with the next launch on a side stream; double-buffered:
+            # the gather that last read this slot is waited for before the copy
             slot = i & 1
+            if len(pending) == 2:
+                pending.pop(0).wait()
             desc_in[slot].copy_(src)
             comm.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(comm):
                 pending.append(dist.all_gather_into_tensor(desc_out[slot], desc_in[slot],
                                                            async_op=True))
-            if len(pending) > 2:
-                pending.pop(0).wait()
 
     for i in range(args.warmup // S):
         launch(i)
