@@ -21,15 +21,24 @@ nrm = (nrm / nrm.norm(dim=1, keepdim=True)).contiguous()
 feat = (torch.rand((b, c, n), generator=g, device=dev) * 2 - 1).contiguous()
 ex = SphExtractor(b, n, c, k, r, device=dev)
 modes = sys.argv[1:] or ["three", "two", "four", "sortvox"]
+print("stream priority range", torch.cuda.Stream.priority_range(), flush=True)
+plain = (ex.s_nbr, ex.s_vox)
+prio = {"hi_knn": (torch.cuda.Stream(device=dev, priority=-1), plain[1]),
+        "hi_vox": (plain[0], torch.cuda.Stream(device=dev, priority=-1))}
 res = {m: [] for m in modes}
 for rnd in range(3):
     for m in modes:
+        mm = m
+        ex.s_nbr, ex.s_vox = plain
+        if m in prio:
+            ex.s_nbr, ex.s_vox = prio[m]
+            mm = "two_fused"
         for _ in range(2):
-            ex.run_pipelined(xyz, nrm, feat, 10, mode=m)
+            ex.run_pipelined(xyz, nrm, feat, 10, mode=mm)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(20):
-            ex.run_pipelined(xyz, nrm, feat, 10, mode=m)
+            ex.run_pipelined(xyz, nrm, feat, 10, mode=mm)
         torch.cuda.synchronize()
         res[m].append(b * 200 / (time.perf_counter() - t0))
 for m, v in res.items():
