@@ -822,8 +822,16 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
         const int j4[4] = {jj.x, jj.y, jj.z, jj.w};
 #pragma unroll
         for (int h = 0; h < 4; h++) {
+#if defined(KNN_EXP) && KNN_EXP == 9
           buf_s[(take[h] ? slot : kCap) * kBlk + lane] = make_key(d[h], j4[h]);
           slot += take[h] ? 1 : 0;
+#else
+          // exec-masked: only the taking lanes store (few lanes of a wave)
+          if (take[h]) {
+            buf_s[slot * kBlk + lane] = make_key(d[h], j4[h]);
+            slot++;
+          }
+#endif
         }
       }
     });
