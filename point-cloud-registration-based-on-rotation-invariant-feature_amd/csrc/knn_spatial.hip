@@ -21,7 +21,10 @@
 
 namespace pcr {
 
-constexpr int kKnnMaxSortN = 4096;
+constexpr int kKnnMaxSortN = 4096;        // single-workgroup LDS sort up to here
+constexpr int kKnnMaxN = 1 << 22;         // global counting sort beyond
+constexpr int kBigCellBits = 15;          // top Morton bits of the global sort (32^3 cells)
+constexpr int kBigCells = 1 << kBigCellBits;
 constexpr int kBlk = 64;
 
 struct KnnSet {
@@ -30,6 +33,11 @@ struct KnnSet {
   float* z;
   int* j;     // [b][npad] original index (-1 padding)
   float* box; // [b][nblk][8] min xyz, max xyz, -, -
+  // clouds of more than kKnnMaxSortN points (global counting sort):
+  int* cell;     // [b][kBigCells] counts, then starts
+  int* pcell;    // [b][n] cell of each point
+  int* pslot;    // [b][n] arrival slot inside the cell
+  float* frame;  // [b][8] lo xyz, scale xyz
   int n, npad, nblk;
 };
 
@@ -48,7 +56,16 @@ static size_t knn_set_layout(int b, int n, KnnSet* s, char* base, size_t off) {
   float* z = (float*)take((size_t)b * npad * 4);
   int* j = (int*)take((size_t)b * npad * 4);
   float* box = (float*)take((size_t)b * nblk * 8 * 4);
+  const bool big = n > kKnnMaxSortN;
+  int* cell = big ? (int*)take((size_t)b * kBigCells * 4) : nullptr;
+  int* pcell = big ? (int*)take((size_t)b * n * 4) : nullptr;
+  int* pslot = big ? (int*)take((size_t)b * n * 4) : nullptr;
+  float* frame = big ? (float*)take((size_t)b * 8 * 4) : nullptr;
   if (s) {
+    s->cell = cell;
+    s->pcell = pcell;
+    s->pslot = pslot;
+    s->frame = frame;
     s->x = x;
     s->y = y;
     s->z = z;
@@ -208,6 +225,129 @@ __global__ __launch_bounds__(kSortBlock) void knn_sort_kernel(const float* __res
       s.box[((size_t)b * s.nblk + blk) * 8 + lane] = v;
     }
   }
+}
+
+// ---- clouds of more than kKnnMaxSortN points: the same coarse Morton
+// order through a global counting sort (frame, cell counts, scan, scatter,
+// block boxes); order inside a cell arbitrary, as above.
+__global__ __launch_bounds__(kSortBlock) void knn_big_frame_kernel(const float* __restrict__ pts,
+                                                                   int n, KnnSet s) {
+  __shared__ float red[6][kSortBlock / kWave];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const float* P = pts + (size_t)b * 3 * n;
+  float mn[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
+  float mx[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
+  for (int i = tid; i < n; i += kSortBlock) {
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+      const float v = P[i + (size_t)a * n];
+      mn[a] = fminf(mn[a], v);
+      mx[a] = fmaxf(mx[a], v);
+    }
+  }
+  int* cnt = s.cell + (size_t)b * kBigCells;
+  for (int c = tid; c < kBigCells; c += kSortBlock) cnt[c] = 0;
+#pragma unroll
+  for (int a = 0; a < 3; a++) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      mn[a] = fminf(mn[a], __shfl_xor(mn[a], off, kWave));
+      mx[a] = fmaxf(mx[a], __shfl_xor(mx[a], off, kWave));
+    }
+  }
+  if ((tid & 63) == 0) {
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+      red[a][tid >> 6] = mn[a];
+      red[3 + a][tid >> 6] = mx[a];
+    }
+  }
+  __syncthreads();
+  if (tid < 3) {
+    float lo = red[tid][0], hi = red[3 + tid][0];
+    for (int w = 1; w < kSortBlock / kWave; w++) {
+      lo = fminf(lo, red[tid][w]);
+      hi = fmaxf(hi, red[3 + tid][w]);
+    }
+    const float ext = hi - lo;
+    s.frame[(size_t)b * 8 + tid] = lo;
+    s.frame[(size_t)b * 8 + 3 + tid] = (ext > 0.0f && ext < __builtin_inff()) ? 1023.0f / ext : 0.0f;
+  }
+}
+
+__global__ __launch_bounds__(256) void knn_big_count_kernel(const float* __restrict__ pts, int n,
+                                                            KnnSet s) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (i >= n) return;
+  const float* P = pts + (size_t)b * 3 * n;
+  const float* f = s.frame + (size_t)b * 8;
+  const unsigned code = spread10(quant10(P[i], f[0], f[3])) |
+                        (spread10(quant10(P[i + n], f[1], f[4])) << 1) |
+                        (spread10(quant10(P[i + 2 * (size_t)n], f[2], f[5])) << 2);
+  const int c = (int)(code >> (30 - kBigCellBits));
+  s.pcell[(size_t)b * n + i] = c;
+  s.pslot[(size_t)b * n + i] = atomicAdd(&s.cell[(size_t)b * kBigCells + c], 1);
+}
+
+__global__ __launch_bounds__(kSortBlock) void knn_big_scan_kernel(KnnSet s) {
+  __shared__ int scan_b[kSortBlock / kWave + 1];
+  constexpr int CPT = kBigCells / kSortBlock;
+  int* cnt = s.cell + (size_t)blockIdx.x * kBigCells;
+  const int c0 = threadIdx.x * CPT;
+  int sum = 0;
+  for (int q = 0; q < CPT; q++) sum += cnt[c0 + q];
+  const int incl = block_inclusive_scan(sum, scan_b);
+  int run = incl - sum;
+  for (int q = 0; q < CPT; q++) {
+    const int v = cnt[c0 + q];
+    cnt[c0 + q] = run;
+    run += v;
+  }
+}
+
+__global__ __launch_bounds__(256) void knn_big_scatter_kernel(const float* __restrict__ pts, int n,
+                                                              KnnSet s) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  const size_t base = (size_t)b * s.npad;
+  if (i < n) {
+    const float* P = pts + (size_t)b * 3 * n;
+    const size_t o = base + s.cell[(size_t)b * kBigCells + s.pcell[(size_t)b * n + i]] +
+                     s.pslot[(size_t)b * n + i];
+    s.x[o] = P[i];
+    s.y[o] = P[i + n];
+    s.z[o] = P[i + 2 * (size_t)n];
+    s.j[o] = i;
+  } else if (i < s.npad) {
+    s.x[base + i] = s.y[base + i] = s.z[base + i] = __builtin_nanf("");
+    s.j[base + i] = -1;
+  }
+}
+
+// one wave per 64-point block
+__global__ __launch_bounds__(256) void knn_big_boxes_kernel(KnnSet s) {
+  const int blk = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int b = blockIdx.y;
+  const int lane = threadIdx.x & 63;
+  if (blk >= s.nblk) return;
+  const size_t p = (size_t)b * s.npad + (size_t)blk * kBlk + lane;
+  const float v[3] = {s.x[p], s.y[p], s.z[p]};
+  float bmn[3], bmx[3];
+#pragma unroll
+  for (int a = 0; a < 3; a++) {
+    const bool real = s.j[p] >= 0 && v[a] == v[a];
+    bmn[a] = real ? v[a] : __builtin_inff();
+    bmx[a] = real ? v[a] : -__builtin_inff();
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      bmn[a] = fminf(bmn[a], __shfl_xor(bmn[a], off, kWave));
+      bmx[a] = fmaxf(bmx[a], __shfl_xor(bmx[a], off, kWave));
+    }
+  }
+  const float bv = lane == 0 ? bmn[0] : lane == 1 ? bmn[1] : lane == 2 ? bmn[2]
+                 : lane == 3 ? bmx[0] : lane == 4 ? bmx[1] : lane == 5 ? bmx[2] : 0.0f;
+  if (lane < 8) s.box[((size_t)b * s.nblk + blk) * 8 + lane] = bv;
 }
 
 // Top-k in registers as packed keys (float bits of the squared distance << 32
@@ -1001,6 +1141,16 @@ static int next_pow2i(int v) {
 }
 
 static void launch_sort(const float* pts, int b, int n, const KnnSet& s, hipStream_t st) {
+  if (n > kKnnMaxSortN) {
+    hipLaunchKernelGGL(knn_big_frame_kernel, dim3(b), dim3(kSortBlock), 0, st, pts, n, s);
+    hipLaunchKernelGGL(knn_big_count_kernel, dim3(ceil_div(n, 256), b), dim3(256), 0, st, pts, n,
+                       s);
+    hipLaunchKernelGGL(knn_big_scan_kernel, dim3(b), dim3(kSortBlock), 0, st, s);
+    hipLaunchKernelGGL(knn_big_scatter_kernel, dim3(ceil_div(s.npad, 256), b), dim3(256), 0, st,
+                       pts, n, s);
+    hipLaunchKernelGGL(knn_big_boxes_kernel, dim3(ceil_div(s.nblk, 4), b), dim3(256), 0, st, s);
+    return;
+  }
   const int npad_sort = next_pow2i(n < kSortBlock ? kSortBlock : n);
   const size_t smem = 4096 * 4 + (size_t)n * 4;
   allow_big_lds(knn_sort_kernel, smem);
@@ -1047,7 +1197,7 @@ pcr_status knn_spatial(const float* xyz1, const float* xyz2, int b, int n, int m
                        float* dist1, int* idx1, float* dist2, int* idx2, const float* nrm1,
                        const float* nrm2, int relative, float* ppf1, void* ws, size_t ws_bytes,
                        bool self, hipStream_t st, int stages) {
-  if (ws == nullptr || n > kKnnMaxSortN || m > kKnnMaxSortN || n < 1 || m < 1 || k > 128)
+  if (ws == nullptr || n > kKnnMaxN || m > kKnnMaxN || n < 1 || m < 1 || k > 128)
     return PCR_ERR_UNSUPPORTED;
   if (ws_bytes < knn_ws_size(b, n, m)) return PCR_ERR_UNSUPPORTED;
   KnnSet s1, s2;

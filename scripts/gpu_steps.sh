@@ -4,7 +4,7 @@
 # signal or timeout (anything else non-zero) stops the script: nothing more
 # touches the GPU after a fault.
 #   usage: scripts/gpu_steps.sh <step> [<step> ...]
-#   steps: smoke tests bench prof pmc
+#   steps: smoke tests tests_all large c5 bench modes prof pmc
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
@@ -36,6 +36,8 @@ for step in "$@"; do
     pmc)  run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --kernel-iters 5 --no-cpu-baseline --mode eager
           run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --kernel-iters 5 --no-cpu-baseline --mode eager
           run pmc_json 60 python3 scripts/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc_traffic.json 32 1024 32 32 64 ;;
+    large) run pytest_large 600 python -m pytest tests/test_gpu_large.py -q -m gpu -p no:cacheprovider ;;
+    c5) run c5_time 300 python scripts/c5_time.py ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

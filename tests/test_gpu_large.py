@@ -83,6 +83,30 @@ def test_knn_large_k64(dev):
     assert np.array_equal(N(ppf), ep, equal_nan=True)
 
 
+@pytest.mark.parametrize("n,k", [(4097, 32), (6000, 16), (9000, 64)])
+def test_knn_large_sorted_path(dev, n, k):
+    """Clouds past the single-workgroup sort: global counting sort, then the
+    selection (k <= 32) or block kernels, bit-exact."""
+    from pcr_amd import ops
+    xyz, nrm, _ = gaussian_clouds(2, n, seed=n + k)
+    xyz[1, :, 50:90] = xyz[1, :, 50:51]          # duplicates
+    xyz[0, :, 7] = np.nan                        # a NaN point
+    idx, ppf, dist = ops.knn_local_ppf(T(xyz, dev), T(nrm, dev), k, want_dist=True)
+    ed, ei = oracle.knn_dir(xyz, xyz, k)
+    assert np.array_equal(N(idx), ei)
+    assert np.array_equal(N(dist), ed)
+
+
+def test_knn_large_two_sets(dev):
+    from pcr_amd import ops
+    rng = np.random.default_rng(12)
+    x1 = rng.standard_normal((1, 3, 7000)).astype(np.float32)
+    x2 = (rng.standard_normal((1, 3, 5000)) * 0.5 + 0.3).astype(np.float32)
+    got = ops.knn_forward_cuda(T(x1, dev), T(x2, dev), 32)
+    for a, b in zip(got, oracle.knn_forward(x1, x2, 32)):
+        assert np.array_equal(N(a), b)
+
+
 def test_c5_cloud_properties(dev):
     """One c5-sized cloud (65,536 points, k = 64, r = 64, C = 64):
     size-independent properties of the whole path."""
