@@ -701,6 +701,13 @@ constexpr int kSelMaxK = 32;
 
 typedef float pf2 __attribute__((ext_vector_type(2)));
 
+// clamp to [lo, hi] in one instruction (the compiler emits min + max)
+__device__ inline int med3_i32(int x, int lo, int hi) {
+  int r;
+  asm volatile("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(lo), "v"(hi));
+  return r;
+}
+
 // Upper bound of the FMA-chain squared distance from q to any point of box.
 __device__ inline float box_ub(float qx, float qy, float qz, const float* bx) {
   const float gx = fmaxf(fabsf(qx - bx[0]), fabsf(qx - bx[3]));
@@ -889,11 +896,11 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     // counter of bin e (clamped to [ebase, ebase + kNB]; the last = not
     // counted, also NaN) at hwb + e * kBlk
     unsigned* hwb = hw - ebase * kBlk;
+    const int etop1 = ebase + kNB;
     visit(ftop, [&](int, const float (&d)[4]) {
 #pragma unroll
       for (int h = 0; h < 4; h++) {
-        int e = (int)(__float_as_uint(d[h]) >> 21);
-        e = max(ebase, min(e, ebase + kNB));
+        const int e = med3_i32((int)(__float_as_uint(d[h]) >> 21), ebase, etop1);
 #if defined(KNN_EXP) && KNN_EXP == 7
         xacc += (unsigned)e << (h * 5);
 #else
@@ -975,17 +982,22 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
         }
       }
     });
-    __syncthreads();
-    PCR_STAMP(3);
-
-    // 5. rank
-    constexpr int kE = kCap / NW;  // collected keys ranked per wave
-    kkey key[kE];
-    int rank[kE];
+    // rows [total, tmax) of every lane read as padding in the rank sweep
     int tmax = total;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) tmax = max(tmax, __shfl_xor(tmax, off, kWave));
     tmax = __builtin_amdgcn_readfirstlane(tmax);
+    for (int i = total + wv; i < tmax; i += NW) buf_s[i * kBlk + lane] = PCR_KEY_PAD;
+    __syncthreads();
+    PCR_STAMP(3);
+
+    // 5. rank: wave wv holds keys wv, wv + NW, ... (ne of them, wave-uniform)
+    //    and counts, for each, the keys below it in one sweep of all tmax
+    //    rows; the sweep is compiled for a few key counts so that no compare
+    //    is wasted on empty key slots and none needs a guard
+    constexpr int kE = kCap / NW;  // collected keys ranked per wave (max)
+    kkey key[kE];
+    int rank[kE];
     const int ne = (tmax - wv + NW - 1) / NW;  // keys this wave holds: wv + e * NW < tmax
 #pragma unroll
     for (int e = 0; e < kE; e++) {
@@ -993,12 +1005,25 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
       key[e] = i < total ? buf_s[i * kBlk + lane] : PCR_KEY_PAD;
       rank[e] = 0;
     }
-    for (int j2 = 0; j2 < tmax; j2++) {
-      const kkey o = j2 < total ? buf_s[j2 * kBlk + lane] : PCR_KEY_PAD;
+    auto sweep = [&](auto ne_c) {
+      constexpr int NE = decltype(ne_c)::value;
+#pragma unroll 2
+      for (int j2 = 0; j2 < tmax; j2++) {
+        const kkey o = buf_s[j2 * kBlk + lane];
 #pragma unroll
-      for (int e = 0; e < kE; e++)
-        if (e < ne) rank[e] += o < key[e] ? 1 : 0;
-    }
+        for (int e = 0; e < NE; e++) rank[e] += o < key[e] ? 1 : 0;
+      }
+    };
+    if (ne <= 3)
+      sweep(std::integral_constant<int, 3>());
+    else if (ne <= 5)
+      sweep(std::integral_constant<int, 5>());
+    else if (ne <= 7)
+      sweep(std::integral_constant<int, 7>());
+    else if (ne <= 9)
+      sweep(std::integral_constant<int, 9>());
+    else
+      sweep(std::integral_constant<int, kE>());
     PCR_STAMP(4);
     __syncthreads();  // all ranking reads of buf_s are done
 #pragma unroll

@@ -360,30 +360,29 @@ __global__ __launch_bounds__(kPrepThreads) void vox_prep_kernel(
       s_stat[1] = __int_as_float(incl);  // number of valid points
     }
   }
-  // 5. place the points, then restore ascending point order inside each
-  //    voxel (the order the means are accumulated in) with a per-voxel
-  //    insertion sort; a cloud with a crowded voxel takes the bitonic path
+  // 5. place the points in arrival order, then every point finds its rank
+  //    among its voxel's points (ascending point order, the order the means
+  //    are accumulated in) by one sweep of that voxel's slots -- independent
+  //    LDS reads, no serial per-voxel pass.  A cloud with a crowded voxel
+  //    takes the bitonic path.
   const int crowded = __syncthreads_or(big > 32);
   if (!crowded) {
 #pragma unroll
     for (int e = 0; e < kMaxE; e++)
       if (seg_of[e] >= 0) perm_l[cnt_l[seg_of[e]] + slot_of[e]] = (int)(unsigned)(kv[e] & 0xFFFFFFFFull);
     __syncthreads();
-    for (int q = tid; q < nseg; q += nt) {
-      const int o0 = cnt_l[q], o1 = (q + 1 < nseg) ? cnt_l[q + 1] : __float_as_int(s_stat[1]);
-      for (int x = o0 + 1; x < o1; x++) {
-        const int val = perm_l[x];
-        int y = x - 1;
-        while (y >= o0 && perm_l[y] > val) {
-          perm_l[y + 1] = perm_l[y];
-          y--;
-        }
-        perm_l[y + 1] = val;
+    const int nvalid = __float_as_int(s_stat[1]);
+#pragma unroll
+    for (int e = 0; e < kMaxE; e++) {
+      const int sg = seg_of[e];
+      if (sg >= 0) {
+        const int id = (int)(unsigned)(kv[e] & 0xFFFFFFFFull);
+        const int o0 = cnt_l[sg], o1 = (sg + 1 < nseg) ? cnt_l[sg + 1] : nvalid;
+        int rank = 0;
+        for (int x = o0; x < o1; x++) rank += perm_l[x] < id ? 1 : 0;
+        perm[o0 + rank] = id;
       }
     }
-    __syncthreads();
-    const int nvalid = __float_as_int(s_stat[1]);
-    for (int p = tid; p < nvalid; p += nt) perm[p] = perm_l[p];
   } else {
     // unique 64-bit keys (the low word is the point id): sorting them is a
     // stable sort by voxel
