@@ -78,8 +78,29 @@ static __device__ unsigned long long pcr_diag_stamps[1024][16];  // one copy per
   } while (0)
 #endif
 
+// Issue priority of the latency-bound per-cloud kernels (prep, Morton sort):
+// they share CUs with the other stream's throughput kernels, whose waves
+// would otherwise take most issue slots and stretch them several-fold.
+__device__ inline void latency_kernel_priority() {
+#if !(defined(KNN_EXP) && KNN_EXP == 12)
+  __builtin_amdgcn_s_setprio(3);
+#endif
+}
+
+// Workgroup barrier that orders LDS only.  __syncthreads() also waits for the
+// thread's outstanding global stores (vmcnt(0)) before the barrier, so a
+// barrier after a burst of global writes stalls on their completion; this one
+// does not.  Use it only where threads exchange data through LDS, never
+// through global memory.
+__device__ inline void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // Inclusive block-wide scan of one int per thread (blockDim.x threads,
-// multiple of 64, <= 1024).  `smem` needs blockDim.x/64 + 1 ints.
+// multiple of 64, <= 1024).  `smem` needs blockDim.x/64 + 1 ints.  Its
+// barriers order LDS only (lds_barrier).
 __device__ inline int block_inclusive_scan(int v, int* smem) {
   const int lane = threadIdx.x & (kWave - 1);
   const int wid = threadIdx.x >> 6;
@@ -90,7 +111,7 @@ __device__ inline int block_inclusive_scan(int v, int* smem) {
     if (lane >= off) v += t;
   }
   if (lane == kWave - 1) smem[wid] = v;
-  __syncthreads();
+  lds_barrier();
   if (wid == 0) {
     int w = (lane < nw) ? smem[lane] : 0;
 #pragma unroll
@@ -100,9 +121,9 @@ __device__ inline int block_inclusive_scan(int v, int* smem) {
     }
     if (lane < nw) smem[lane] = w;
   }
-  __syncthreads();
+  lds_barrier();
   int base = (wid > 0) ? smem[wid - 1] : 0;
-  __syncthreads();
+  lds_barrier();
   return v + base;
 }
 
@@ -128,21 +149,23 @@ __device__ inline unsigned long long shfl_xor_u64(unsigned long long v, int m) {
   return ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
 }
 
-// Ascending bitonic sort of E*1024 keys, element (e, tid) at index e*1024+tid.
+// Ascending bitonic sort of E*NT keys (NT threads), element (e, tid) at
+// index e*NT+tid.
+template <int NT>
 __device__ inline void block_bitonic(unsigned long long (&v)[kMaxE], int E,
                                      unsigned long long* lds) {
   const int tid = threadIdx.x;
-  const int npad = E * kSortBlock;
+  const int npad = E * NT;
   for (int kk = 2; kk <= npad; kk <<= 1) {
     int j = kk >> 1;
     // partner in another register of this thread
-    for (; j >= kSortBlock; j >>= 1) {
-      const int je = j / kSortBlock;
+    for (; j >= NT; j >>= 1) {
+      const int je = j / NT;
 #pragma unroll
       for (int e = 0; e < kMaxE; e++) {
         const int pe = e ^ je;
         if (e < E && pe > e) {
-          const int i = e * kSortBlock + tid;
+          const int i = e * NT + tid;
           const bool up = (i & kk) == 0;
           const unsigned long long a = v[e], b = v[pe];
           if ((a > b) == up) {
@@ -156,10 +179,10 @@ __device__ inline void block_bitonic(unsigned long long (&v)[kMaxE], int E,
     if (j >= kWave) {
 #pragma unroll
       for (int e = 0; e < kMaxE; e++)
-        if (e < E) lds[e * kSortBlock + tid] = v[e];
+        if (e < E) lds[e * NT + tid] = v[e];
       __syncthreads();
       for (; j >= kWave; j >>= 1) {
-        for (int t = tid; t < (npad >> 1); t += kSortBlock) {
+        for (int t = tid; t < (npad >> 1); t += NT) {
           const int i = 2 * j * (t / j) + (t % j);
           const int l = i + j;
           const unsigned long long a = lds[i], b = lds[l];
@@ -172,7 +195,7 @@ __device__ inline void block_bitonic(unsigned long long (&v)[kMaxE], int E,
       }
 #pragma unroll
       for (int e = 0; e < kMaxE; e++)
-        if (e < E) v[e] = lds[e * kSortBlock + tid];
+        if (e < E) v[e] = lds[e * NT + tid];
       __syncthreads();
     }
     // partner in the same wave: cross-lane exchange
@@ -180,7 +203,7 @@ __device__ inline void block_bitonic(unsigned long long (&v)[kMaxE], int E,
 #pragma unroll
       for (int e = 0; e < kMaxE; e++) {
         if (e < E) {
-          const int i = e * kSortBlock + tid;
+          const int i = e * NT + tid;
           const unsigned long long o = shfl_xor_u64(v[e], j);
           const bool lower = (i & j) == 0;
           const bool up = (i & kk) == 0;

@@ -22,6 +22,8 @@
 namespace pcr {
 
 constexpr int kKnnMaxSortN = 4096;        // single-workgroup LDS sort up to here
+constexpr int kSmallSortThreads = 256;
+constexpr int kSmallSortN = kSmallSortThreads * kMaxE;
 constexpr int kKnnMaxN = 1 << 22;         // global counting sort beyond
 constexpr int kBigCellBits = 15;          // top Morton bits of the global sort (32^3 cells)
 constexpr int kBigCells = 1 << kBigCellBits;
@@ -94,21 +96,23 @@ __device__ inline unsigned quant10(float v, float lo, float scale) {
   return (unsigned)t;
 }
 
-__global__ __launch_bounds__(kSortBlock) void knn_sort_kernel(const float* __restrict__ pts,
-                                                              int n, int npad_sort, KnnSet s) {
+template <int NT>
+__global__ __launch_bounds__(NT) void knn_sort_kernel(const float* __restrict__ pts, int n,
+                                                      int npad_sort, KnnSet s) {
   extern __shared__ __align__(16) unsigned long long keys[];  // [npad_sort]
-  __shared__ float red[6][kSortBlock / kWave];
+  __shared__ float red[6][NT / kWave];
   __shared__ float frame[6];
+  latency_kernel_priority();
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
-  const int E = npad_sort / kSortBlock;
+  const int E = npad_sort / NT;
   const float* P = pts + (size_t)b * 3 * n;
   float px[kMaxE], py[kMaxE], pz[kMaxE];
   float mn[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
   float mx[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
 #pragma unroll
   for (int e = 0; e < kMaxE; e++) {
-    const int i = e * kSortBlock + tid;
+    const int i = e * NT + tid;
     const bool ok = e < E && i < n;
     px[e] = ok ? P[i] : __builtin_nanf("");
     py[e] = ok ? P[n + i] : __builtin_nanf("");
@@ -138,7 +142,7 @@ __global__ __launch_bounds__(kSortBlock) void knn_sort_kernel(const float* __res
   __syncthreads();
   if (tid < 6) {
     float v = red[tid][0];
-    for (int w = 1; w < kSortBlock / kWave; w++)
+    for (int w = 1; w < NT / kWave; w++)
       v = tid < 3 ? fminf(v, red[tid][w]) : fmaxf(v, red[tid][w]);
     frame[tid] = v;
   }
@@ -155,13 +159,13 @@ __global__ __launch_bounds__(kSortBlock) void knn_sort_kernel(const float* __res
   // order (keys are compared lexicographically), only its speed does.
   int* hist = (int*)keys;     // [4096]
   int* order = hist + 4096;   // [n]
-  __shared__ int scan_b[kSortBlock / kWave + 1];
-  for (int c = tid; c < 4096; c += kSortBlock) hist[c] = 0;
+  __shared__ int scan_b[NT / kWave + 1];
+  for (int c = tid; c < 4096; c += NT) hist[c] = 0;
   __syncthreads();
   int cell[kMaxE], slot[kMaxE];
 #pragma unroll
   for (int e = 0; e < kMaxE; e++) {
-    const int i = e * kSortBlock + tid;
+    const int i = e * NT + tid;
     cell[e] = -1;
     if (e < E && i < n) {
       const unsigned code = spread10(quant10(px[e], lo[0], sc[0])) |
@@ -173,25 +177,32 @@ __global__ __launch_bounds__(kSortBlock) void knn_sort_kernel(const float* __res
   }
   __syncthreads();
   {
-    const int c0 = tid * 4;  // 4096 bins / 1024 threads
-    const int h0 = hist[c0], h1 = hist[c0 + 1], h2 = hist[c0 + 2], h3 = hist[c0 + 3];
-    const int sum = h0 + h1 + h2 + h3;
+    constexpr int CPT = 4096 / NT;  // bins per thread
+    const int c0 = tid * CPT;
+    int h[CPT];
+    int sum = 0;
+#pragma unroll
+    for (int q = 0; q < CPT; q++) {
+      h[q] = hist[c0 + q];
+      sum += h[q];
+    }
     const int incl = block_inclusive_scan(sum, scan_b);
-    const int run = incl - sum;
-    hist[c0] = run;
-    hist[c0 + 1] = run + h0;
-    hist[c0 + 2] = run + h0 + h1;
-    hist[c0 + 3] = run + h0 + h1 + h2;
+    int run = incl - sum;
+#pragma unroll
+    for (int q = 0; q < CPT; q++) {
+      hist[c0 + q] = run;
+      run += h[q];
+    }
   }
   __syncthreads();
 #pragma unroll
   for (int e = 0; e < kMaxE; e++)
-    if (cell[e] >= 0) order[hist[cell[e]] + slot[e]] = e * kSortBlock + tid;
+    if (cell[e] >= 0) order[hist[cell[e]] + slot[e]] = e * NT + tid;
   __syncthreads();
   // sorted SoA + per-block boxes (one wave per block)
   const size_t base = (size_t)b * s.npad;
   const int lane = tid & 63;
-  for (int blk = tid >> 6; blk < s.nblk; blk += kSortBlock / kWave) {
+  for (int blk = tid >> 6; blk < s.nblk; blk += NT / kWave) {
     const int p = blk * kBlk + lane;
     float x = __builtin_nanf(""), y = x, z = x;
     int j = -1;
@@ -1176,10 +1187,20 @@ static void launch_sort(const float* pts, int b, int n, const KnnSet& s, hipStre
     hipLaunchKernelGGL(knn_big_boxes_kernel, dim3(ceil_div(s.nblk, 4), b), dim3(256), 0, st, s);
     return;
   }
-  const int npad_sort = next_pow2i(n < kSortBlock ? kSortBlock : n);
+  // clouds of <= 1024 points: 256 threads (four points each), so the sort
+  // fits on a CU beside the other stream's grid kernel
   const size_t smem = 4096 * 4 + (size_t)n * 4;
-  allow_big_lds(knn_sort_kernel, smem);
-  hipLaunchKernelGGL(knn_sort_kernel, dim3(b), dim3(kSortBlock), smem, st, pts, n, npad_sort, s);
+  if (n <= kSmallSortN) {
+    const int npad_sort = next_pow2i(n < kSmallSortThreads ? kSmallSortThreads : n);
+    allow_big_lds(knn_sort_kernel<kSmallSortThreads>, smem);
+    hipLaunchKernelGGL((knn_sort_kernel<kSmallSortThreads>), dim3(b), dim3(kSmallSortThreads),
+                       smem, st, pts, n, npad_sort, s);
+  } else {
+    const int npad_sort = next_pow2i(n < kSortBlock ? kSortBlock : n);
+    allow_big_lds(knn_sort_kernel<kSortBlock>, smem);
+    hipLaunchKernelGGL((knn_sort_kernel<kSortBlock>), dim3(b), dim3(kSortBlock), smem, st, pts,
+                       n, npad_sort, s);
+  }
 }
 
 template <int KM, bool PPF>

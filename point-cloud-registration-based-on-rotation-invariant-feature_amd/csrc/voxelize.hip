@@ -29,6 +29,8 @@
 namespace pcr {
 
 constexpr int kPrepThreads = kSortBlock;
+constexpr int kSmallPrepThreads = 256;
+constexpr int kSmallPrepN = kSmallPrepThreads * kMaxE;
 constexpr int kMaxSortN = kSortBlock * kMaxE;
 constexpr int kGridThreads = 256;
 constexpr int kDevoxThreads = 1024;
@@ -95,32 +97,45 @@ static inline int next_pow2(int v) {
 // 1024 keys instead of 55.
 
 // Fixed-order per-axis mean of a cloud in double, the order the oracle
-// restates (orc_cloud_mean): thread t sums points t, t+1024, ... ascending;
-// each wave halves 64 partials (l += l+s for s = 32..1); the 16 wave sums
-// are halved the same way.  Returns the three means on every thread.
+// restates (orc_cloud_mean): "virtual thread" T of 1024 sums points T,
+// T+1024, ... ascending; each virtual wave halves its 64 partials (l += l+s
+// for s = 32..1); the 16 virtual-wave sums are halved the same way.  With
+// NT = 1024 threads the virtual threads are the real ones; with NT = 256
+// (clouds of <= 1024 points) thread t holds virtual threads t + e*256, e = 0..3
+// (one point each), so its register e joins virtual wave 4e + (t >> 6).
+// Returns the three means on every thread.
+template <int NT>
 __device__ inline void cloud_mean(const float (&px)[kMaxE], const float (&py)[kMaxE],
                                   const float (&pz)[kMaxE], int E, int n, double* red,
                                   float* mean_out) {
+  static_assert(NT == 1024 || NT == 256, "prep workgroup size");
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  double s[3] = {0.0, 0.0, 0.0};
+  constexpr int R = NT == 1024 ? 1 : kMaxE;  // virtual waves per real wave
+  double s[R][3];
+#pragma unroll
+  for (int q = 0; q < R; q++) s[q][0] = s[q][1] = s[q][2] = 0.0;
 #pragma unroll
   for (int e = 0; e < kMaxE; e++) {
-    if (e < E && e * kPrepThreads + tid < n) {
-      s[0] += (double)px[e];
-      s[1] += (double)py[e];
-      s[2] += (double)pz[e];
+    const int q = NT == 1024 ? 0 : e;
+    if (e < E && e * NT + tid < n) {
+      s[q][0] += (double)px[e];
+      s[q][1] += (double)py[e];
+      s[q][2] += (double)pz[e];
     }
   }
 #pragma unroll
-  for (int a = 0; a < 3; a++) {
+  for (int q = 0; q < R; q++) {
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      const double o = __shfl_down(s[a], off, kWave);
-      if (lane < off) s[a] += o;
+    for (int a = 0; a < 3; a++) {
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        const double o = __shfl_down(s[q][a], off, kWave);
+        if (lane < off) s[q][a] += o;
+      }
+      if (lane == 0) red[a * 16 + q * (NT / kWave) + w] = s[q][a];
     }
-    if (lane == 0) red[a * 16 + w] = s[a];
   }
-  __syncthreads();
+  lds_barrier();
   if (tid < 3) {
     double v[16];
 #pragma unroll
@@ -131,27 +146,29 @@ __device__ inline void cloud_mean(const float (&px)[kMaxE], const float (&py)[kM
       for (int i = 0; i < off; i++) v[i] += v[i + off];
     mean_out[tid] = (float)(v[0] / (double)n);
   }
-  __syncthreads();
+  lds_barrier();
 }
 
-template <int MODE>
-__global__ __launch_bounds__(kPrepThreads) void vox_prep_kernel(
+template <int MODE, int NT>
+__global__ __launch_bounds__(NT) void vox_prep_kernel(
     const float* __restrict__ coords_f, const int* __restrict__ coords_i, int n, int r, int npad,
     float* __restrict__ norm_out, int* __restrict__ ind, VoxWs ws, int* __restrict__ dinds,
     float* __restrict__ dwgts) {
   extern __shared__ __align__(16) unsigned char smem_raw[];
   unsigned long long* keys = (unsigned long long*)smem_raw;  // [npad]
   unsigned* bm = (unsigned*)(keys + npad);                     // [W]
-  __shared__ int scan_s[kPrepThreads / kWave + 1];
+  __shared__ int scan_s[NT / kWave + 1];
   __shared__ double red[48];
   __shared__ float s_stat[4];
+  __shared__ int s_flag;  // a crowded voxel: the bitonic path
 
+  latency_kernel_priority();
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
-  const int nt = kPrepThreads;
+  constexpr int nt = NT;
   const int r3 = r * r * r;
   const int W = ws.W;
-  const int E = npad / kPrepThreads;
+  const int E = npad / NT;
   PCR_STAMP(0);
 
   float px[kMaxE], py[kMaxE], pz[kMaxE];
@@ -178,9 +195,10 @@ __global__ __launch_bounds__(kPrepThreads) void vox_prep_kernel(
     }
   }
   for (int w = tid; w < W; w += nt) bm[w] = 0u;
+  if (tid == 0) s_flag = 0;
 
   if (MODE == kSphNormalize) {
-    cloud_mean(px, py, pz, E, n, red, s_stat);
+    cloud_mean<NT>(px, py, pz, E, n, red, s_stat);
     PCR_STAMP(1);
     const float m0 = s_stat[0], m1 = s_stat[1], m2 = s_stat[2];
     float mx = 0.0f;
@@ -195,13 +213,13 @@ __global__ __launch_bounds__(kPrepThreads) void vox_prep_kernel(
     }
     mx = wave_max(mx);
     if ((tid & 63) == 0) scan_s[tid >> 6] = __float_as_int(mx);
-    __syncthreads();
+    lds_barrier();
     if (tid == 0) {
       float m = 0.0f;
       for (int w = 0; w < nt / kWave; w++) m = fmaxf(m, __int_as_float(scan_s[w]));
       s_stat[3] = m + 1e-20f;
     }
-    __syncthreads();
+    lds_barrier();
     const float den = s_stat[3];
 #pragma unroll
     for (int e = 0; e < kMaxE; e++) {
@@ -274,7 +292,7 @@ __global__ __launch_bounds__(kPrepThreads) void vox_prep_kernel(
     const unsigned v = (unsigned)(kv[e] >> 32);
     if (e < E && v != 0xFFFFFFFFu) atomicOr(&bm[v >> 5], 1u << (v & 31));
   }
-  __syncthreads();
+  lds_barrier();
   // 2. per-word exclusive prefix of popcounts (rank of a voxel among the
   //    occupied ones == its segment id, segments in voxel order)
   {
@@ -293,7 +311,7 @@ __global__ __launch_bounds__(kPrepThreads) void vox_prep_kernel(
     }
     if (tid == nt - 1) s_stat[0] = __int_as_float(pincl);  // number of segments
   }
-  __syncthreads();
+  lds_barrier();
   const int nseg = __float_as_int(s_stat[0]);
   // devox corners -> their voxel's segment (the grid kernel's devox part
   // gathers the voxel means by segment without a bitmap lookup); the corner
@@ -320,6 +338,7 @@ __global__ __launch_bounds__(kPrepThreads) void vox_prep_kernel(
       }
     }
   }
+  PCR_STAMP(4);
   // 3. counts per segment; arrival slot within the segment (unstable)
   int seg_of[kMaxE], slot_of[kMaxE];
 #pragma unroll
@@ -334,7 +353,7 @@ __global__ __launch_bounds__(kPrepThreads) void vox_prep_kernel(
       seg_vox[sg] = (int)v;
     }
   }
-  __syncthreads();
+  lds_barrier();
   // 4. exclusive scan of the counts -> segment offsets; largest segment
   int big = 0;
   {
@@ -347,7 +366,7 @@ __global__ __launch_bounds__(kPrepThreads) void vox_prep_kernel(
     }
     const int incl = block_inclusive_scan(sum, scan_s);
     int run = incl - sum;
-    __syncthreads();
+    lds_barrier();
     for (int q = s0; q < s1; q++) {
       const int c = cnt_l[q];
       cnt_l[q] = run;  // now the segment start
@@ -360,17 +379,20 @@ __global__ __launch_bounds__(kPrepThreads) void vox_prep_kernel(
       s_stat[1] = __int_as_float(incl);  // number of valid points
     }
   }
+  PCR_STAMP(5);
   // 5. place the points in arrival order, then every point finds its rank
   //    among its voxel's points (ascending point order, the order the means
   //    are accumulated in) by one sweep of that voxel's slots -- independent
   //    LDS reads, no serial per-voxel pass.  A cloud with a crowded voxel
   //    takes the bitonic path.
-  const int crowded = __syncthreads_or(big > 32);
+  if (__any(big > 32)) s_flag = 1;
+  lds_barrier();
+  const int crowded = s_flag;
   if (!crowded) {
 #pragma unroll
     for (int e = 0; e < kMaxE; e++)
       if (seg_of[e] >= 0) perm_l[cnt_l[seg_of[e]] + slot_of[e]] = (int)(unsigned)(kv[e] & 0xFFFFFFFFull);
-    __syncthreads();
+    lds_barrier();
     const int nvalid = __float_as_int(s_stat[1]);
 #pragma unroll
     for (int e = 0; e < kMaxE; e++) {
@@ -386,15 +408,13 @@ __global__ __launch_bounds__(kPrepThreads) void vox_prep_kernel(
   } else {
     // unique 64-bit keys (the low word is the point id): sorting them is a
     // stable sort by voxel
-    block_bitonic(kv, E, keys);
+    block_bitonic<NT>(kv, E, keys);
 #pragma unroll
     for (int e = 0; e < kMaxE; e++)
       if (e < E) keys[e * nt + tid] = kv[e];
-    __syncthreads();
+    lds_barrier();
     for (int p = tid; p < n; p += nt) perm[p] = (int)(unsigned)(keys[p] & 0xFFFFFFFFull);
   }
-  PCR_STAMP(4);
-  PCR_STAMP(5);
   PCR_STAMP(6);
 }
 
@@ -411,6 +431,9 @@ __global__ __launch_bounds__(NT) void vox_grid_kernel(
     float* __restrict__ out, int* __restrict__ cnt_out, const int* __restrict__ dinds,
     const float* __restrict__ dwgts, float* __restrict__ devox, float* __restrict__ desc) {
   extern __shared__ __align__(16) unsigned char smem_raw[];
+#if defined(KNN_EXP) && KNN_EXP == 11
+  if (PART & 1) __builtin_amdgcn_s_setprio(2);
+#endif
   const int tile = blockIdx.x;
   const int role = PART;
   const int grp = blockIdx.y;
@@ -660,7 +683,7 @@ __global__ __launch_bounds__(NT) void vox_grid_kernel(
         float m = wave_max(vmax[g]);
         if ((tid & 63) == 0) red[tid >> 6][g] = m;
       }
-      __syncthreads();
+      lds_barrier();  // not waiting for the grid / devox stores
       if (tid < gcount) {
         float m = red[0][tid];
         for (int w = 1; w < NT / kWave; w++) m = fmaxf(m, red[w][tid]);
@@ -717,7 +740,7 @@ __global__ __launch_bounds__(kPrepThreads) void sph_normalize_kernel(
     py[e] = ok ? x[i + n] : 0.0f;
     pz[e] = ok ? x[i + 2 * n] : 0.0f;
   }
-  cloud_mean(px, py, pz, E, n, red, s_stat);
+  cloud_mean<kPrepThreads>(px, py, pz, E, n, red, s_stat);
   const float m0 = s_stat[0], m1 = s_stat[1], m2 = s_stat[2];
   float mx = 0.0f;
 #pragma unroll
@@ -913,12 +936,25 @@ static pcr_status run_voxelize(const float* features, const float* coords_f, con
   PCR_REQUIRE(workspace != nullptr && ws_bytes >= need, "%s: workspace too small (%zu < %zu)",
               name, ws_bytes, need);
   if (what & 1) {
-    const int npad = next_pow2(n < kPrepThreads ? kPrepThreads : n);
+    // clouds of <= 1024 points: 256 threads (four points each), so a prep
+    // workgroup fits on a CU beside the other stream's KNN selection instead
+    // of waiting for whole CUs to drain
+    const bool small = n <= kSmallPrepN;
+    const int nt = small ? kSmallPrepThreads : kPrepThreads;
+    const int npad = next_pow2(n < nt ? nt : n);
     size_t prep_smem = (size_t)npad * 8 + (size_t)ws.W * 8 + (size_t)n * 8;
     PCR_REQUIRE(prep_smem <= 150 * 1024, "%s: prep LDS %zu too large", name, prep_smem);
-    allow_big_lds(vox_prep_kernel<MODE>, prep_smem);
-    hipLaunchKernelGGL(vox_prep_kernel<MODE>, dim3(b), dim3(kPrepThreads), prep_smem, stream,
-                       coords_f, coords_i, n, r, npad, norm_out, ind, ws, dinds, dwgts);
+    if (small) {
+      allow_big_lds(vox_prep_kernel<MODE, kSmallPrepThreads>, prep_smem);
+      hipLaunchKernelGGL((vox_prep_kernel<MODE, kSmallPrepThreads>), dim3(b),
+                         dim3(kSmallPrepThreads), prep_smem, stream, coords_f, coords_i, n, r,
+                         npad, norm_out, ind, ws, dinds, dwgts);
+    } else {
+      allow_big_lds(vox_prep_kernel<MODE, kPrepThreads>, prep_smem);
+      hipLaunchKernelGGL((vox_prep_kernel<MODE, kPrepThreads>), dim3(b), dim3(kPrepThreads),
+                         prep_smem, stream, coords_f, coords_i, n, r, npad, norm_out, ind, ws,
+                         dinds, dwgts);
+    }
   }
   const bool do_grid = (what & 2) != 0;
   const bool do_dev = (what & 4) != 0 && devox != nullptr;
