@@ -456,11 +456,14 @@ __global__ __launch_bounds__(NT) void vox_grid_kernel(
   const int s_end = (we >= W) ? nseg : gpre[we];
   const int S = s_end - s_begin;
 
-  // LDS carve: feat_s[G][n] | mean_s[G][n] | scnt_s[n] | bm_s[nw] | pre_s[nw]
+  // LDS carve: feat_s[G][n] | mean_s[G][ns] | scnt_s[ns] | bm_s[nw] | pre_s[nw];
+  // ns = n + 1: slot n of every mean / count row holds 0, the value of an
+  // empty cell or corner, so the gathers below need no masking
+  const int ns = n + 1;
   float* feat_s = (float*)smem_raw;
   float* mean_s = feat_s + (size_t)G * n;
-  int* scnt_s = (int*)(mean_s + (size_t)G * n);
-  unsigned* bm_s = (unsigned*)(scnt_s + n);
+  int* scnt_s = (int*)(mean_s + (size_t)G * ns);
+  unsigned* bm_s = (unsigned*)(scnt_s + ns);
   int* pre_s = (int*)(bm_s + nw);
 
   for (int w = tid; w < nw; w += NT) {
@@ -502,9 +505,11 @@ __global__ __launch_bounds__(NT) void vox_grid_kernel(
     }
 #pragma unroll
     for (int g = 0; g < MG; g++)
-      if (g < gcount) mean_s[(size_t)g * n + si] = acc[g];
+      if (g < gcount) mean_s[(size_t)g * ns + si] = acc[g];
     scnt_s[si] = end - off;
   }
+  if (tid < G) mean_s[(size_t)tid * ns + n] = 0.0f;
+  if (tid == 0) scnt_s[n] = 0;
   __syncthreads();
 
   PCR_STAMP(10);
@@ -531,8 +536,7 @@ __global__ __launch_bounds__(NT) void vox_grid_kernel(
       if (g < gcount) {
         float fv[8];
 #pragma unroll
-        for (int q = 0; q < 8; q++)
-          fv[q] = dv_s[u][q] >= 0 ? mean_s[(size_t)g * n + dv_s[u][q]] : 0.0f;
+        for (int q = 0; q < 8; q++) fv[q] = mean_s[(size_t)g * ns + dv_s[u][q]];
         const float v = pcr_wsum8(dv_w[u], fv);
         ov[(size_t)g * n + i] = v;
         vmax[g] = fmaxf(vmax[g], v);
@@ -548,10 +552,44 @@ __global__ __launch_bounds__(NT) void vox_grid_kernel(
 #pragma unroll
       for (int q = 0; q < 8; q++) {
         dv_w[u][q] = i < n ? Wt[i + (size_t)q * n] : 0.0f;
-        dv_s[u][q] = i < n ? Dg[i + (size_t)q * n] : -1;
+        const int sg = i < n ? Dg[i + (size_t)q * n] : -1;
+        dv_s[u][q] = sg >= 0 ? sg : n;  // empty corner -> the zero slot
       }
     }
   }
+  // one streaming iteration: 4 consecutive cells from `base` (r^3 % 4 == 0),
+  // one 16-byte store per channel (+ cnt).  The cells' ranks come from the
+  // occupancy word and its prefix; a wave whose 256 cells are all empty
+  // (common: the outer shells of the spherical grid) stores zeros directly.
+  auto stream4 = [&](int base) {
+    const int wl = (base >> 5) - wb;
+    const unsigned word = bm_s[wl];
+    const int sh = base & 31;
+    const unsigned nib = (word >> sh) & 15u;
+    if (__any(nib != 0u)) {
+      const int pre = pre_s[wl] + __popc(word & ((1u << sh) - 1u));
+      int ix[4];
+      ix[0] = (nib & 1u) ? pre : n;
+      ix[1] = (nib & 2u) ? pre + (int)(nib & 1u) : n;
+      ix[2] = (nib & 4u) ? pre + __popc(nib & 3u) : n;
+      ix[3] = (nib & 8u) ? pre + __popc(nib & 7u) : n;
+#pragma unroll
+      for (int g = 0; g < MG; g++) {
+        if (g < gcount) {
+          const float* ms = mean_s + (size_t)g * ns;
+          const float4 v = {ms[ix[0]], ms[ix[1]], ms[ix[2]], ms[ix[3]]};
+          *(float4*)(ob + (size_t)g * r3 + base) = v;
+        }
+      }
+      if (cb) *(int4*)(cb + base) = int4{scnt_s[ix[0]], scnt_s[ix[1]], scnt_s[ix[2]], scnt_s[ix[3]]};
+    } else {
+      const float4 z = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int g = 0; g < MG; g++)
+        if (g < gcount) *(float4*)(ob + (size_t)g * r3 + base) = z;
+      if (cb) *(int4*)(cb + base) = int4{0, 0, 0, 0};
+    }
+  };
   if (!(role & 1)) {
   } else if (interleave) {
     // the streaming iterations in PB chunks, one devox point after each
@@ -561,67 +599,12 @@ __global__ __launch_bounds__(NT) void vox_grid_kernel(
       const int it1 = (u + 1) * iters / PB;
       for (int it = u * iters / PB; it < it1; it++) {
         const int base = cell0 + tid * 4 + it * NT * 4;
-        if (base >= cell1) continue;
-        const int wl = (base >> 5) - wb;
-        const unsigned word = bm_s[wl];
-        const int pre = pre_s[wl];
-        const int sh = base & 31;
-        int rk[4];
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-          const unsigned bit = 1u << (sh + j);
-          rk[j] = (word & bit) ? pre + __popc(word & (bit - 1u)) : -1;
-        }
-        for (int g = 0; g < gcount; g++) {
-          const float* ms = mean_s + (size_t)g * n;
-          float4 v;
-          v.x = rk[0] >= 0 ? ms[rk[0]] : 0.0f;
-          v.y = rk[1] >= 0 ? ms[rk[1]] : 0.0f;
-          v.z = rk[2] >= 0 ? ms[rk[2]] : 0.0f;
-          v.w = rk[3] >= 0 ? ms[rk[3]] : 0.0f;
-          *(float4*)(ob + (size_t)g * r3 + base) = v;
-        }
-        if (cb) {
-          int4 cv;
-          cv.x = rk[0] >= 0 ? scnt_s[rk[0]] : 0;
-          cv.y = rk[1] >= 0 ? scnt_s[rk[1]] : 0;
-          cv.z = rk[2] >= 0 ? scnt_s[rk[2]] : 0;
-          cv.w = rk[3] >= 0 ? scnt_s[rk[3]] : 0;
-          *(int4*)(cb + base) = cv;
-        }
+        if (base < cell1) stream4(base);
       }
       devox_point(u);
     }
   } else if ((r3 & 3) == 0) {
-    for (int base = cell0 + tid * 4; base < cell1; base += NT * 4) {
-      const int wl = (base >> 5) - wb;
-      const unsigned word = bm_s[wl];
-      const int pre = pre_s[wl];
-      const int sh = base & 31;
-      int rk[4];
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const unsigned bit = 1u << (sh + j);
-        rk[j] = (word & bit) ? pre + __popc(word & (bit - 1u)) : -1;
-      }
-      for (int g = 0; g < gcount; g++) {
-        const float* ms = mean_s + (size_t)g * n;
-        float4 v;
-        v.x = rk[0] >= 0 ? ms[rk[0]] : 0.0f;
-        v.y = rk[1] >= 0 ? ms[rk[1]] : 0.0f;
-        v.z = rk[2] >= 0 ? ms[rk[2]] : 0.0f;
-        v.w = rk[3] >= 0 ? ms[rk[3]] : 0.0f;
-        *(float4*)(ob + (size_t)g * r3 + base) = v;
-      }
-      if (cb) {
-        int4 cv;
-        cv.x = rk[0] >= 0 ? scnt_s[rk[0]] : 0;
-        cv.y = rk[1] >= 0 ? scnt_s[rk[1]] : 0;
-        cv.z = rk[2] >= 0 ? scnt_s[rk[2]] : 0;
-        cv.w = rk[3] >= 0 ? scnt_s[rk[3]] : 0;
-        *(int4*)(cb + base) = cv;
-      }
-    }
+    for (int base = cell0 + tid * 4; base < cell1; base += NT * 4) stream4(base);
   } else {
     for (int cell = cell0 + tid; cell < cell1; cell += NT) {
       const int wl = (cell >> 5) - wb;
@@ -629,7 +612,7 @@ __global__ __launch_bounds__(NT) void vox_grid_kernel(
       const unsigned bit = 1u << (cell & 31);
       const int rk = (word & bit) ? pre_s[wl] + __popc(word & (bit - 1u)) : -1;
       for (int g = 0; g < gcount; g++)
-        ob[(size_t)g * r3 + cell] = rk >= 0 ? mean_s[(size_t)g * n + rk] : 0.0f;
+        ob[(size_t)g * r3 + cell] = rk >= 0 ? mean_s[(size_t)g * ns + rk] : 0.0f;
       if (cb) cb[cell] = rk >= 0 ? scnt_s[rk] : 0;
     }
   }
@@ -653,7 +636,8 @@ __global__ __launch_bounds__(NT) void vox_grid_kernel(
 #pragma unroll
           for (int q = 0; q < 8; q++) {
             dv_w[u][q] = i < n ? Wt[i + (size_t)q * n] : 0.0f;
-            dv_s[u][q] = i < n ? Dg[i + (size_t)q * n] : -1;
+            const int sg = i < n ? Dg[i + (size_t)q * n] : -1;
+            dv_s[u][q] = sg >= 0 ? sg : n;
           }
         }
         float* ov = devox + ((size_t)b * c + c0) * n;
@@ -667,7 +651,7 @@ __global__ __launch_bounds__(NT) void vox_grid_kernel(
               float fv[8];
 #pragma unroll
               for (int q = 0; q < 8; q++)
-                fv[q] = dv_s[u][q] >= 0 ? mean_s[(size_t)g * n + dv_s[u][q]] : 0.0f;
+                fv[q] = mean_s[(size_t)g * ns + dv_s[u][q]];
               const float v = pcr_wsum8(dv_w[u], fv);
               ov[(size_t)g * n + i] = v;
               vmax[g] = fmaxf(vmax[g], v);
@@ -911,7 +895,7 @@ static int pick_groups(int c, int n, int max_g, int* G_out) {
 }
 
 static size_t grid_smem_bytes(int G, int n, int nw) {
-  return ((size_t)2 * G * n + n + 2 * (size_t)nw) * 4;
+  return ((size_t)G * n + (size_t)G * (n + 1) + (n + 1) + 2 * (size_t)nw) * 4;
 }
 
 // Launch helpers.  `what`: 1 = prep only, 2 = grid only, 3 = both.
