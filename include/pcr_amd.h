@@ -226,6 +226,23 @@ pcr_status pcr_extractor_voxel_grid_devox(const float *features, int b, int c, i
                                           const float *dwgts, float *desc, void *workspace,
                                           size_t workspace_bytes, void *stream);
 
+/* The voxel stage split so the dense grid streams beside the KNN selection
+ * (what vox_grid_kernel<3> does in one launch, in two):
+ *   means_devox: the voxel means of every occupied segment (fixed ascending
+ *     point order) into the workspace, spherical_trilinear_devoxelize of them
+ *     (spherical_trilinear_devox.cu:23-136) and the per-cloud descriptor;
+ *   stream: the dense [B, C, r^3] grid + cnt [B, r^3] of
+ *     spherical_avg_voxelize_forward (spherical_vox.cu:19-125) from those
+ *     means, written once, zeros included.
+ * Both read the workspace pcr_extractor_voxel_prep filled; its size is
+ * pcr_extractor_workspace_size(b, n, c, r).  r^3 <= 65536, r^3 % 4 == 0. */
+pcr_status pcr_extractor_voxel_means_devox(const float *features, int b, int c, int n, int r,
+                                           float *devox, const int *dinds, const float *dwgts,
+                                           float *desc, void *workspace, size_t workspace_bytes,
+                                           void *stream);
+pcr_status pcr_extractor_voxel_stream(int b, int c, int n, int r, int *cnt, float *grid,
+                                      void *workspace, size_t workspace_bytes, void *stream);
+
 /* ------------------------------------------------------ self tests ------
  * Device evaluation of the shared bit-exact math (include/pcr_math.h) for
  * host-vs-device parity tests.  op: 0 acosf, 1 atanf, 2 sqrtf, 3 x/y,

@@ -46,12 +46,15 @@ struct VoxWs {
   unsigned* bitmap;  // [b][W] occupancy bits
   int* wprefix;      // [b][W] occupied voxels before word w
   int* dseg;         // [b][8][n] segment of each devox corner (-1: empty / none)
+  float* means;      // [b][c][ms] voxel means per occupied segment (extractor only)
+  unsigned short* segcnt;  // [b][ms] points per occupied segment (extractor only)
+  int ms;            // row stride of means / segcnt: n + 1 rounded up to 4
   int W;             // words per cloud = ceil(r^3 / 32)
 };
 
 static inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
-static size_t vox_ws_layout(int b, int n, int r, VoxWs* ws, void* base) {
+static size_t vox_ws_layout(int b, int n, int r, VoxWs* ws, void* base, int cm = 0) {
   const int64_t r3 = (int64_t)r * r * r;
   const int W = (int)((r3 + 31) / 32);
   size_t off = 0;
@@ -68,7 +71,15 @@ static size_t vox_ws_layout(int b, int n, int r, VoxWs* ws, void* base) {
   unsigned* bitmap = (unsigned*)take((size_t)b * W * 4);
   int* wprefix = (int*)take((size_t)b * W * 4);
   int* dseg = (int*)take((size_t)b * 8 * n * 4);
+  const int ms = (n + 1 + 3) / 4 * 4;
+  // + 16 KB: vox_stream_kernel's LDS-DMA reads a whole item's pieces, past
+  // the last row when c is odd
+  float* means = cm > 0 ? (float*)take((size_t)b * cm * ms * 4 + 16384) : nullptr;
+  unsigned short* segcnt = cm > 0 ? (unsigned short*)take((size_t)b * ms * 2 + 16) : nullptr;
   if (ws) {
+    ws->means = means;
+    ws->segcnt = segcnt;
+    ws->ms = ms;
     ws->dseg = dseg;
     ws->perm = perm;
     ws->seg_off = seg_off;
@@ -108,15 +119,15 @@ template <int NT>
 __device__ inline void cloud_mean(const float (&px)[kMaxE], const float (&py)[kMaxE],
                                   const float (&pz)[kMaxE], int E, int n, double* red,
                                   float* mean_out) {
-  static_assert(NT == 1024 || NT == 256, "prep workgroup size");
+  static_assert(NT == 1024 || NT == 512 || NT == 256, "prep workgroup size");
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  constexpr int R = NT == 1024 ? 1 : kMaxE;  // virtual waves per real wave
+  constexpr int R = 1024 / NT;  // virtual waves per real wave
   double s[R][3];
 #pragma unroll
   for (int q = 0; q < R; q++) s[q][0] = s[q][1] = s[q][2] = 0.0;
 #pragma unroll
   for (int e = 0; e < kMaxE; e++) {
-    const int q = NT == 1024 ? 0 : e;
+    const int q = e % R;
     if (e < E && e * NT + tid < n) {
       s[q][0] += (double)px[e];
       s[q][1] += (double)py[e];
@@ -429,15 +440,18 @@ template <int PART, int NT, int MG>
 __global__ __launch_bounds__(NT) void vox_grid_kernel(
     const float* __restrict__ feat, int c, int n, int r3, int G, int tile_cells, VoxWs ws,
     float* __restrict__ out, int* __restrict__ cnt_out, const int* __restrict__ dinds,
-    const float* __restrict__ dwgts, float* __restrict__ devox, float* __restrict__ desc) {
+    const float* __restrict__ dwgts, float* __restrict__ devox, float* __restrict__ desc,
+    int ntiles, int ngrp, int nitems) {
   extern __shared__ __align__(16) unsigned char smem_raw[];
-#if defined(KNN_EXP) && KNN_EXP == 11
-  if (PART & 1) __builtin_amdgcn_s_setprio(2);
-#endif
-  const int tile = blockIdx.x;
+  // work items (tile, channel group, cloud), tile fastest; a launch of fewer
+  // workgroups than items loops over them, so the kernel holds few CU slots
+  // while it streams and other streams' kernels fit beside it
+  for (int item = blockIdx.x; item < nitems; item += gridDim.x) {
+  if (item != (int)blockIdx.x) __syncthreads();  // LDS of the previous item
+  const int tile = item % ntiles;
   const int role = PART;
-  const int grp = blockIdx.y;
-  const int b = blockIdx.z;
+  const int grp = (item / ntiles) % ngrp;
+  const int b = item / (ntiles * ngrp);
   const int tid = threadIdx.x;
   const int W = ws.W;
   const int cell0 = tile * tile_cells;
@@ -513,6 +527,17 @@ __global__ __launch_bounds__(NT) void vox_grid_kernel(
   __syncthreads();
 
   PCR_STAMP(10);
+  // compact means for vox_stream_kernel (one tile per cloud: s_begin = 0)
+  if (ws.means && ntiles == 1) {
+    float* mo = ws.means + ((size_t)b * c + c0) * ws.ms;
+    for (int g = 0; g < gcount; g++) {
+      for (int si = tid; si < S; si += NT) mo[(size_t)g * ws.ms + si] = mean_s[(size_t)g * ns + si];
+      if (tid == 0) mo[(size_t)g * ws.ms + n] = 0.0f;  // the empty-cell slot
+    }
+    if (grp == 0)
+      for (int si = tid; si < S; si += NT)
+        ws.segcnt[(size_t)b * ws.ms + si] = (unsigned short)scnt_s[si];
+  }
   // stream the [gcount, cell0..cell1) slab once; zeros included
   float* ob = out + ((size_t)b * c + c0) * r3;
   int* cb = (cnt_out && grp == 0) ? cnt_out + (size_t)b * r3 : nullptr;
@@ -676,6 +701,248 @@ __global__ __launch_bounds__(NT) void vox_grid_kernel(
     }
   }
   PCR_STAMP(12);
+  }
+}
+
+// ------------------------------------------------------- streaming kernel
+// The dense [B, C, r^3] grid + cnt from the compact voxel means that the
+// means / devox launch left in ws.means ([b][c][ms], one row per channel,
+// occupied segments in voxel order, slot n = 0) and prep's occupancy bitmap.
+// Small and persistent: per cloud a few workgroups, each a contiguous range
+// of channel-pair items; ~35 KB of LDS and five waves, so the KNN
+// selection's two workgroups fit on the same CU and run beside it (a dense
+// write stream needs few waves; vox_grid_kernel's per-item setup is what
+// made it occupy whole CUs).
+//  - streamer waves (NS) only read LDS and store: they never wait on vmcnt,
+//    so their stores stay in flight across items;
+//  - the loader wave only loads: bitmap, word prefix and counts once, then
+//    the means of item t+2 by LDS-DMA (global_load_lds_dwordx4) into the
+//    third buffer while the streamers store item t.  Under the write stream
+//    a load round trip takes microseconds; with two items of slack it never
+//    holds a barrier.  The barriers wait for LDS operations only.
+constexpr int kStreamG = 2;      // channels per item
+constexpr int kStreamNG = 9;     // 1 KB LDS-DMA pieces per item: two rows of ms <= 1152 floats
+constexpr int kStreamNB = 3;     // means buffers (item t streams, t+1 ready, t+2 landing)
+constexpr int kStreamMaxN = 1024;
+constexpr int kStreamMaxW = 1024;  // occupancy words (r^3 <= 32768)
+
+typedef __attribute__((address_space(3))) void* lds_void_p;
+typedef __attribute__((address_space(1))) void* gbl_void_p;
+
+// s_waitcnt vmcnt(N) only (gfx9 encoding: expcnt / lgkmcnt at their maxima)
+template <int N>
+__device__ inline void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+// workgroup barrier after this wave's LDS operations (lgkmcnt(0)); outstanding
+// stores and LDS-DMA loads stay in flight
+__device__ inline void lds_only_barrier() {
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_s_barrier();
+}
+
+template <int NS, int NB>
+__global__ __launch_bounds__((NS + 1) * 64) void vox_stream_kernel(int c, int n, int r3, VoxWs ws,
+                                                                  float* __restrict__ out,
+                                                                  int* __restrict__ cnt_out,
+                                                                  int ngrp, int wpc, int per,
+                                                                  int dbg) {
+  constexpr int G = kStreamG, NG = kStreamNG;
+  constexpr int D = NB - 1;     // prefetch distance in items
+  constexpr int NTS = NS * 64;  // streamer threads
+  constexpr int BUFB = NG * 1024;
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  const int W = ws.W;
+  const int ms = ws.ms;
+  float* mean_s = (float*)smem_raw;                                // [NB][BUFB / 4]
+  unsigned* bm_s = (unsigned*)(smem_raw + NB * BUFB);              // [W]
+  unsigned short* pre_s = (unsigned short*)(bm_s + W);             // [W]
+  unsigned short* scnt_s = pre_s + W;                              // [ms], slot n = 0
+  const int b = blockIdx.x / wpc;
+  const int j0 = (blockIdx.x % wpc) * per;
+  const int nit = min(ngrp, j0 + per) - j0;
+  if (nit <= 0) return;  // uniform over the workgroup
+  const int tid = threadIdx.x;
+  const int lt = tid & 63;
+  PCR_STAMP(0);
+
+  if (tid >= NTS) {
+    // ---- loader wave
+    // item j (channel pair) of this cloud into means buffer `buf`: NG whole
+    // 1 KB pieces (the two rows are adjacent; the tail past them is unused)
+    auto issue = [&](int j, int buf) {
+      if (dbg & 2) return;
+      const char* src = (const char*)(ws.means + ((size_t)b * c + (size_t)j * G) * ms);
+      char* dst = (char*)smem_raw + buf * BUFB;
+#pragma unroll
+      for (int p = 0; p < NG; p++)
+        __builtin_amdgcn_global_load_lds((gbl_void_p)(src + p * 1024 + lt * 16),
+                                         (lds_void_p)(dst + p * 1024), 16, 0, 0);
+    };
+    // every load of the prologue in flight at once: the first two items'
+    // means, the bitmap, the segment counts and nseg
+#pragma unroll
+    for (int q = 0; q < D; q++)
+      if (q < nit) issue(j0 + q, q);
+    if (!(dbg & 2)) {
+      const unsigned* gbm = ws.bitmap + (size_t)b * W;
+      unsigned v[kStreamMaxW / 64];
+#pragma unroll
+      for (int q = 0; q < kStreamMaxW / 64; q++) {
+        const int w = q * 64 + lt;
+        v[q] = w < W ? gbm[w] : 0u;
+      }
+      const unsigned short* gsc = ws.segcnt + (size_t)b * ms;
+      constexpr int kSc = (kStreamMaxN + 1 + 3 + 63) / 64 + 1;
+      unsigned short t[kSc];
+#pragma unroll
+      for (int q = 0; q < kSc; q++) {
+        const int s2 = q * 64 + lt;
+        t[q] = s2 < ms ? gsc[s2] : (unsigned short)0;
+      }
+      const int nseg = ws.nseg[b];
+      int carry = 0;
+#pragma unroll
+      for (int q = 0; q < kStreamMaxW / 64; q++) {
+        const int w = q * 64 + lt;
+        const int pc = __popc(v[q]);
+        int incl = pc;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+          const int o = __shfl_up(incl, off, kWave);
+          if (lt >= off) incl += o;
+        }
+        if (w < W) {
+          bm_s[w] = v[q];
+          pre_s[w] = (unsigned short)(carry + incl - pc);
+        }
+        carry += __shfl(incl, 63, kWave);
+      }
+#pragma unroll
+      for (int q = 0; q < kSc; q++) {
+        const int s2 = q * 64 + lt;
+        if (s2 < ms) scnt_s[s2] = s2 < nseg ? t[q] : (unsigned short)0;  // slot n = 0
+      }
+    }
+    wait_vmcnt<0>();  // the plain loads above already waited; keeps it simple
+    lds_only_barrier();
+    for (int it = 0; it < nit; it++) {
+      // buffer (it + D) % NB held item it - 1, released by the last barrier;
+      // item it + 1 must have landed before the streamers start it
+      if (it + D < nit) {
+        issue(j0 + it + D, (it + D) % NB);
+        wait_vmcnt<NG * (D - 1)>();
+      } else {
+        wait_vmcnt<0>();
+      }
+      lds_only_barrier();
+    }
+    return;
+  }
+
+  // ---- streamer waves
+  // U streaming iterations at once, branch-free: every LDS read of the U
+  // groups of 4 consecutive cells (occupancy word + prefix, then the means /
+  // counts, slot n = 0 for empty cells) is issued before any is waited on;
+  // one 16-byte store per channel (+ cnt) and group
+  constexpr int U = 4;
+  auto stream_u = [&](int base0, float* ob, int g_lo, int gcount, const float* ms0, int* cb) {
+    if (dbg & 1) {  // diagnostic: zeros only, no LDS reads
+      const float4 z = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int base = base0 + u * NTS * 4;
+        if (base < r3)
+#pragma unroll
+          for (int g = 0; g < G; g++)
+            if (g >= g_lo && g < gcount) *(float4*)(ob + (size_t)g * r3 + base) = z;
+      }
+      return;
+    }
+    unsigned word[U];
+    int pw[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int base = min(base0 + u * NTS * 4, r3 - 4);
+      word[u] = bm_s[base >> 5];
+      pw[u] = pre_s[base >> 5];
+    }
+    int ix[U][4];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int sh = (base0 + u * NTS * 4) & 31;
+      const unsigned nib = (word[u] >> sh) & 15u;
+      const int pre = pw[u] + __popc(word[u] & ((1u << sh) - 1u));
+      ix[u][0] = (nib & 1u) ? pre : n;
+      ix[u][1] = (nib & 2u) ? pre + (int)(nib & 1u) : n;
+      ix[u][2] = (nib & 4u) ? pre + __popc(nib & 3u) : n;
+      ix[u][3] = (nib & 8u) ? pre + __popc(nib & 7u) : n;
+    }
+    float4 v[U][G];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+      for (int g = 0; g < G; g++) {
+        if (g >= g_lo && g < gcount) {
+          const float* ms_g = ms0 + (size_t)g * ms;
+          v[u][g] = float4{ms_g[ix[u][0]], ms_g[ix[u][1]], ms_g[ix[u][2]], ms_g[ix[u][3]]};
+        }
+      }
+#pragma unroll
+    for (int g = 0; g < G; g++) {
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int base = base0 + u * NTS * 4;
+        if (base < r3 && g >= g_lo && g < gcount) *(float4*)(ob + (size_t)g * r3 + base) = v[u][g];
+      }
+    }
+    if (cb) {
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int base = base0 + u * NTS * 4;
+        const int4 cv = {scnt_s[ix[u][0]], scnt_s[ix[u][1]], scnt_s[ix[u][2]], scnt_s[ix[u][3]]};
+        if (base < r3) *(int4*)(cb + base) = cv;
+      }
+    }
+  };
+  lds_only_barrier();
+  PCR_STAMP(1);
+  // the sweep starts at a workgroup-dependent step of the item and wraps, so
+  // the workgroups do not all hit the same HBM channels at once
+  const int nstep = (r3 + NTS * 4 * U - 1) / (NTS * 4 * U);
+  const int rot = (dbg & 4) ? 0 : (int)(blockIdx.x % nstep);
+  for (int it = 0; it < nit; it++) {
+    const int j = j0 + it;
+    const int c0 = j * G;
+    const int gcount = min(G, c - c0);
+    float* ob = out + ((size_t)b * c + c0) * r3;
+    int* cb = (cnt_out && j == 0) ? cnt_out + (size_t)b * r3 : nullptr;
+    const float* ms0 = mean_s + (size_t)(it % NB) * (BUFB / 4);
+    if (dbg & 8) {
+      // one row at a time: the item's two rows are one contiguous 2 r^3 sweep
+      for (int g = 0; g < gcount; g++)
+        for (int st = 0; st < nstep; st++) {
+          const int sp = st + rot < nstep ? st + rot : st + rot - nstep;
+          stream_u(sp * NTS * 4 * U + tid * 4, ob, g, g + 1, ms0, g == 0 ? cb : nullptr);
+        }
+    } else {
+      for (int st = 0; st < nstep; st++) {
+        const int sp = st + rot < nstep ? st + rot : st + rot - nstep;
+        stream_u(sp * NTS * 4 * U + tid * 4, ob, 0, gcount, ms0, cb);
+      }
+    }
+    if (it < 4) PCR_STAMP(2 + it);
+    lds_only_barrier();
+    if (it < 4) PCR_STAMP(8 + it);
+  }
+}
+
+// workgroups of a grid launch: every item its own workgroup unless
+// PCR_GRID_WGS caps the count (then each loops over several items)
+static int grid_wgs(int nitems) {
+  static const int cap = getenv("PCR_GRID_WGS") ? atoi(getenv("PCR_GRID_WGS")) : 0;
+  return cap > 0 && cap < nitems ? cap : nitems;
 }
 
 // ------------------------------------------------------ backward gather
@@ -928,15 +1195,24 @@ static pcr_status run_voxelize(const float* features, const float* coords_f, con
     const int npad = next_pow2(n < nt ? nt : n);
     size_t prep_smem = (size_t)npad * 8 + (size_t)ws.W * 8 + (size_t)n * 8;
     PCR_REQUIRE(prep_smem <= 150 * 1024, "%s: prep LDS %zu too large", name, prep_smem);
-    if (small) {
+    static const int exp_nt = getenv("PCR_PREP_NT") ? atoi(getenv("PCR_PREP_NT")) : 256;
+    if (small && exp_nt == 512 && n > 256) {
+      const int npad5 = next_pow2(n < 512 ? 512 : n);
+      const size_t sm5 = (size_t)npad5 * 8 + (size_t)ws.W * 8 + (size_t)n * 8;
+      allow_big_lds(vox_prep_kernel<MODE, 512>, sm5);
+      hipLaunchKernelGGL((vox_prep_kernel<MODE, 512>), dim3(b), dim3(512), sm5, stream, coords_f,
+                         coords_i, n, r, npad5, norm_out, ind, ws, dinds, dwgts);
+    } else if (small && exp_nt != 1024) {
       allow_big_lds(vox_prep_kernel<MODE, kSmallPrepThreads>, prep_smem);
       hipLaunchKernelGGL((vox_prep_kernel<MODE, kSmallPrepThreads>), dim3(b),
                          dim3(kSmallPrepThreads), prep_smem, stream, coords_f, coords_i, n, r,
                          npad, norm_out, ind, ws, dinds, dwgts);
     } else {
-      allow_big_lds(vox_prep_kernel<MODE, kPrepThreads>, prep_smem);
+      const int npad1 = next_pow2(n < kPrepThreads ? kPrepThreads : n);
+      const size_t sm1 = (size_t)npad1 * 8 + (size_t)ws.W * 8 + (size_t)n * 8;
+      allow_big_lds(vox_prep_kernel<MODE, kPrepThreads>, sm1);
       hipLaunchKernelGGL((vox_prep_kernel<MODE, kPrepThreads>), dim3(b), dim3(kPrepThreads),
-                         prep_smem, stream, coords_f, coords_i, n, r, npad, norm_out, ind, ws,
+                         sm1, stream, coords_f, coords_i, n, r, npad1, norm_out, ind, ws,
                          dinds, dwgts);
     }
   }
@@ -959,18 +1235,18 @@ static pcr_status run_voxelize(const float* features, const float* coords_f, con
     const size_t smem = grid_smem_bytes(G, n, nw);
     PCR_REQUIRE(smem <= 150 * 1024, "%s: grid LDS %zu too large", name, smem);
     allow_big_lds(vox_grid_kernel<3, kGridThreads, 2>, smem);
-    hipLaunchKernelGGL((vox_grid_kernel<3, kGridThreads, 2>), dim3(1, ngrp, b), dim3(kGridThreads),
-                       smem, stream, features, c, n, r3, G, tile, ws, out, cnt, dinds, dwgts,
-                       devox, desc);
+    hipLaunchKernelGGL((vox_grid_kernel<3, kGridThreads, 2>), dim3(grid_wgs(ngrp * b)),
+                       dim3(kGridThreads), smem, stream, features, c, n, r3, G, tile, ws, out, cnt,
+                       dinds, dwgts, devox, desc, 1, ngrp, ngrp * b);
   } else if (do_dev) {
     int G = 1;
     const int ngrp = pick_groups(c, n, 4, &G);
     const size_t smem = grid_smem_bytes(G, n, nw);
     PCR_REQUIRE(smem <= 150 * 1024, "%s: grid LDS %zu too large", name, smem);
     allow_big_lds(vox_grid_kernel<2, kDevoxThreads, 4>, smem);
-    hipLaunchKernelGGL((vox_grid_kernel<2, kDevoxThreads, 4>), dim3(1, ngrp, b),
+    hipLaunchKernelGGL((vox_grid_kernel<2, kDevoxThreads, 4>), dim3(ngrp * b),
                        dim3(kDevoxThreads), smem, stream, features, c, n, r3, G, tile, ws, nullptr,
-                       nullptr, dinds, dwgts, devox, desc);
+                       nullptr, dinds, dwgts, devox, desc, 1, ngrp, ngrp * b);
   } else if (do_grid && (c > 0 || cnt)) {
     // streaming part: two channels per workgroup keep its LDS small (~29 KB
     // at n = 1024), so its workgroups fit beside the KNN selection's
@@ -979,9 +1255,10 @@ static pcr_status run_voxelize(const float* features, const float* coords_f, con
     const size_t smem = grid_smem_bytes(G, n, nw);
     PCR_REQUIRE(smem <= 150 * 1024, "%s: grid LDS %zu too large", name, smem);
     allow_big_lds(vox_grid_kernel<1, kGridThreads, 2>, smem);
-    hipLaunchKernelGGL((vox_grid_kernel<1, kGridThreads, 2>), dim3(ntiles, ngrp, b),
-                       dim3(kGridThreads), smem, stream, features, c, n, r3, G, tile, ws, out, cnt,
-                       nullptr, nullptr, nullptr, nullptr);
+    hipLaunchKernelGGL((vox_grid_kernel<1, kGridThreads, 2>),
+                       dim3(grid_wgs(ntiles * ngrp * b)), dim3(kGridThreads), smem, stream,
+                       features, c, n, r3, G, tile, ws, out, cnt, nullptr, nullptr, nullptr,
+                       nullptr, ntiles, ngrp, ntiles * ngrp * b);
   }
   return launch_status(name);
 }
@@ -1040,8 +1317,113 @@ extern "C" pcr_status pcr_spherical_normalize(const float* coords, int b, int n,
 }
 
 extern "C" size_t pcr_extractor_workspace_size(int b, int n, int c, int r) {
-  (void)c;
-  return pcr_voxelize_workspace_size(b, n, r);
+  if (b <= 0 || n <= 0 || r <= 0) return 256;
+  return vox_ws_layout(b, n, r, nullptr, nullptr, c > 0 ? c : 0);
+}
+
+// The extractor's voxel stage as prep -> means/devox -> stream (the split
+// that lets the dense grid stream beside the KNN selection):
+static pcr_status extractor_ws(int b, int c, int n, int r, void* workspace, size_t ws_bytes,
+                               VoxWs* ws, const char* name) {
+  PCR_REQUIRE(b >= 0 && c >= 1 && n >= 1 && n <= kMaxSortN && r >= 1,
+              "%s: invalid sizes b=%d c=%d n=%d r=%d", name, b, c, n, r);
+  const int64_t r3 = (int64_t)r * r * r;
+  PCR_REQUIRE(r3 <= 65536 && r3 % 4 == 0, "%s: resolution %d unsupported (r^3 <= 65536, r^3 %% 4 == 0)",
+              name, r);
+  const size_t need = vox_ws_layout(b, n, r, ws, workspace, c);
+  PCR_REQUIRE(workspace != nullptr && ws_bytes >= need, "%s: workspace too small (%zu < %zu)",
+              name, ws_bytes, need);
+  return PCR_OK;
+}
+
+extern "C" pcr_status pcr_extractor_voxel_means_devox(const float* features, int b, int c, int n,
+                                                      int r, float* devox, const int* dinds,
+                                                      const float* dwgts, float* desc,
+                                                      void* workspace, size_t workspace_bytes,
+                                                      void* stream) {
+  const char* name = "extractor_voxel_means_devox";
+  VoxWs ws;
+  pcr_status rc = extractor_ws(b, c, n, r, workspace, workspace_bytes, &ws, name);
+  if (rc != PCR_OK) return rc;
+  PCR_REQUIRE(devox != nullptr && dinds != nullptr && dwgts != nullptr,
+              "%s: devox, dinds, dwgts required", name);
+  if (b == 0) return PCR_OK;
+  const int r3 = r * r * r;
+  const int tile = ((r3 + 31) / 32) * 32;
+  const int nw = tile / 32 + 1;
+  static const int mv = getenv("PCR_MEANS_V") ? atoi(getenv("PCR_MEANS_V")) : 0;
+  int G = 1;
+  const int ngrp = pick_groups(c, n, mv == 0 ? 4 : 2, &G);
+  const size_t smem = grid_smem_bytes(G, n, nw);
+  PCR_REQUIRE(smem <= 150 * 1024, "%s: LDS %zu too large", name, smem);
+  if (mv == 0) {
+    allow_big_lds(vox_grid_kernel<2, kDevoxThreads, 4>, smem);
+    hipLaunchKernelGGL((vox_grid_kernel<2, kDevoxThreads, 4>), dim3(ngrp * b), dim3(kDevoxThreads),
+                       smem, as_stream(stream), features, c, n, r3, G, tile, ws, nullptr, nullptr,
+                       dinds, dwgts, devox, desc, 1, ngrp, ngrp * b);
+  } else if (mv == 1) {
+    allow_big_lds(vox_grid_kernel<2, 256, 2>, smem);
+    hipLaunchKernelGGL((vox_grid_kernel<2, 256, 2>), dim3(ngrp * b), dim3(256), smem,
+                       as_stream(stream), features, c, n, r3, G, tile, ws, nullptr, nullptr, dinds,
+                       dwgts, devox, desc, 1, ngrp, ngrp * b);
+  } else {
+    allow_big_lds(vox_grid_kernel<2, 512, 2>, smem);
+    hipLaunchKernelGGL((vox_grid_kernel<2, 512, 2>), dim3(ngrp * b), dim3(512), smem,
+                       as_stream(stream), features, c, n, r3, G, tile, ws, nullptr, nullptr, dinds,
+                       dwgts, devox, desc, 1, ngrp, ngrp * b);
+  }
+  return launch_status(name);
+}
+
+static int device_cus() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+  }
+  return cus;
+}
+
+extern "C" pcr_status pcr_extractor_voxel_stream(int b, int c, int n, int r, int* cnt,
+                                                 float* grid, void* workspace,
+                                                 size_t workspace_bytes, void* stream) {
+  const char* name = "extractor_voxel_stream";
+  VoxWs ws;
+  pcr_status rc = extractor_ws(b, c, n, r, workspace, workspace_bytes, &ws, name);
+  if (rc != PCR_OK) return rc;
+  PCR_REQUIRE(grid != nullptr, "%s: grid required", name);
+  if (b == 0) return PCR_OK;
+  const int r3 = r * r * r;
+  PCR_REQUIRE(n <= kStreamMaxN && r3 <= 32 * kStreamMaxW && r3 % 128 == 0,
+              "%s: n=%d r=%d unsupported (n <= %d, r^3 <= %d, r^3 %% 128 == 0)", name, n, r,
+              kStreamMaxN, 32 * kStreamMaxW);
+  PCR_REQUIRE(2 * ws.ms * 4 <= kStreamNG * 1024, "%s: means rows too long", name);
+  const int ngrp = ceil_div(c, kStreamG);
+  // a few workgroups per cloud (about one per CU in all), each a contiguous
+  // range of channel-pair items of that cloud
+  static const int cap = getenv("PCR_STREAM_WGS") ? atoi(getenv("PCR_STREAM_WGS")) : 0;
+  const int total = cap > 0 ? cap : device_cus();
+  int wpc = total / (b > 0 ? b : 1);
+  if (wpc < 1) wpc = 1;
+  if (wpc > ngrp) wpc = ngrp;
+  const int per = ceil_div(ngrp, wpc);
+  static const int dbg = getenv("PCR_STREAM_DBG") ? atoi(getenv("PCR_STREAM_DBG")) : 0;
+  static const int nb = getenv("PCR_STREAM_NB") ? atoi(getenv("PCR_STREAM_NB")) : kStreamNB;
+  const size_t smem = (size_t)nb * kStreamNG * 1024 + (size_t)ws.W * 6 +
+                      ((size_t)ws.ms * 2 + 15) / 16 * 16;
+  if (nb == 2) {
+    allow_big_lds(vox_stream_kernel<4, 2>, smem);
+    hipLaunchKernelGGL((vox_stream_kernel<4, 2>), dim3(b * wpc), dim3(5 * 64), smem,
+                       as_stream(stream), c, n, r3, ws, grid, cnt, ngrp, wpc, per, dbg);
+  } else {
+    allow_big_lds(vox_stream_kernel<4, kStreamNB>, smem);
+    hipLaunchKernelGGL((vox_stream_kernel<4, kStreamNB>), dim3(b * wpc), dim3(5 * 64), smem,
+                       as_stream(stream), c, n, r3, ws, grid, cnt, ngrp, wpc, per, dbg);
+  }
+  return launch_status(name);
 }
 
 extern "C" pcr_status pcr_extractor_voxel_prep(const float* xyz, int b, int n, int r,

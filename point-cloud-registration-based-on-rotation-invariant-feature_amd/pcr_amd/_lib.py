@@ -48,6 +48,8 @@ SIGNATURES = {
     "pcr_extractor_voxel_grid": (ST, [P, I, I, I, I, P, P, P, SZ, P]),
     "pcr_extractor_voxel_devox": (ST, [P, I, I, I, I, P, P, P, P, P, SZ, P]),
     "pcr_extractor_voxel_grid_devox": (ST, [P, I, I, I, I, P, P, P, P, P, P, P, SZ, P]),
+    "pcr_extractor_voxel_means_devox": (ST, [P, I, I, I, I, P, P, P, P, P, SZ, P]),
+    "pcr_extractor_voxel_stream": (ST, [I, I, I, I, P, P, P, SZ, P]),
     "pcr_selftest_math": (ST, [I, P, P, I, I, P, P, P]),
     "pcr_selftest_math_d": (ST, [I, P, P, I, P, P]),
 }

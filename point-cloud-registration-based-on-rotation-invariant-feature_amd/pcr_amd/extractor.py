@@ -67,10 +67,11 @@ class SphExtractor:
     # front stages while step i's back stages still read set i % 2.
     def _set(self, slot):
         if slot == 0:
-            return self.knn_ws, self.ws, self.dinds, self.dwgts
+            return self.knn_ws, self.ws, self.dinds, self.dwgts, self.knn_idx
         if self._set1 is None:
             e = torch.empty_like
-            self._set1 = (e(self.knn_ws), e(self.ws), e(self.dinds), e(self.dwgts))
+            self._set1 = (e(self.knn_ws), e(self.ws), e(self.dinds), e(self.dwgts),
+                          e(self.knn_idx))
         return self._set1
 
     def neighbor_stage(self, xyz, normals, stream):
@@ -91,23 +92,24 @@ class SphExtractor:
         _lib.check(rc, "knn_prepare")
         return True
 
-    def knn_select(self, xyz, normals, stream, slot=0, sorted_ok=True):
-        kws = self._set(slot)[0]
+    def knn_select(self, xyz, normals, stream, slot=0, sorted_ok=True, ppf=True):
+        """Selection (+ local PPF unless ppf=False) into index set `slot`."""
+        kws, idx = self._set(slot)[0], self._set(slot)[4]
         if not sorted_ok:
             _lib.check(_lib.load().pcr_knn_local_ppf(
                 _ptr(xyz), _ptr(normals), self.b, self.n, self.k, int(self.relative),
-                _ptr(self.knn_idx), _ptr(self.knn_dist), _ptr(self.local_ppf), _ptr(kws),
+                _ptr(idx), _ptr(self.knn_dist), _ptr(self.local_ppf), _ptr(kws),
                 kws.numel(), stream), "knn_local_ppf")
             return
         lib = _lib.load()
         _lib.check(lib.pcr_knn_local_ppf_prepared(
             _ptr(xyz), _ptr(normals), self.b, self.n, self.k, int(self.relative),
-            _ptr(self.knn_idx), _ptr(self.knn_dist), None if self.split_ppf else
+            _ptr(idx), _ptr(self.knn_dist), None if self.split_ppf else
             _ptr(self.local_ppf), _ptr(kws), kws.numel(), stream), "knn_local_ppf_prepared")
-        if self.split_ppf:
+        if self.split_ppf and ppf:
             # PPF as its own launch: one thread per (slot, point), coalesced
             _lib.check(lib.pcr_local_ppf_forward(
-                _ptr(xyz), _ptr(normals), _ptr(xyz), _ptr(normals), _ptr(self.knn_idx), self.b,
+                _ptr(xyz), _ptr(normals), _ptr(xyz), _ptr(normals), _ptr(idx), self.b,
                 self.n, self.n, self.k, 1, int(self.relative), _ptr(self.local_ppf), stream),
                 "local_ppf_forward")
 
@@ -121,7 +123,7 @@ class SphExtractor:
             "extractor_voxel_stage")
 
     def voxel_prep(self, xyz, stream, slot=0):
-        _, ws, dinds, dwgts = self._set(slot)
+        _, ws, dinds, dwgts, _ = self._set(slot)
         _lib.check(_lib.load().pcr_extractor_voxel_prep(
             _ptr(xyz), self.b, self.n, self.r, _ptr(self.norm_coords), _ptr(self.ind),
             _ptr(dinds), _ptr(dwgts), _ptr(ws), ws.numel(), stream), "extractor_voxel_prep")
@@ -133,17 +135,35 @@ class SphExtractor:
             _ptr(features), self.b, self.c, self.n, self.r, _ptr(self.cnt), _ptr(self.grid),
             _ptr(ws), ws.numel(), stream), "extractor_voxel_grid")
 
-    def voxel_grid_devox(self, features, stream, desc=None):
+    def voxel_grid_devox(self, features, stream, desc=None, slot=0):
         """The dominant kernel of the default step (vox_grid_kernel<3>: dense
         grid + cnt, devox + descriptor from the same LDS means)."""
+        _, ws, dinds, dwgts, _ = self._set(slot)
         d = self.desc if desc is None else desc
         _lib.check(_lib.load().pcr_extractor_voxel_grid_devox(
             _ptr(features), self.b, self.c, self.n, self.r, _ptr(self.cnt), _ptr(self.grid),
-            _ptr(self.devox), _ptr(self.dinds), _ptr(self.dwgts), _ptr(d), _ptr(self.ws),
-            self.ws.numel(), stream), "extractor_voxel_grid_devox")
+            _ptr(self.devox), _ptr(dinds), _ptr(dwgts), _ptr(d), _ptr(ws),
+            ws.numel(), stream), "extractor_voxel_grid_devox")
+
+    def voxel_means_devox(self, features, stream, desc=None, slot=0):
+        """Voxel means of the occupied segments into the workspace + devox +
+        descriptor (the first half of the split voxel stage)."""
+        _, ws, dinds, dwgts, _ = self._set(slot)
+        d = self.desc if desc is None else desc
+        _lib.check(_lib.load().pcr_extractor_voxel_means_devox(
+            _ptr(features), self.b, self.c, self.n, self.r, _ptr(self.devox), _ptr(dinds),
+            _ptr(dwgts), _ptr(d), _ptr(ws), ws.numel(), stream), "extractor_voxel_means_devox")
+
+    def voxel_stream(self, stream, slot=0):
+        """The dense grid + cnt from the workspace means (the dominant,
+        HBM-bound kernel of the split voxel stage)."""
+        ws = self._set(slot)[1]
+        _lib.check(_lib.load().pcr_extractor_voxel_stream(
+            self.b, self.c, self.n, self.r, _ptr(self.cnt), _ptr(self.grid), _ptr(ws),
+            ws.numel(), stream), "extractor_voxel_stream")
 
     def voxel_devox(self, features, stream, desc=None, slot=0):
-        _, ws, dinds, dwgts = self._set(slot)
+        _, ws, dinds, dwgts, _ = self._set(slot)
         d = self.desc if desc is None else desc
         _lib.check(_lib.load().pcr_extractor_voxel_devox(
             _ptr(features), self.b, self.c, self.n, self.r, _ptr(self.devox), _ptr(dinds),
@@ -211,10 +231,11 @@ class SphExtractor:
         self._join(cur)
         return self.outputs()
 
-    def outputs(self, slot=0):
-        _, _, dinds, dwgts = self._set(slot)
+    def outputs(self, slot=0, idx_slot=0):
+        _, _, dinds, dwgts, _ = self._set(slot)
         return {
-            "knn_idx": self.knn_idx, "local_ppf": self.local_ppf, "norm_coords": self.norm_coords,
+            "knn_idx": self._set(idx_slot)[4], "local_ppf": self.local_ppf,
+            "norm_coords": self.norm_coords,
             "ind": self.ind, "cnt": self.cnt, "grid": self.grid, "devox": self.devox,
             "dinds": dinds, "dwgts": dwgts, "desc": self.desc,
         }
@@ -305,6 +326,120 @@ class SphExtractor:
                 sel_done[slot].record(self.s_nbr)
             self._join(cur)
             return self.outputs()
+        if mode == "two_stream":
+            # s_nbr: sort + select + PPF; s_vox: prep, means / devox /
+            # descriptor, then the small persistent grid-streaming kernel
+            # (it leaves room on every CU for the selection beside it)
+            sn, sv = self.s_nbr.cuda_stream, self.s_vox.cuda_stream
+            for s in range(steps):
+                d = None if desc_steps is None else desc_steps[s]
+                ok = self.knn_sort(xyz, sn)
+                self.knn_select(xyz, normals, sn, 0, ok)
+                self.voxel_prep(xyz, sv)
+                self.voxel_means_devox(features, sv, d)
+                self.voxel_stream(sv)
+            self._join(cur)
+            return self.outputs()
+        if mode == "three_stream":
+            # s_nbr: sort + select + PPF; s_pre: prep + means / devox /
+            # descriptor of step s into workspace set s % 2 (after the grid
+            # stream of step s-2 read it); s_vox: the grid stream of step s
+            sn = self.s_nbr.cuda_stream
+            stream_done = [None, None]
+            for s in range(steps):
+                slot = s & 1
+                d = None if desc_steps is None else desc_steps[s]
+                if stream_done[slot] is not None:
+                    self.s_pre.wait_event(stream_done[slot])
+                self.voxel_prep(xyz, self.s_pre.cuda_stream, slot)
+                self.voxel_means_devox(features, self.s_pre.cuda_stream, d, slot)
+                e_m = torch.cuda.Event()
+                e_m.record(self.s_pre)
+                self.s_vox.wait_event(e_m)
+                self.voxel_stream(self.s_vox.cuda_stream, slot)
+                stream_done[slot] = torch.cuda.Event()
+                stream_done[slot].record(self.s_vox)
+                ok = self.knn_sort(xyz, sn)
+                self.knn_select(xyz, normals, sn, 0, ok)
+            self._join(cur)
+            return self.outputs(slot=(steps - 1) & 1)
+        if mode == "three_split":
+            # s_nbr: sort + select + PPF of every step; s_pre: voxel prep of
+            # step s into set s % 2 (after step s-2's grid kernel read it);
+            # s_vox: fused grid / devox / descriptor kernel after its prep
+            sn = self.s_nbr.cuda_stream
+            grid_done = [None, None]
+            for s in range(steps):
+                slot = s & 1
+                d = None if desc_steps is None else desc_steps[s]
+                if grid_done[slot] is not None:
+                    self.s_pre.wait_event(grid_done[slot])
+                self.voxel_prep(xyz, self.s_pre.cuda_stream, slot)
+                e_prep = torch.cuda.Event()
+                e_prep.record(self.s_pre)
+                self.s_vox.wait_event(e_prep)
+                self.voxel_grid_devox(features, self.s_vox.cuda_stream, d, slot)
+                grid_done[slot] = torch.cuda.Event()
+                grid_done[slot].record(self.s_vox)
+                ok = self.knn_sort(xyz, sn)
+                self.knn_select(xyz, normals, sn, 0, ok)
+            self._join(cur)
+            return self.outputs(slot=(steps - 1) & 1)
+        if mode == "four_split":
+            # s_pre: Morton sort of step s+1, then local PPF of step s (after
+            # its selection); s_nbr: selections back to back; s_dev: voxel
+            # prep; s_vox: fused grid / devox / descriptor kernel.  KNN
+            # workspace, KNN indices and voxel workspace / corners alternate
+            # between two sets; a set is rewritten only after step s-2's
+            # readers of it are done.
+            sa, sb = self.s_pre, self.s_nbr
+            sc, sd = self.s_dev, self.s_vox
+            lib = _lib.load()
+            ok = [None, None]
+            e_sort = [None, None]
+            ppf_done, sel_done, grid_done = [None, None], [None, None], [None, None]
+
+            def ev(st):
+                e_ = torch.cuda.Event()
+                e_.record(st)
+                return e_
+
+            def sort(s):
+                slot = s & 1
+                if sel_done[slot] is not None:
+                    sa.wait_event(sel_done[slot])
+                ok[slot] = self.knn_sort(xyz, sa.cuda_stream, slot)
+                e_sort[slot] = ev(sa)
+
+            sort(0)
+            for s in range(steps):
+                slot = s & 1
+                d = None if desc_steps is None else desc_steps[s]
+                # voxel side
+                if grid_done[slot] is not None:
+                    sc.wait_event(grid_done[slot])
+                self.voxel_prep(xyz, sc.cuda_stream, slot)
+                sd.wait_event(ev(sc))
+                self.voxel_grid_devox(features, sd.cuda_stream, d, slot)
+                grid_done[slot] = ev(sd)
+                # neighbour side
+                sb.wait_event(e_sort[slot])
+                if ppf_done[slot] is not None:
+                    sb.wait_event(ppf_done[slot])
+                self.knn_select(xyz, normals, sb.cuda_stream, slot, ok[slot], ppf=False)
+                sel_done[slot] = ev(sb)
+                if s + 1 < steps:
+                    sort(s + 1)
+                sa.wait_event(sel_done[slot])
+                idx = self._set(slot)[4]
+                _lib.check(lib.pcr_local_ppf_forward(
+                    _ptr(xyz), _ptr(normals), _ptr(xyz), _ptr(normals), _ptr(idx), self.b,
+                    self.n, self.n, self.k, 1, int(self.relative), _ptr(self.local_ppf),
+                    sa.cuda_stream), "local_ppf_forward")
+                ppf_done[slot] = ev(sa)
+            self._join(cur)
+            last = (steps - 1) & 1
+            return self.outputs(slot=last, idx_slot=last)
         if mode == "two_fused":
             # voxel stream: prep, then one kernel for grid + devox + descriptor
             sn, sv = self.s_nbr.cuda_stream, self.s_vox.cuda_stream

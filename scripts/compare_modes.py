@@ -28,19 +28,20 @@ prio = {"hi_knn": (torch.cuda.Stream(device=dev, priority=-1), plain[1]),
 res = {m: [] for m in modes}
 for rnd in range(3):
     for m in modes:
-        mm = m
+        mm, S = (m.split(":") + ["10"])[:2]
+        S = int(S)
         ex.s_nbr, ex.s_vox = plain
         if m in prio:
             ex.s_nbr, ex.s_vox = prio[m]
             mm = "two_fused"
         for _ in range(2):
-            ex.run_pipelined(xyz, nrm, feat, 10, mode=mm)
+            ex.run_pipelined(xyz, nrm, feat, S, mode=mm)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(20):
-            ex.run_pipelined(xyz, nrm, feat, 10, mode=mm)
+        for _ in range(200 // S):
+            ex.run_pipelined(xyz, nrm, feat, S, mode=mm)
         torch.cuda.synchronize()
-        res[m].append(b * 200 / (time.perf_counter() - t0))
+        res[m].append(b * (200 // S) * S / (time.perf_counter() - t0))
 for m, v in res.items():
     v = sorted(v)
-    print("%-8s median %.0f clouds/s  (min %.0f max %.0f)" % (m, v[1], v[0], v[2]), flush=True)
+    print("%-16s median %.0f clouds/s  (min %.0f max %.0f)" % (m, v[1], v[0], v[2]), flush=True)

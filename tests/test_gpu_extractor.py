@@ -71,7 +71,8 @@ def test_extractor_pipelined_graph(dev):
     tx, tn, tf = T(xyz, dev), T(nrm, dev), T(feat, dev)
     ex = SphExtractor(b, n, c, k, r, device=dev)
     ref = {kk: v.clone() for kk, v in ex.forward(tx, tn, tf).items()}
-    for mode in ("two", "two_dg", "two_fused", "two_sv", "three", "four", "sortvox"):
+    for mode in ("two", "two_dg", "two_fused", "two_sv", "three", "four", "sortvox", "four_split",
+                 "three_split", "two_stream", "three_stream"):
         desc_steps = torch.empty((5, b, c), device=dev)
         for _ in range(2):
             out = ex.run_pipelined(tx, tn, tf, 5, desc_steps, mode=mode)
