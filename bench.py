@@ -49,7 +49,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", choices=("pipelined", "pipelined_split", "pipelined3", "pipelined4",
-                                       "pipelined_sv", "pipelined_fs", "graph", "eager"),
+                                       "pipelined_sv", "pipelined_fs", "pipelined_3s", "pipelined_2s", "graph",
+                                       "eager"),
                     default="pipelined",
                     help="pipelined: S steps on two independent streams (KNN / voxel, fused "
                          "grid+devox kernel) with no join between them; pipelined_split: "
@@ -151,7 +152,8 @@ def main():
                              mode={"pipelined": "two_fused", "pipelined_split": "two",
                                    "pipelined3": "three",
                                    "pipelined4": "four", "pipelined_sv": "sortvox",
-                                   "pipelined_fs": "four_split"}[args.mode])
+                                   "pipelined_fs": "four_split", "pipelined_3s": "three_stream",
+                                   "pipelined_2s": "two_stream"}[args.mode])
             src = desc_steps.view(S * b, c)
         elif args.mode == "graph":
             ex.replay()

@@ -243,6 +243,38 @@ pcr_status pcr_extractor_voxel_means_devox(const float *features, int b, int c, 
 pcr_status pcr_extractor_voxel_stream(int b, int c, int n, int r, int *cnt, float *grid,
                                       void *workspace, size_t workspace_bytes, void *stream);
 
+/* ------------------------------------------------ native step runner ----
+ * `steps` consecutive extractor steps (the pipelined schedule bench.py
+ * measures), enqueued from native code: every launch and cross-stream event
+ * of every step is issued here, so the host enqueue rate never limits the
+ * step rate.  Forked from and joined back into `origin`.
+ *   schedule 0: two streams -- s_nbr: Morton sort, KNN selection, local PPF;
+ *               s_vox: prep + the fused grid / devox / descriptor kernel.
+ *   schedule 1: three streams -- s_nbr as above; s_pre: prep + means / devox
+ *               / descriptor of step s into buffer set s % 2 (after the grid
+ *               stream of step s-2 read it); s_vox: the grid stream of step s.
+ * Buffers with two entries are the alternating sets (schedule 0 uses set 0).
+ * desc_steps: [steps][b][c] per-step descriptors, or NULL (then desc). */
+typedef struct pcr_extractor_args {
+  int b, n, c, k, r, relative;
+  const float *xyz, *normals, *features;  /* [b,3,n], [b,3,n], [b,c,n] */
+  int *knn_idx;                           /* [b,k,n] */
+  float *knn_dist;                        /* [b,k,n] or NULL */
+  float *local_ppf;                       /* [b,4,k,n] */
+  float *norm_coords;                     /* [b,3,n] */
+  int *ind, *cnt;                         /* [b,n], [b,r^3] */
+  float *grid, *devox, *desc;             /* [b,c,r^3], [b,c,n], [b,c] */
+  int *dinds[2];                          /* [b,8,n] */
+  float *dwgts[2];                        /* [b,8,n] */
+  void *knn_ws;                           /* pcr_knn_workspace_size(b, n, n) */
+  size_t knn_ws_bytes;
+  void *vox_ws[2];                        /* pcr_extractor_workspace_size(b, n, c, r) */
+  size_t vox_ws_bytes;
+} pcr_extractor_args;
+pcr_status pcr_extractor_run(const pcr_extractor_args *args, int steps, int schedule,
+                             float *desc_steps, void *origin, void *s_nbr, void *s_pre,
+                             void *s_vox);
+
 /* ------------------------------------------------------ self tests ------
  * Device evaluation of the shared bit-exact math (include/pcr_math.h) for
  * host-vs-device parity tests.  op: 0 acosf, 1 atanf, 2 sqrtf, 3 x/y,

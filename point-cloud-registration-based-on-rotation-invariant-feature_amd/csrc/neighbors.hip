@@ -263,6 +263,69 @@ __global__ __launch_bounds__(256) void local_ppf_kernel(
   for (unsigned ch = 0; ch < 4; ch++) O[(ch * uu + q) * um + j] = o[ch];
 }
 
+// The same local PPF when the centres are the points themselves and the
+// indices are k-major [B, k, N] (the extractor's self-KNN neighbours): one
+// workgroup per (cloud, 256 points, SL slots).  The cloud's coordinates and
+// normals are staged in LDS in the same round trip as the workgroup's index
+// rows, so every neighbour gather is an LDS read: no dependent global loads,
+// which under the grid kernel's write stream take microseconds each.
+constexpr int kPpfSelfMaxN = 2048;
+template <int SL>
+__global__ __launch_bounds__(256) void local_ppf_self_kernel(const float* __restrict__ xyz,
+                                                             const float* __restrict__ nrm,
+                                                             const int* __restrict__ idx, int n,
+                                                             int k, int relative,
+                                                             float* __restrict__ out) {
+  extern __shared__ __align__(16) float cl_s[];  // [6][n]: x y z nx ny nz
+  const int tid = threadIdx.x;
+  const int j = blockIdx.x * 256 + tid;
+  const int q0 = blockIdx.y * SL;
+  const int b = blockIdx.z;
+  const float* P = xyz + (size_t)b * 3 * n;
+  const float* Nn = nrm + (size_t)b * 3 * n;
+  int id[SL];
+#pragma unroll
+  for (int s = 0; s < SL; s++)
+    id[s] = (j < n && q0 + s < k) ? idx[((size_t)b * k + q0 + s) * n + j] : 0;
+  constexpr int E = kPpfSelfMaxN / 256;
+  float st[E][6];
+#pragma unroll
+  for (int e = 0; e < E; e++) {
+    const int i = e * 256 + tid;
+    if (i < n) {
+#pragma unroll
+      for (int a = 0; a < 3; a++) {
+        st[e][a] = P[(size_t)a * n + i];
+        st[e][3 + a] = Nn[(size_t)a * n + i];
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < E; e++) {
+    const int i = e * 256 + tid;
+    if (i < n)
+#pragma unroll
+      for (int a = 0; a < 6; a++) cl_s[(size_t)a * n + i] = st[e][a];
+  }
+  __syncthreads();
+  if (j >= n) return;
+  const float cx = cl_s[j], cy = cl_s[n + j], cz = cl_s[2 * n + j];
+  const float cnx = cl_s[3 * n + j], cny = cl_s[4 * n + j], cnz = cl_s[5 * n + j];
+  float* O = out + (size_t)b * 4 * k * n;
+#pragma unroll
+  for (int s = 0; s < SL; s++) {
+    const int q = q0 + s;
+    if (q < k) {
+      const unsigned si = (id[s] < 0 || id[s] >= n) ? 0u : (unsigned)id[s];
+      float o[4];
+      pcr_local_ppf(cx, cy, cz, cnx, cny, cnz, cl_s[si], cl_s[n + si], cl_s[2 * n + si],
+                    cl_s[3 * n + si], cl_s[4 * n + si], cl_s[5 * n + si], relative, o);
+#pragma unroll
+      for (int ch = 0; ch < 4; ch++) O[((size_t)ch * k + q) * n + j] = o[ch];
+    }
+  }
+}
+
 // ball_query.cu:30-49: points staged through LDS tiles; per-centre early exit
 constexpr int kBqTile = 1024;
 __global__ __launch_bounds__(256) void ball_query_kernel(const float* __restrict__ centers,
@@ -514,6 +577,14 @@ extern "C" pcr_status pcr_local_ppf_forward(const float* points, const float* no
   PCR_REQUIRE(b >= 0 && n >= 1 && m >= 0 && u >= 0, "local_ppf_forward: invalid sizes");
   PCR_REQUIRE(u <= 65535, "local_ppf_forward: u too large");
   if (b == 0 || m == 0 || u == 0) return PCR_OK;
+  if (points == centers && normals == center_normals && n == m && idx_kmajor &&
+      n <= kPpfSelfMaxN) {
+    constexpr int SL = 8;
+    hipLaunchKernelGGL((local_ppf_self_kernel<SL>), dim3(ceil_div(n, 256), ceil_div(u, SL), b),
+                       dim3(256), (size_t)6 * n * 4, as_stream(stream), points, normals, idx, n,
+                       u, relative, out);
+    return launch_status("local_ppf_forward");
+  }
   hipLaunchKernelGGL(local_ppf_kernel, dim3(ceil_div(m, 256), u, b), dim3(256), 0,
                      as_stream(stream), points, normals, centers, center_normals, idx, n, m, u,
                      idx_kmajor, relative, out);

@@ -704,6 +704,150 @@ __global__ __launch_bounds__(NT) void vox_grid_kernel(
   }
 }
 
+// ------------------------------------------------------------ means kernel
+// The first half of the split voxel stage: the voxel means of every occupied
+// segment of G channels of one cloud, in ascending point order inside each
+// voxel (the order vox_grid_kernel and the oracle use), written as compact
+// rows ws.means[b][c][ms] (slot n = 0) + the segment counts (channel group
+// 0), then the spherical devoxelisation of those means
+// (spherical_trilinear_devox.cu:127-134, corner -> segment map from prep) and
+// the per-cloud max-pooled descriptor.  Latency-bound by design (little
+// work per workgroup), so every global read of the launch -- features,
+// point order, segment offsets, corner segments and weights -- is requested
+// before any is used: one round trip instead of a chain of dependent loads,
+// which under the grid stream's write traffic take microseconds each.
+constexpr int kMeansNT = 256;
+constexpr int kMeansMaxN = 1024;
+template <int G>
+__global__ __launch_bounds__(kMeansNT) void vox_means_kernel(
+    const float* __restrict__ feat, int c, int n, VoxWs ws, const float* __restrict__ dwgts,
+    float* __restrict__ devox, float* __restrict__ desc, int ngrp) {
+  constexpr int NT = kMeansNT;
+  constexpr int PB = kMeansMaxN / NT;  // points per thread
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  const int b = blockIdx.x / ngrp;
+  const int grp = blockIdx.x % ngrp;
+  const int c0 = grp * G;
+  const int gcount = min(G, c - c0);
+  const int tid = threadIdx.x;
+  const int ns = n + 1;
+  float* feat_s = (float*)smem_raw;               // [G][n]
+  float* mean_s = feat_s + (size_t)G * n;         // [G][ns], slot n = 0
+  int* perm_s = (int*)(mean_s + (size_t)G * ns);  // [n]
+  int* soff_s = perm_s + n;                       // [ns]
+
+  // ---- every load in flight before any use
+  const float* fb = feat + ((size_t)b * c + c0) * n;
+  const int* gperm = ws.perm + (size_t)b * n;
+  const int* gsoff = ws.seg_off + (size_t)b * (n + 1);
+  float fv[G][PB];
+  int pv[PB], sv[PB + 1];
+#pragma unroll
+  for (int e = 0; e < PB; e++) {
+    const int i = e * NT + tid;
+#pragma unroll
+    for (int g = 0; g < G; g++) fv[g][e] = (i < n && g < gcount) ? fb[(size_t)g * n + i] : 0.0f;
+    pv[e] = i < n ? gperm[i] : 0;
+  }
+#pragma unroll
+  for (int e = 0; e <= PB; e++) {
+    const int i = e * NT + tid;
+    sv[e] = i <= n ? gsoff[i] : 0;
+  }
+  const float* Wt = dwgts + (size_t)b * 8 * n;
+  const int* Dg = ws.dseg + (size_t)b * 8 * n;
+  float dw[PB][8];
+  int ds[PB][8];
+#pragma unroll
+  for (int e = 0; e < PB; e++) {
+    const int i = e * NT + tid;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      dw[e][q] = i < n ? Wt[i + (size_t)q * n] : 0.0f;
+      const int sg = i < n ? Dg[i + (size_t)q * n] : -1;
+      ds[e][q] = sg >= 0 ? sg : n;  // empty corner -> the zero slot
+    }
+  }
+  const int nseg = ws.nseg[b];
+#pragma unroll
+  for (int e = 0; e < PB; e++) {
+    const int i = e * NT + tid;
+    if (i < n) {
+#pragma unroll
+      for (int g = 0; g < G; g++) feat_s[(size_t)g * n + i] = fv[g][e];
+      perm_s[i] = pv[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e <= PB; e++) {
+    const int i = e * NT + tid;
+    if (i <= n) soff_s[i] = sv[e];
+  }
+  if (tid < G) mean_s[(size_t)tid * ns + n] = 0.0f;
+  lds_barrier();
+
+  // ---- means (spherical_vox.cu:112-116 order: ascending point ids; the
+  // reference accumulates feat * (1/cnt) atomically in arbitrary order)
+  float* mo = ws.means + ((size_t)b * c + c0) * ws.ms;
+  for (int si = tid; si < nseg; si += NT) {
+    const int off = soff_s[si], end = soff_s[si + 1];
+    const float inv = pcr_inv_count(end - off);
+    float acc[G];
+#pragma unroll
+    for (int g = 0; g < G; g++) acc[g] = 0.0f;
+    for (int p = off; p < end; p++) {
+      const int pt = perm_s[p];
+#pragma unroll
+      for (int g = 0; g < G; g++) acc[g] = acc[g] + feat_s[(size_t)g * n + pt] * inv;
+    }
+#pragma unroll
+    for (int g = 0; g < G; g++) {
+      mean_s[(size_t)g * ns + si] = acc[g];
+      if (g < gcount) mo[(size_t)g * ws.ms + si] = acc[g];
+    }
+    if (grp == 0) ws.segcnt[(size_t)b * ws.ms + si] = (unsigned short)(end - off);
+  }
+  if (tid < gcount) mo[(size_t)tid * ws.ms + n] = 0.0f;  // the empty-cell slot
+  lds_barrier();
+
+  // ---- devox of the G channels + descriptor
+  float vmax[G];
+#pragma unroll
+  for (int g = 0; g < G; g++) vmax[g] = -__builtin_inff();
+  float* ov = devox + ((size_t)b * c + c0) * n;
+#pragma unroll
+  for (int e = 0; e < PB; e++) {
+    const int i = e * NT + tid;
+    if (i < n) {
+#pragma unroll
+      for (int g = 0; g < G; g++) {
+        if (g < gcount) {
+          float fq[8];
+#pragma unroll
+          for (int q = 0; q < 8; q++) fq[q] = mean_s[(size_t)g * ns + ds[e][q]];
+          const float v = pcr_wsum8(dw[e], fq);
+          ov[(size_t)g * n + i] = v;
+          vmax[g] = fmaxf(vmax[g], v);
+        }
+      }
+    }
+  }
+  if (desc) {
+    __shared__ float red[NT / kWave][G];
+#pragma unroll
+    for (int g = 0; g < G; g++) {
+      const float m = wave_max(vmax[g]);
+      if ((tid & 63) == 0) red[tid >> 6][g] = m;
+    }
+    lds_barrier();  // not waiting for the devox / means stores
+    if (tid < gcount) {
+      float m = red[0][tid];
+      for (int w = 1; w < NT / kWave; w++) m = fmaxf(m, red[w][tid]);
+      desc[(size_t)b * c + c0 + tid] = m;
+    }
+  }
+}
+
 // ------------------------------------------------------- streaming kernel
 // The dense [B, C, r^3] grid + cnt from the compact voxel means that the
 // means / devox launch left in ws.means ([b][c][ms], one row per channel,
@@ -742,7 +886,8 @@ __device__ inline void lds_only_barrier() {
   __builtin_amdgcn_s_barrier();
 }
 
-template <int NS, int NB>
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+template <int NS, int NB, int U, int AUX>
 __global__ __launch_bounds__((NS + 1) * 64) void vox_stream_kernel(int c, int n, int r3, VoxWs ws,
                                                                   float* __restrict__ out,
                                                                   int* __restrict__ cnt_out,
@@ -758,7 +903,7 @@ __global__ __launch_bounds__((NS + 1) * 64) void vox_stream_kernel(int c, int n,
   float* mean_s = (float*)smem_raw;                                // [NB][BUFB / 4]
   unsigned* bm_s = (unsigned*)(smem_raw + NB * BUFB);              // [W]
   unsigned short* pre_s = (unsigned short*)(bm_s + W);             // [W]
-  unsigned short* scnt_s = pre_s + W;                              // [ms], slot n = 0
+  unsigned short* scnt_s = pre_s + W;                              // [ms -> 256 B], slot n = 0
   const int b = blockIdx.x / wpc;
   const int j0 = (blockIdx.x % wpc) * per;
   const int nit = min(ngrp, j0 + per) - j0;
@@ -786,44 +931,34 @@ __global__ __launch_bounds__((NS + 1) * 64) void vox_stream_kernel(int c, int n,
     for (int q = 0; q < D; q++)
       if (q < nit) issue(j0 + q, q);
     if (!(dbg & 2)) {
-      const unsigned* gbm = ws.bitmap + (size_t)b * W;
-      unsigned v[kStreamMaxW / 64];
-#pragma unroll
-      for (int q = 0; q < kStreamMaxW / 64; q++) {
-        const int w = q * 64 + lt;
-        v[q] = w < W ? gbm[w] : 0u;
-      }
-      const unsigned short* gsc = ws.segcnt + (size_t)b * ms;
-      constexpr int kSc = (kStreamMaxN + 1 + 3 + 63) / 64 + 1;
-      unsigned short t[kSc];
-#pragma unroll
-      for (int q = 0; q < kSc; q++) {
-        const int s2 = q * 64 + lt;
-        t[q] = s2 < ms ? gsc[s2] : (unsigned short)0;
-      }
+      // bitmap and segment counts by LDS-DMA too (4-byte pieces: 256 B per
+      // wave instruction), so the loader holds no staging registers
+      const char* gbm = (const char*)(ws.bitmap + (size_t)b * W);
+      for (int p = 0; p < W / 64; p++)
+        __builtin_amdgcn_global_load_lds((gbl_void_p)(gbm + p * 256 + lt * 4),
+                                         (lds_void_p)((char*)bm_s + p * 256), 4, 0, 0);
+      const char* gsc = (const char*)(ws.segcnt + (size_t)b * ms);
+      for (int p = 0; p < (ms * 2 + 255) / 256; p++)
+        __builtin_amdgcn_global_load_lds((gbl_void_p)(gsc + p * 256 + lt * 4),
+                                         (lds_void_p)((char*)scnt_s + p * 256), 4, 0, 0);
       const int nseg = ws.nseg[b];
+      wait_vmcnt<0>();
+      // word prefix (u16) from the landed bitmap; unused counts -> 0 (slot n)
       int carry = 0;
-#pragma unroll
-      for (int q = 0; q < kStreamMaxW / 64; q++) {
+      for (int q = 0; q < W / 64; q++) {
         const int w = q * 64 + lt;
-        const int pc = __popc(v[q]);
+        const unsigned v = bm_s[w];
+        const int pc = __popc(v);
         int incl = pc;
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) {
           const int o = __shfl_up(incl, off, kWave);
           if (lt >= off) incl += o;
         }
-        if (w < W) {
-          bm_s[w] = v[q];
-          pre_s[w] = (unsigned short)(carry + incl - pc);
-        }
+        pre_s[w] = (unsigned short)(carry + incl - pc);
         carry += __shfl(incl, 63, kWave);
       }
-#pragma unroll
-      for (int q = 0; q < kSc; q++) {
-        const int s2 = q * 64 + lt;
-        if (s2 < ms) scnt_s[s2] = s2 < nseg ? t[q] : (unsigned short)0;  // slot n = 0
-      }
+      for (int s2 = nseg + lt; s2 < ms; s2 += 64) scnt_s[s2] = 0;
     }
     wait_vmcnt<0>();  // the plain loads above already waited; keeps it simple
     lds_only_barrier();
@@ -846,7 +981,6 @@ __global__ __launch_bounds__((NS + 1) * 64) void vox_stream_kernel(int c, int n,
   // groups of 4 consecutive cells (occupancy word + prefix, then the means /
   // counts, slot n = 0 for empty cells) is issued before any is waited on;
   // one 16-byte store per channel (+ cnt) and group
-  constexpr int U = 4;
   auto stream_u = [&](int base0, float* ob, int g_lo, int gcount, const float* ms0, int* cb) {
     if (dbg & 1) {  // diagnostic: zeros only, no LDS reads
       const float4 z = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -889,20 +1023,27 @@ __global__ __launch_bounds__((NS + 1) * 64) void vox_stream_kernel(int c, int n,
           v[u][g] = float4{ms_g[ix[u][0]], ms_g[ix[u][1]], ms_g[ix[u][2]], ms_g[ix[u][3]]};
         }
       }
+    // buffer stores with cache policy AUX (16 = sc1: write-through, the
+    // line is not kept in the XCD's L2, so the grid stream does not evict
+    // the other kernels' working sets)
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(ob, (short)0, 2 * r3 * 4, 0x00020000);
 #pragma unroll
     for (int g = 0; g < G; g++) {
 #pragma unroll
       for (int u = 0; u < U; u++) {
         const int base = base0 + u * NTS * 4;
-        if (base < r3 && g >= g_lo && g < gcount) *(float4*)(ob + (size_t)g * r3 + base) = v[u][g];
+        if (base < r3 && g >= g_lo && g < gcount)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v[u][g]), rs,
+                                                 (g * r3 + base) * 4, 0, AUX);
       }
     }
     if (cb) {
+      const auto rc = __builtin_amdgcn_make_buffer_rsrc(cb, (short)0, r3 * 4, 0x00020000);
 #pragma unroll
       for (int u = 0; u < U; u++) {
         const int base = base0 + u * NTS * 4;
-        const int4 cv = {scnt_s[ix[u][0]], scnt_s[ix[u][1]], scnt_s[ix[u][2]], scnt_s[ix[u][3]]};
-        if (base < r3) *(int4*)(cb + base) = cv;
+        const u32x4_t cv = {scnt_s[ix[u][0]], scnt_s[ix[u][1]], scnt_s[ix[u][2]], scnt_s[ix[u][3]]};
+        if (base < r3) __builtin_amdgcn_raw_buffer_store_b128(cv, rc, base * 4, 0, AUX);
       }
     }
   };
@@ -1351,7 +1492,18 @@ extern "C" pcr_status pcr_extractor_voxel_means_devox(const float* features, int
   const int r3 = r * r * r;
   const int tile = ((r3 + 31) / 32) * 32;
   const int nw = tile / 32 + 1;
-  static const int mv = getenv("PCR_MEANS_V") ? atoi(getenv("PCR_MEANS_V")) : 0;
+  static const int mv = getenv("PCR_MEANS_V") ? atoi(getenv("PCR_MEANS_V")) : 3;
+  if (mv == 3 && n <= kMeansMaxN) {
+    // two channels per workgroup: ~24 KB of LDS, so it fits beside the
+    // KNN selection's workgroups
+    constexpr int G = 2;
+    const int ngrp = ceil_div(c, G);
+    const size_t smem = ((size_t)G * n + (size_t)G * (n + 1) + n + (n + 1)) * 4;
+    allow_big_lds(vox_means_kernel<G>, smem);
+    hipLaunchKernelGGL((vox_means_kernel<G>), dim3(ngrp * b), dim3(kMeansNT), smem,
+                       as_stream(stream), features, c, n, ws, dwgts, devox, desc, ngrp);
+    return launch_status(name);
+  }
   int G = 1;
   const int ngrp = pick_groups(c, n, mv == 0 ? 4 : 2, &G);
   const size_t smem = grid_smem_bytes(G, n, nw);
@@ -1361,14 +1513,9 @@ extern "C" pcr_status pcr_extractor_voxel_means_devox(const float* features, int
     hipLaunchKernelGGL((vox_grid_kernel<2, kDevoxThreads, 4>), dim3(ngrp * b), dim3(kDevoxThreads),
                        smem, as_stream(stream), features, c, n, r3, G, tile, ws, nullptr, nullptr,
                        dinds, dwgts, devox, desc, 1, ngrp, ngrp * b);
-  } else if (mv == 1) {
+  } else {
     allow_big_lds(vox_grid_kernel<2, 256, 2>, smem);
     hipLaunchKernelGGL((vox_grid_kernel<2, 256, 2>), dim3(ngrp * b), dim3(256), smem,
-                       as_stream(stream), features, c, n, r3, G, tile, ws, nullptr, nullptr, dinds,
-                       dwgts, devox, desc, 1, ngrp, ngrp * b);
-  } else {
-    allow_big_lds(vox_grid_kernel<2, 512, 2>, smem);
-    hipLaunchKernelGGL((vox_grid_kernel<2, 512, 2>), dim3(ngrp * b), dim3(512), smem,
                        as_stream(stream), features, c, n, r3, G, tile, ws, nullptr, nullptr, dinds,
                        dwgts, devox, desc, 1, ngrp, ngrp * b);
   }
@@ -1412,17 +1559,24 @@ extern "C" pcr_status pcr_extractor_voxel_stream(int b, int c, int n, int r, int
   const int per = ceil_div(ngrp, wpc);
   static const int dbg = getenv("PCR_STREAM_DBG") ? atoi(getenv("PCR_STREAM_DBG")) : 0;
   static const int nb = getenv("PCR_STREAM_NB") ? atoi(getenv("PCR_STREAM_NB")) : kStreamNB;
+  PCR_REQUIRE(ws.W % 64 == 0, "%s: r^3 %% 2048 != 0 unsupported", name);
+  static const int uu = getenv("PCR_STREAM_U") ? atoi(getenv("PCR_STREAM_U")) : 2;
   const size_t smem = (size_t)nb * kStreamNG * 1024 + (size_t)ws.W * 6 +
-                      ((size_t)ws.ms * 2 + 15) / 16 * 16;
-  if (nb == 2) {
-    allow_big_lds(vox_stream_kernel<4, 2>, smem);
-    hipLaunchKernelGGL((vox_stream_kernel<4, 2>), dim3(b * wpc), dim3(5 * 64), smem,
-                       as_stream(stream), c, n, r3, ws, grid, cnt, ngrp, wpc, per, dbg);
-  } else {
-    allow_big_lds(vox_stream_kernel<4, kStreamNB>, smem);
-    hipLaunchKernelGGL((vox_stream_kernel<4, kStreamNB>), dim3(b * wpc), dim3(5 * 64), smem,
-                       as_stream(stream), c, n, r3, ws, grid, cnt, ngrp, wpc, per, dbg);
-  }
+                      ((size_t)ws.ms * 2 + 255) / 256 * 256;
+  static const int aux = getenv("PCR_STREAM_AUX") ? atoi(getenv("PCR_STREAM_AUX")) : 16;
+#define PCR_LAUNCH_STREAM(NSV, NBV, UV, AV)                                                    \
+  do {                                                                                        \
+    allow_big_lds(vox_stream_kernel<NSV, NBV, UV, AV>, smem);                                 \
+    hipLaunchKernelGGL((vox_stream_kernel<NSV, NBV, UV, AV>), dim3(b * wpc),                  \
+                       dim3((NSV + 1) * 64), smem, as_stream(stream), c, n, r3, ws, grid, cnt, \
+                       ngrp, wpc, per, dbg);                                                  \
+  } while (0)
+  if (aux == 0 && uu == 4) PCR_LAUNCH_STREAM(4, 3, 4, 0);
+  else if (aux == 0) PCR_LAUNCH_STREAM(4, 3, 2, 0);
+  else if (aux == 2) PCR_LAUNCH_STREAM(4, 3, 2, 2);
+  else if (uu == 4) PCR_LAUNCH_STREAM(4, 3, 4, 16);
+  else PCR_LAUNCH_STREAM(4, 3, 2, 16);
+#undef PCR_LAUNCH_STREAM
   return launch_status(name);
 }
 

@@ -50,9 +50,21 @@ SIGNATURES = {
     "pcr_extractor_voxel_grid_devox": (ST, [P, I, I, I, I, P, P, P, P, P, P, P, SZ, P]),
     "pcr_extractor_voxel_means_devox": (ST, [P, I, I, I, I, P, P, P, P, P, SZ, P]),
     "pcr_extractor_voxel_stream": (ST, [I, I, I, I, P, P, P, SZ, P]),
+    "pcr_extractor_run": (ST, [P, I, I, P, P, P, P, P]),
     "pcr_selftest_math": (ST, [I, P, P, I, I, P, P, P]),
     "pcr_selftest_math_d": (ST, [I, P, P, I, P, P]),
 }
+
+
+
+class ExtractorArgs(ctypes.Structure):
+    """struct pcr_extractor_args of include/pcr_amd.h"""
+    _fields_ = [("b", I), ("n", I), ("c", I), ("k", I), ("r", I), ("relative", I),
+                ("xyz", P), ("normals", P), ("features", P), ("knn_idx", P), ("knn_dist", P),
+                ("local_ppf", P), ("norm_coords", P), ("ind", P), ("cnt", P), ("grid", P),
+                ("devox", P), ("desc", P), ("dinds", P * 2), ("dwgts", P * 2), ("knn_ws", P),
+                ("knn_ws_bytes", SZ), ("vox_ws", P * 2), ("vox_ws_bytes", SZ)]
+
 
 _lib = None
 

@@ -20,6 +20,8 @@ The streams are forked from and joined back to the caller's stream.
 S consecutive steps with no join between them on alternating buffer sets, so
 step i+1's front stage overlaps step i's back stages.
 """
+import ctypes
+
 import torch
 
 from . import _lib
@@ -240,6 +242,38 @@ class SphExtractor:
             "dinds": dinds, "dwgts": dwgts, "desc": self.desc,
         }
 
+    def run_native(self, xyz, normals, features, steps, desc_steps=None, schedule=1):
+        """`steps` pipelined steps enqueued by the library's native runner
+        (pcr_extractor_run): schedule 1 = three streams (prep + means / devox
+        on s_pre, the grid stream on s_vox, sort + select + PPF on s_nbr,
+        voxel buffer sets alternating), 0 = two streams with the fused grid
+        kernel.  One ctypes call for all steps."""
+        self._check_inputs(xyz, normals, features)
+        s1 = self._set(1)
+        a = _lib.ExtractorArgs()
+        a.b, a.n, a.c, a.k, a.r, a.relative = self.b, self.n, self.c, self.k, self.r, \
+            int(self.relative)
+        a.xyz, a.normals, a.features = _ptr(xyz), _ptr(normals), _ptr(features)
+        a.knn_idx, a.knn_dist, a.local_ppf = _ptr(self.knn_idx), _ptr(self.knn_dist), \
+            _ptr(self.local_ppf)
+        a.norm_coords, a.ind, a.cnt, a.grid = _ptr(self.norm_coords), _ptr(self.ind), \
+            _ptr(self.cnt), _ptr(self.grid)
+        a.devox, a.desc = _ptr(self.devox), _ptr(self.desc)
+        a.dinds[0], a.dinds[1] = _ptr(self.dinds), _ptr(s1[2])
+        a.dwgts[0], a.dwgts[1] = _ptr(self.dwgts), _ptr(s1[3])
+        a.knn_ws, a.knn_ws_bytes = _ptr(self.knn_ws), self.knn_ws.numel()
+        a.vox_ws[0], a.vox_ws[1] = _ptr(self.ws), _ptr(s1[1])
+        a.vox_ws_bytes = self.ws.numel()
+        if desc_steps is not None and tuple(desc_steps.shape) != (steps, self.b, self.c):
+            raise RuntimeError("desc_steps must be [steps, B, C]")
+        cur = torch.cuda.current_stream(self.device)
+        _lib.check(_lib.load().pcr_extractor_run(
+            ctypes.byref(a), steps, schedule, _ptr(desc_steps), cur.cuda_stream,
+            self.s_nbr.cuda_stream, self.s_pre.cuda_stream, self.s_vox.cuda_stream),
+            "extractor_run")
+        last = (steps - 1) & 1 if schedule == 1 else 0
+        return self.outputs(slot=last)
+
     def run_pipelined(self, xyz, normals, features, steps, desc_steps=None, mode="two_fused"):
         """Enqueue `steps` consecutive steps with no join between them, forked
         from and joined back to the current stream once.  Step s writes its
@@ -340,6 +374,45 @@ class SphExtractor:
                 self.voxel_stream(sv)
             self._join(cur)
             return self.outputs()
+        if mode == "four_stream":
+            # s_dev: Morton sort of step s+1 (KNN set (s+1) % 2, after the
+            # selection of step s-1 read it); s_nbr: selection + PPF of step s;
+            # s_pre: prep + means / devox / descriptor (voxel set s % 2);
+            # s_vox: the grid stream of step s
+            sa, sn = self.s_dev, self.s_nbr
+            stream_done, sel_done, e_sort, ok = [None, None], [None, None], [None, None], [None, None]
+
+            def rec(st):
+                e_ = torch.cuda.Event()
+                e_.record(st)
+                return e_
+
+            def sort(s):
+                sl = s & 1
+                if sel_done[sl] is not None:
+                    sa.wait_event(sel_done[sl])
+                ok[sl] = self.knn_sort(xyz, sa.cuda_stream, sl)
+                e_sort[sl] = rec(sa)
+
+            sort(0)
+            for s in range(steps):
+                slot = s & 1
+                d = None if desc_steps is None else desc_steps[s]
+                if s + 1 < steps:
+                    sort(s + 1)
+                if stream_done[slot] is not None:
+                    self.s_pre.wait_event(stream_done[slot])
+                self.voxel_prep(xyz, self.s_pre.cuda_stream, slot)
+                self.voxel_means_devox(features, self.s_pre.cuda_stream, d, slot)
+                self.s_vox.wait_event(rec(self.s_pre))
+                self.voxel_stream(self.s_vox.cuda_stream, slot)
+                stream_done[slot] = rec(self.s_vox)
+                sn.wait_event(e_sort[slot])
+                self.knn_select(xyz, normals, sn.cuda_stream, slot, ok[slot])
+                sel_done[slot] = rec(sn)
+            self._join(cur)
+            last = (steps - 1) & 1
+            return self.outputs(slot=last, idx_slot=last)
         if mode == "three_stream":
             # s_nbr: sort + select + PPF; s_pre: prep + means / devox /
             # descriptor of step s into workspace set s % 2 (after the grid

@@ -34,12 +34,17 @@ for rnd in range(3):
         if m in prio:
             ex.s_nbr, ex.s_vox = prio[m]
             mm = "two_fused"
+        def go(mm=mm, S=S):
+            if mm.startswith("native"):
+                ex.run_native(xyz, nrm, feat, S, schedule=int(mm[6:] or 1))
+            else:
+                ex.run_pipelined(xyz, nrm, feat, S, mode=mm)
         for _ in range(2):
-            ex.run_pipelined(xyz, nrm, feat, S, mode=mm)
+            go()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(200 // S):
-            ex.run_pipelined(xyz, nrm, feat, S, mode=mm)
+            go()
         torch.cuda.synchronize()
         res[m].append(b * (200 // S) * S / (time.perf_counter() - t0))
 for m, v in res.items():

@@ -52,6 +52,17 @@ def run(name, f):
           flush=True)
 
 
+ex_lib.exp_stream_fat.argtypes = [ctypes.c_void_p, ctypes.c_long, ctypes.c_int, ctypes.c_int,
+                                  ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+run("select alone", sel)
+for nt, vr, lds in ((256, 4, 0), (320, 4, 0), (256, 48, 0), (256, 4, 36000), (320, 48, 36000)):
+    def stf(nt=nt, vr=vr, lds=lds):
+        ex_lib.exp_stream_fat(_ptr(grid), n4, 256, nt, vr, lds, sv.cuda_stream)
+
+    tag = "fat nt=%d vregs=%d lds=%d" % (nt, vr, lds)
+    run("stream " + tag, stf)
+    run("sel+stream " + tag, lambda: (sel(), stf()))
+sys.exit(0)
 run("select alone", sel)
 for wgs, nt, mode, lds in ((256, 256, 65536, 0), (256, 256, 16384, 0), (1024, 256, 16384, 0),
                            (256, 256, 0, 0), (256, 512, 0, 0), (256, 1024, 0, 0), (512, 256, 0, 0),

@@ -52,6 +52,7 @@ steps = {
     "ppf+grid": lambda: (ppf(sn.cuda_stream), ex.voxel_grid_devox(feat, sv.cuda_stream)),
     "stream": lambda: ex.voxel_stream(sv.cuda_stream),
     "stream+sel": lambda: (ex.voxel_stream(sv.cuda_stream), sel(sn.cuda_stream)),
+    "ppf+stream": lambda: (ppf(sn.cuda_stream), ex.voxel_stream(sv.cuda_stream)),
     "means": lambda: ex.voxel_means_devox(feat, sv.cuda_stream),
     "sel+stream": lambda: (sel(sn.cuda_stream), ex.voxel_stream(sv.cuda_stream)),
     "vox2": lambda: (ex.voxel_prep(xyz, sv.cuda_stream), ex.voxel_means_devox(feat, sv.cuda_stream),
