@@ -39,7 +39,7 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=40)
     ap.add_argument("--batch", type=int, default=32, help="clouds per GPU")
     ap.add_argument("--points", type=int, default=1024)
     ap.add_argument("--k", type=int, default=32)
@@ -48,15 +48,19 @@ def parse():
     ap.add_argument("--kernel-iters", type=int, default=50)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--mode", choices=("pipelined", "pipelined_split", "pipelined3", "pipelined4",
+    ap.add_argument("--mode", choices=("native", "native2", "pipelined", "pipelined_split",
+                                       "pipelined3", "pipelined4",
                                        "pipelined_sv", "pipelined_fs", "pipelined_3s", "pipelined_2s", "graph",
                                        "eager"),
-                    default="pipelined",
-                    help="pipelined: S steps on two independent streams (KNN / voxel, fused "
-                         "grid+devox kernel) with no join between them; pipelined_split: "
+                    default="native",
+                    help="native: S steps enqueued by the library (pcr_extractor_run) on three "
+                         "streams -- KNN, prep + means/devox, grid stream; native2: the same "
+                         "runner, two streams with the fused grid kernel; "
+                         "pipelined: S steps on two independent streams (KNN / voxel, fused "
+                         "grid+devox kernel) from Python with no join between them; pipelined_split: "
                          "separate grid and devox launches; pipelined3/4/_sv: schedules with cross-stream "
                          "events; graph: one hipGraph replay per step; eager: fork/join per step")
-    ap.add_argument("--steps-per-launch", type=int, default=10,
+    ap.add_argument("--steps-per-launch", type=int, default=40,
                     help="pipelined steps per launch group (must divide --steps and --warmup)")
     return ap.parse_args()
 
@@ -126,14 +130,15 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from pcr_amd.extractor import (SphExtractor, algorithmic_bytes_per_cloud,
-                                   fused_grid_kernel_bytes_per_cloud)
+                                   fused_grid_kernel_bytes_per_cloud,
+                                   stream_kernel_bytes_per_cloud)
     b, n, c, k, r = args.batch, args.points, args.channels, args.k, args.res
     xyz, nrm, feat = synthetic_inputs(b, n, c, dev, seed=1234 + rank)
     ex = SphExtractor(b, n, c, k, r, device=dev)
 
     # S pipelined steps per graph launch (one launch = S batches); S must
     # divide the step counts so exactly --steps steps are timed
-    S = max(1, args.steps_per_launch) if args.mode.startswith("pipelined") else 1
+    S = max(1, args.steps_per_launch) if args.mode.startswith(("pipelined", "native")) else 1
     if args.steps % S or (args.warmup and args.warmup % S):
         S = 1
     comm = torch.cuda.Stream(device=dev) if world > 1 else None
@@ -147,7 +152,10 @@ def main():
 
     def launch(i):
         """Steps i*S .. i*S+S-1."""
-        if args.mode.startswith("pipelined"):
+        if args.mode.startswith("native"):
+            ex.run_native(xyz, nrm, feat, S, desc_steps, schedule=0 if args.mode == "native2" else 1)
+            src = desc_steps.view(S * b, c)
+        elif args.mode.startswith("pipelined"):
             ex.run_pipelined(xyz, nrm, feat, S, desc_steps,
                              mode={"pipelined": "two_fused", "pipelined_split": "two",
                                    "pipelined3": "three",
@@ -199,21 +207,33 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # dominant kernel: voxel-grid kernel, HIP events on its stream
+    # dominant kernel, HIP events on the stream it is launched on: the grid
+    # stream kernel of the split voxel stage (native) or the fused grid /
+    # devox kernel (the other schedules)
+    split = args.mode == "native"
     s_k = ex.s_vox
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.kernel_iters)]
     with torch.cuda.stream(s_k):
         for e0, e1 in ev:
             ex.voxel_prep(xyz, s_k.cuda_stream)
-            e0.record(s_k)
-            ex.voxel_grid_devox(feat, s_k.cuda_stream)
+            if split:
+                ex.voxel_means_devox(feat, s_k.cuda_stream)
+                e0.record(s_k)
+                ex.voxel_stream(s_k.cuda_stream)
+            else:
+                e0.record(s_k)
+                ex.voxel_grid_devox(feat, s_k.cuda_stream)
             e1.record(s_k)
     torch.cuda.synchronize(dev)
     grid_ms = sorted(e0.elapsed_time(e1) for e0, e1 in ev)
     grid_avg_ms = sum(grid_ms) / len(grid_ms)
-    grid_bytes = fused_grid_kernel_bytes_per_cloud(n, r, c) * b
+    grid_bytes = (stream_kernel_bytes_per_cloud(r, c) if split
+                  else fused_grid_kernel_bytes_per_cloud(n, r, c)) * b
     achieved = grid_bytes / (grid_avg_ms * 1e-3) / 1e9
+    kname = ("vox_stream_kernel (sph-vox dense grid + cnt from the voxel means, write-through "
+             "stores)" if split else
+             "vox_grid_kernel<3> (sph-vox dense grid + cnt, sph-devox + descriptor)")
 
     total_clouds = b * world * args.steps
     value = total_clouds / elapsed
@@ -224,7 +244,7 @@ def main():
         try:
             with open(pmc_path) as f:
                 pm = json.load(f)
-            if pm.get("config") == [b, n, k, r, c]:
+            if pm.get("config") == [b, n, k, r, c] and pm.get("kernel", "") in kname:
                 traffic = pm.get("grid_kernel_hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
@@ -251,8 +271,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic,
-                     "kernel": "vox_grid_kernel<3> (sph-vox dense grid + cnt, sph-devox + "
-                               "descriptor)",
+                     "kernel": kname,
                      "kernel_avg_ms": round(grid_avg_ms, 5),
                      "kernel_bytes_per_launch": grid_bytes},
         "step_algorithmic_GBps": round(step_bytes * world * args.steps / elapsed / 1e9, 1),

@@ -253,6 +253,9 @@ pcr_status pcr_extractor_voxel_stream(int b, int c, int n, int r, int *cnt, floa
  *   schedule 1: three streams -- s_nbr as above; s_pre: prep + means / devox
  *               / descriptor of step s into buffer set s % 2 (after the grid
  *               stream of step s-2 read it); s_vox: the grid stream of step s.
+ *   schedule 2: as 1, with the Morton sort moved to s_pre (ahead of prep, into
+ *               KNN workspace s % 2 after the selection of step s-2 read it),
+ *               so s_nbr only selects and computes the local PPF.
  * Buffers with two entries are the alternating sets (schedule 0 uses set 0).
  * desc_steps: [steps][b][c] per-step descriptors, or NULL (then desc). */
 typedef struct pcr_extractor_args {
@@ -266,7 +269,7 @@ typedef struct pcr_extractor_args {
   float *grid, *devox, *desc;             /* [b,c,r^3], [b,c,n], [b,c] */
   int *dinds[2];                          /* [b,8,n] */
   float *dwgts[2];                        /* [b,8,n] */
-  void *knn_ws;                           /* pcr_knn_workspace_size(b, n, n) */
+  void *knn_ws[2];                        /* pcr_knn_workspace_size(b, n, n) */
   size_t knn_ws_bytes;
   void *vox_ws[2];                        /* pcr_extractor_workspace_size(b, n, c, r) */
   size_t vox_ws_bytes;

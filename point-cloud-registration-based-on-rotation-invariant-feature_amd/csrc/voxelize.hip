@@ -164,7 +164,7 @@ template <int MODE, int NT>
 __global__ __launch_bounds__(NT) void vox_prep_kernel(
     const float* __restrict__ coords_f, const int* __restrict__ coords_i, int n, int r, int npad,
     float* __restrict__ norm_out, int* __restrict__ ind, VoxWs ws, int* __restrict__ dinds,
-    float* __restrict__ dwgts) {
+    float* __restrict__ dwgts, int prio) {
   extern __shared__ __align__(16) unsigned char smem_raw[];
   unsigned long long* keys = (unsigned long long*)smem_raw;  // [npad]
   unsigned* bm = (unsigned*)(keys + npad);                     // [W]
@@ -173,7 +173,7 @@ __global__ __launch_bounds__(NT) void vox_prep_kernel(
   __shared__ float s_stat[4];
   __shared__ int s_flag;  // a crowded voxel: the bitonic path
 
-  latency_kernel_priority();
+  if (prio) latency_kernel_priority();
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
   constexpr int nt = NT;
@@ -1306,6 +1306,12 @@ static size_t grid_smem_bytes(int G, int n, int nw) {
   return ((size_t)G * n + (size_t)G * (n + 1) + (n + 1) + 2 * (size_t)nw) * 4;
 }
 
+// issue priority of the prep kernel (PCR_PREP_PRIO=0 turns the boost off)
+static int prep_prio() {
+  static const int p = getenv("PCR_PREP_PRIO") ? atoi(getenv("PCR_PREP_PRIO")) : 1;
+  return p;
+}
+
 // Launch helpers.  `what`: 1 = prep only, 2 = grid only, 3 = both.
 template <int MODE>
 static pcr_status run_voxelize(const float* features, const float* coords_f, const int* coords_i,
@@ -1342,19 +1348,19 @@ static pcr_status run_voxelize(const float* features, const float* coords_f, con
       const size_t sm5 = (size_t)npad5 * 8 + (size_t)ws.W * 8 + (size_t)n * 8;
       allow_big_lds(vox_prep_kernel<MODE, 512>, sm5);
       hipLaunchKernelGGL((vox_prep_kernel<MODE, 512>), dim3(b), dim3(512), sm5, stream, coords_f,
-                         coords_i, n, r, npad5, norm_out, ind, ws, dinds, dwgts);
+                         coords_i, n, r, npad5, norm_out, ind, ws, dinds, dwgts, prep_prio());
     } else if (small && exp_nt != 1024) {
       allow_big_lds(vox_prep_kernel<MODE, kSmallPrepThreads>, prep_smem);
       hipLaunchKernelGGL((vox_prep_kernel<MODE, kSmallPrepThreads>), dim3(b),
                          dim3(kSmallPrepThreads), prep_smem, stream, coords_f, coords_i, n, r,
-                         npad, norm_out, ind, ws, dinds, dwgts);
+                         npad, norm_out, ind, ws, dinds, dwgts, prep_prio());
     } else {
       const int npad1 = next_pow2(n < kPrepThreads ? kPrepThreads : n);
       const size_t sm1 = (size_t)npad1 * 8 + (size_t)ws.W * 8 + (size_t)n * 8;
       allow_big_lds(vox_prep_kernel<MODE, kPrepThreads>, sm1);
       hipLaunchKernelGGL((vox_prep_kernel<MODE, kPrepThreads>), dim3(b), dim3(kPrepThreads),
                          sm1, stream, coords_f, coords_i, n, r, npad1, norm_out, ind, ws,
-                         dinds, dwgts);
+                         dinds, dwgts, prep_prio());
     }
   }
   const bool do_grid = (what & 2) != 0;

@@ -62,7 +62,7 @@ class ExtractorArgs(ctypes.Structure):
     _fields_ = [("b", I), ("n", I), ("c", I), ("k", I), ("r", I), ("relative", I),
                 ("xyz", P), ("normals", P), ("features", P), ("knn_idx", P), ("knn_dist", P),
                 ("local_ppf", P), ("norm_coords", P), ("ind", P), ("cnt", P), ("grid", P),
-                ("devox", P), ("desc", P), ("dinds", P * 2), ("dwgts", P * 2), ("knn_ws", P),
+                ("devox", P), ("desc", P), ("dinds", P * 2), ("dwgts", P * 2), ("knn_ws", P * 2),
                 ("knn_ws_bytes", SZ), ("vox_ws", P * 2), ("vox_ws_bytes", SZ)]
 
 

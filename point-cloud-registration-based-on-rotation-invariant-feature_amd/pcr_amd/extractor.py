@@ -261,7 +261,8 @@ class SphExtractor:
         a.devox, a.desc = _ptr(self.devox), _ptr(self.desc)
         a.dinds[0], a.dinds[1] = _ptr(self.dinds), _ptr(s1[2])
         a.dwgts[0], a.dwgts[1] = _ptr(self.dwgts), _ptr(s1[3])
-        a.knn_ws, a.knn_ws_bytes = _ptr(self.knn_ws), self.knn_ws.numel()
+        a.knn_ws[0], a.knn_ws[1] = _ptr(self.knn_ws), _ptr(s1[0])
+        a.knn_ws_bytes = self.knn_ws.numel()
         a.vox_ws[0], a.vox_ws[1] = _ptr(self.ws), _ptr(s1[1])
         a.vox_ws_bytes = self.ws.numel()
         if desc_steps is not None and tuple(desc_steps.shape) != (steps, self.b, self.c):
@@ -271,7 +272,7 @@ class SphExtractor:
             ctypes.byref(a), steps, schedule, _ptr(desc_steps), cur.cuda_stream,
             self.s_nbr.cuda_stream, self.s_pre.cuda_stream, self.s_vox.cuda_stream),
             "extractor_run")
-        last = (steps - 1) & 1 if schedule == 1 else 0
+        last = (steps - 1) & 1 if schedule >= 1 else 0
         return self.outputs(slot=last)
 
     def run_pipelined(self, xyz, normals, features, steps, desc_steps=None, mode="two_fused"):
@@ -578,6 +579,16 @@ def grid_kernel_bytes_per_cloud(n, r, c):
     point order 8N) is not counted: it is an artefact of this design."""
     r3 = r ** 3
     return 4 * c * n + 4 * c * r3 + 4 * r3
+
+
+def stream_kernel_bytes_per_cloud(r, c):
+    """Algorithmic HBM bytes of the split voxel stage's dominant kernel
+    (vox_stream_kernel: the spherical_avg_voxelize outputs)
+    per cloud: grid written 4C r^3, cnt written 4 r^3.  Its reads of the
+    compact voxel means (4C per occupied voxel) and of the occupancy bitmap
+    are artefacts of this design and not counted."""
+    r3 = r ** 3
+    return 4 * c * r3 + 4 * r3
 
 
 def fused_grid_kernel_bytes_per_cloud(n, r, c):

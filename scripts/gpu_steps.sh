@@ -32,9 +32,9 @@ for step in "$@"; do
            run bench_graph 300 python bench.py --mode graph --no-cpu-baseline
            run bench_eager 300 python bench.py --mode eager --no-cpu-baseline ;;
     prof) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
-          run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 50 --warmup 10 --no-cpu-baseline ;;
-    pmc)  run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --kernel-iters 5 --no-cpu-baseline --mode eager
-          run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --kernel-iters 5 --no-cpu-baseline --mode eager
+          run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 80 --warmup 40 --no-cpu-baseline ;;
+    pmc)  run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 5 --warmup 5 --steps-per-launch 5 --kernel-iters 5 --no-cpu-baseline
+          run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 5 --warmup 5 --steps-per-launch 5 --kernel-iters 5 --no-cpu-baseline
           run pmc_json 60 python3 scripts/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc_traffic.json 32 1024 32 32 64 ;;
     large) run pytest_large 600 python -m pytest tests/test_gpu_large.py -q -m gpu -p no:cacheprovider ;;
     knnb) run knn_bench 300 python scripts/knn_bench.py ;;

@@ -17,7 +17,7 @@ import os
 import sys
 from collections import defaultdict
 
-KERNEL = "vox_grid_kernel<3,"
+KERNEL = os.environ.get("PCR_PMC_KERNEL", "vox_stream_kernel")
 
 
 def per_dispatch(d, counter):

@@ -84,7 +84,7 @@ def test_extractor_pipelined_graph(dev):
             assert torch.equal(desc_steps[s], ref["desc"]), (mode, s)
 
 
-@pytest.mark.parametrize("schedule", [0, 1])
+@pytest.mark.parametrize("schedule", [0, 1, 2])
 def test_extractor_native_runner(dev, schedule):
     """pcr_extractor_run (the bench's native multi-step enqueue): every
     step's descriptor and the final outputs equal the single-step results."""
