@@ -243,6 +243,19 @@ pcr_status pcr_extractor_voxel_means_devox(const float *features, int b, int c, 
 pcr_status pcr_extractor_voxel_stream(int b, int c, int n, int r, int *cnt, float *grid,
                                       void *workspace, size_t workspace_bytes, void *stream);
 
+/* ------------------------------------------- mutual-NN matching (8f f1) ----
+ * datasets/deepgmr_mn40.py:232-244 find_correspondence_one_pair, for p pairs:
+ * f1 [p, n1, c], f2 [p, n2, c] (rows = points, channels contiguous, as the
+ * numpy [n, c] arrays).  diff = |f1_i|^2 + |f2_j|^2 - 2 f1_i . f2_j;
+ * corr12 [p, n1] = argmin_j, corr21 [p, n2] = argmin_i (first index on ties,
+ * NaN first as np.argmin); idx1 / idx2 [p, n1] = the mutual pairs
+ * (corr21[corr12[i]] == i) in ascending i, -1 after count[p] of them.
+ * Channel sums are k-ordered fmaf chains (fp32 MFMA), include/pcr_math.h. */
+size_t pcr_mutual_nn_workspace_size(int p, int n1, int n2);
+pcr_status pcr_mutual_nn_match(const float *f1, const float *f2, int p, int n1, int n2, int c,
+                               int *corr12, int *corr21, int *idx1, int *idx2, int *count,
+                               void *workspace, size_t workspace_bytes, void *stream);
+
 /* ------------------------------------------------ native step runner ----
  * `steps` consecutive extractor steps (the pipelined schedule bench.py
  * measures), enqueued from native code: every launch and cross-stream event

@@ -378,4 +378,36 @@ PCR_HD void pcr_local_ppf(float cx, float cy, float cz, float cnx, float cny, fl
   out[3] = dn;
 }
 
+/* ---- feature-space mutual nearest neighbours (datasets/deepgmr_mn40.py:
+ * 232-244, find_correspondence_one_pair).  numpy computes, in fp32,
+ *   diff = norm(f1)^2 + norm(f2)^2.T - 2 f1 . f2.T
+ * with BLAS-order sums; here every sum over channels is the k-ordered fmaf
+ * chain an fp32 MFMA produces (acc = fma(a_k, b_k, acc), k ascending), so the
+ * device and this restatement agree bit for bit. ---- */
+/* norm(f)^2 as np.power(np.linalg.norm(f), 2): sqrt of the sum, squared */
+PCR_HD float pcr_match_sqnorm(const float *f, int c) {
+  float s = 0.0f, r;
+  int k;
+  for (k = 0; k < c; k++) s = __builtin_fmaf(f[k], f[k], s);
+  r = __builtin_sqrtf(s);
+  return r * r;
+}
+/* (sq1 + sq2) - 2 dot, the broadcast order of the numpy expression */
+PCR_HD float pcr_match_diff(float sq1, float sq2, float dot) {
+  return (sq1 + sq2) - 2.0f * dot;
+}
+/* ascending-unsigned key of (diff, index): np.argmin's order -- the least
+ * value, the first index among equal ones, NaN before everything (argmin
+ * returns the first NaN); -0 and +0 compare equal */
+PCR_HD unsigned long long pcr_match_key(float v, int idx) {
+  unsigned u;
+  float w = v + 0.0f; /* -0 -> +0 */
+  __builtin_memcpy(&u, &w, 4);
+  if (v != v)
+    u = 0u;
+  else
+    u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  return ((unsigned long long)u << 32) | (unsigned)idx;
+}
+
 #endif /* PCR_MATH_H */

@@ -49,6 +49,7 @@ _SIGS = {
     "orc_atanf_v": [_i, _f32p, _f32p],
     "orc_acos_d_v": [_i, _f64p, _f64p],
     "orc_sph_index_v": [_i, _f32p, _i, _i, _i32p],
+    "orc_mutual_nn": [_i, _i, _i, _i, _f32p, _f32p, _i32p, _i32p, _i32p, _i32p, _i32p],
     "orc_num_threads": [],
     "orc_set_num_threads": [_i],
 }
@@ -280,3 +281,20 @@ def sph_index(xyz, r, use_fma=True):
     ind = np.empty(n, np.int32)
     lib().orc_sph_index_v(n, xyz, r, int(bool(use_fma)), ind)
     return ind
+
+
+def mutual_nn(f1, f2):
+    """Feature-space mutual nearest neighbours (datasets/deepgmr_mn40.py:
+    232-244) of p pairs: f1 [p, n1, c], f2 [p, n2, c] -> corr12 [p, n1],
+    corr21 [p, n2], idx1 [p, n1], idx2 [p, n1] (mutual pairs first, -1
+    after), count [p]."""
+    f1, f2 = _f32(f1), _f32(f2)
+    p, n1, c = f1.shape
+    n2 = f2.shape[1]
+    corr12 = np.empty((p, n1), np.int32)
+    corr21 = np.empty((p, n2), np.int32)
+    idx1 = np.empty((p, n1), np.int32)
+    idx2 = np.empty((p, n1), np.int32)
+    count = np.empty((p,), np.int32)
+    lib().orc_mutual_nn(p, n1, n2, c, f1, f2, corr12, corr21, idx1, idx2, count)
+    return corr12, corr21, idx1, idx2, count

@@ -498,6 +498,56 @@ void orc_sph_index_v(int n, const float *xyz, int r, int use_fma, int *ind) {
   int i;
   for (i = 0; i < n; i++) ind[i] = pcr_sph_index_v(xyz[i], xyz[i + n], xyz[i + 2 * n], r, use_fma);
 }
+/* feature-space mutual nearest neighbours of p registration pairs
+ * (datasets/deepgmr_mn40.py:232-244): f1 [p][n1][c], f2 [p][n2][c];
+ * corr12 [p][n1] = argmin_j diff, corr21 [p][n2] = argmin_i diff; idx1 / idx2
+ * [p][n1] the mutual pairs in ascending i (the rest -1), count [p]. */
+void orc_mutual_nn(int p, int n1, int n2, int c, const float *f1, const float *f2, int *corr12,
+                   int *corr21, int *idx1, int *idx2, int *count) {
+  int q;
+#pragma omp parallel for schedule(dynamic)
+  for (q = 0; q < p; q++) {
+    const float *a = f1 + (size_t)q * n1 * c, *bb = f2 + (size_t)q * n2 * c;
+    float *sq1 = malloc(sizeof(float) * (size_t)n1), *sq2 = malloc(sizeof(float) * (size_t)n2);
+    unsigned long long *colbest = malloc(sizeof(unsigned long long) * (size_t)n2);
+    int i, j, k, cnt = 0;
+    int *c12 = corr12 + (size_t)q * n1, *c21 = corr21 + (size_t)q * n2;
+    for (i = 0; i < n1; i++) sq1[i] = pcr_match_sqnorm(a + (size_t)i * c, c);
+    for (j = 0; j < n2; j++) sq2[j] = pcr_match_sqnorm(bb + (size_t)j * c, c);
+    for (j = 0; j < n2; j++) colbest[j] = ~0ull;
+    for (i = 0; i < n1; i++) {
+      unsigned long long best = ~0ull;
+      for (j = 0; j < n2; j++) {
+        float dot = 0.0f;
+        unsigned long long key;
+        for (k = 0; k < c; k++)
+          dot = __builtin_fmaf(a[(size_t)i * c + k], bb[(size_t)j * c + k], dot);
+        {
+          const float d = pcr_match_diff(sq1[i], sq2[j], dot);
+          key = pcr_match_key(d, j);
+          if (key < best) best = key;
+          key = pcr_match_key(d, i);
+          if (key < colbest[j]) colbest[j] = key;
+        }
+      }
+      c12[i] = (int)(unsigned)(best & 0xFFFFFFFFull);
+    }
+    for (j = 0; j < n2; j++) c21[j] = (int)(unsigned)(colbest[j] & 0xFFFFFFFFull);
+    for (i = 0; i < n1; i++) {
+      if (c21[c12[i]] == i) {
+        idx1[(size_t)q * n1 + cnt] = i;
+        idx2[(size_t)q * n1 + cnt] = c12[i];
+        cnt++;
+      }
+    }
+    for (i = cnt; i < n1; i++) idx1[(size_t)q * n1 + i] = idx2[(size_t)q * n1 + i] = -1;
+    count[q] = cnt;
+    free(sq1);
+    free(sq2);
+    free(colbest);
+  }
+}
+
 int orc_num_threads(void) {
 #ifdef _OPENMP
   return omp_get_max_threads();

@@ -1,0 +1,218 @@
+// matching.hip -- feature-space mutual nearest neighbours of registration
+// pairs, for gfx950 (the step after the extractor in the
+// reference's registration evaluation, datasets/deepgmr_mn40.py:232-244
+// find_correspondence_one_pair):
+//   diff[i][j] = |f1_i|^2 + |f2_j|^2 - 2 f1_i . f2_j
+//   corr12 = argmin_j diff, corr21 = argmin_i diff (first index on ties)
+//   mutual: corr21[corr12[i]] == i  ->  (idx1, idx2) in ascending i.
+// The [n1, n2] cross term is a dense contraction over the channels: fp32
+// MFMA (v_mfma_f32_32x32x2_f32, exact fp32 products, a k-ordered fmaf chain)
+// on 128 x 128 tiles staged through LDS; the epilogue turns each tile into
+// per-row and per-column (diff, index) minima with wave shuffles and merges
+// them across tiles with 64-bit atomicMin on ascending keys, so the
+// [n1, n2] matrix never reaches HBM.  Numerics are restated bit for bit by
+// the oracle (include/pcr_math.h: pcr_match_*).
+#include "common.hpp"
+
+namespace pcr {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// |f|^2 per row (pcr_match_sqnorm: the sequential fmaf chain); one thread per row
+__global__ __launch_bounds__(256) void match_sqnorm_kernel(const float* __restrict__ f, int rows,
+                                                           int c, float* __restrict__ sq) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows) return;
+  sq[i] = pcr_match_sqnorm(f + i * c, c);
+}
+
+constexpr int kMT = 128;  // tile rows (f1) and columns (f2)
+constexpr int kKC = 16;   // channels per LDS stage
+constexpr int kMPad = kMT + 4;
+
+__global__ __launch_bounds__(256) void match_tile_kernel(
+    const float* __restrict__ f1, const float* __restrict__ f2, int n1, int n2, int c,
+    const float* __restrict__ sq1, const float* __restrict__ sq2,
+    unsigned long long* __restrict__ rowbest, unsigned long long* __restrict__ colbest) {
+  __shared__ float a_s[kKC][kMPad];  // [k][i]
+  __shared__ float b_s[kKC][kMPad];  // [k][j]
+  const int p = blockIdx.z;
+  const int i0 = blockIdx.y * kMT, j0 = blockIdx.x * kMT;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wi = wv >> 1, wj = wv & 1;  // 2 x 2 waves, 64 x 64 each
+  const float* A = f1 + (size_t)p * n1 * c;
+  const float* B = f2 + (size_t)p * n2 * c;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int ti = 0; ti < 2; ti++)
+#pragma unroll
+    for (int tj = 0; tj < 2; tj++)
+#pragma unroll
+      for (int v = 0; v < 16; v++) acc[ti][tj][v] = 0.0f;
+  // staging: thread t loads 8 consecutive channels of row t / 2
+  const int lr = tid >> 1, lk = (tid & 1) * 8;
+  for (int k0 = 0; k0 < c; k0 += kKC) {
+    float va[8], vb[8];
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      const int k = k0 + lk + e;
+      va[e] = (i0 + lr < n1 && k < c) ? A[(size_t)(i0 + lr) * c + k] : 0.0f;
+      vb[e] = (j0 + lr < n2 && k < c) ? B[(size_t)(j0 + lr) * c + k] : 0.0f;
+    }
+    __syncthreads();  // the previous stage's reads are done
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      a_s[lk + e][lr] = va[e];
+      b_s[lk + e][lr] = vb[e];
+    }
+    __syncthreads();
+    // k ascending: every product enters its accumulator in channel order
+#pragma unroll
+    for (int kk = 0; kk < kKC; kk += 2) {
+      const int kr = kk + (lane >> 5);
+#pragma unroll
+      for (int ti = 0; ti < 2; ti++) {
+        const float a = a_s[kr][wi * 64 + ti * 32 + (lane & 31)];
+#pragma unroll
+        for (int tj = 0; tj < 2; tj++) {
+          const float bq = b_s[kr][wj * 64 + tj * 32 + (lane & 31)];
+          acc[ti][tj] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bq, acc[ti][tj], 0, 0, 0);
+        }
+      }
+    }
+  }
+  // epilogue: C/D layout col = lane & 31, row = (v & 3) + 8 (v >> 2) + 4 (lane >> 5)
+  unsigned long long* rb = rowbest + (size_t)p * n1;
+  unsigned long long* cb = colbest + (size_t)p * n2;
+  const float* s1 = sq1 + (size_t)p * n1;
+  const float* s2 = sq2 + (size_t)p * n2;
+  unsigned long long cmin[2] = {~0ull, ~0ull};
+#pragma unroll
+  for (int ti = 0; ti < 2; ti++) {
+#pragma unroll
+    for (int v = 0; v < 16; v++) {
+      const int row = i0 + wi * 64 + ti * 32 + (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5);
+      const float sr = row < n1 ? s1[row] : 0.0f;
+      unsigned long long rmin = ~0ull;
+#pragma unroll
+      for (int tj = 0; tj < 2; tj++) {
+        const int col = j0 + wj * 64 + tj * 32 + (lane & 31);
+        if (row < n1 && col < n2) {
+          const float d = pcr_match_diff(sr, s2[col], acc[ti][tj][v]);
+          const unsigned long long kr = pcr_match_key(d, col);
+          const unsigned long long kc = pcr_match_key(d, row);
+          rmin = kr < rmin ? kr : rmin;
+          cmin[tj] = kc < cmin[tj] ? kc : cmin[tj];
+        }
+      }
+      // min over the 32 columns of this lane half
+#pragma unroll
+      for (int off = 16; off > 0; off >>= 1) {
+        const unsigned long long o = shfl_xor_u64(rmin, off);
+        rmin = o < rmin ? o : rmin;
+      }
+      if ((lane & 31) == 0 && row < n1) atomicMin(rb + row, rmin);
+    }
+  }
+#pragma unroll
+  for (int tj = 0; tj < 2; tj++) {
+    const unsigned long long o = shfl_xor_u64(cmin[tj], 32);
+    const unsigned long long m = o < cmin[tj] ? o : cmin[tj];
+    const int col = j0 + wj * 64 + tj * 32 + lane;
+    if (lane < 32 && col < n2) atomicMin(cb + col, m);
+  }
+}
+
+// corr12 / corr21 from the minima; mutual pairs compacted in ascending i
+// (one workgroup per pair)
+__global__ __launch_bounds__(1024) void match_finalize_kernel(
+    const unsigned long long* __restrict__ rowbest, const unsigned long long* __restrict__ colbest,
+    int n1, int n2, int* __restrict__ corr12, int* __restrict__ corr21, int* __restrict__ idx1,
+    int* __restrict__ idx2, int* __restrict__ count) {
+  __shared__ int scan_s[1024 / kWave + 1];
+  const int p = blockIdx.x, tid = threadIdx.x;
+  const unsigned long long* rb = rowbest + (size_t)p * n1;
+  const unsigned long long* cb = colbest + (size_t)p * n2;
+  int* c12 = corr12 + (size_t)p * n1;
+  int* c21 = corr21 + (size_t)p * n2;
+  for (int j = tid; j < n2; j += 1024) c21[j] = (int)(unsigned)(cb[j] & 0xFFFFFFFFull);
+  int base = 0;
+  for (int i0 = 0; i0 < n1; i0 += 1024) {
+    const int i = i0 + tid;
+    int m = 0, ci = 0;
+    if (i < n1) {
+      ci = (int)(unsigned)(rb[i] & 0xFFFFFFFFull);
+      c12[i] = ci;
+      m = (ci >= 0 && ci < n2 && (int)(unsigned)(cb[ci] & 0xFFFFFFFFull) == i) ? 1 : 0;
+    }
+    const int incl = block_inclusive_scan(m, scan_s);
+    if (m) {
+      idx1[(size_t)p * n1 + base + incl - 1] = i;
+      idx2[(size_t)p * n1 + base + incl - 1] = ci;
+    }
+    __shared__ int tot_s;
+    if (tid == 1023) tot_s = incl;
+    __syncthreads();
+    base += tot_s;
+    __syncthreads();
+  }
+  for (int i = base + tid; i < n1; i += 1024) idx1[(size_t)p * n1 + i] = idx2[(size_t)p * n1 + i] = -1;
+  if (tid == 0) count[p] = base;
+}
+
+static size_t match_ws_layout(int p, int n1, int n2, float** sq1, float** sq2,
+                              unsigned long long** rb, unsigned long long** cb, char* base) {
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    char* q = base ? base + off : nullptr;
+    off = (off + bytes + 255) / 256 * 256;
+    return q;
+  };
+  float* a = (float*)take((size_t)p * n1 * 4);
+  float* b = (float*)take((size_t)p * n2 * 4);
+  unsigned long long* r = (unsigned long long*)take((size_t)p * n1 * 8);
+  unsigned long long* c = (unsigned long long*)take((size_t)p * n2 * 8);
+  if (sq1) {
+    *sq1 = a;
+    *sq2 = b;
+    *rb = r;
+    *cb = c;
+  }
+  return off;
+}
+
+}  // namespace pcr
+
+using namespace pcr;
+
+extern "C" size_t pcr_mutual_nn_workspace_size(int p, int n1, int n2) {
+  if (p <= 0 || n1 <= 0 || n2 <= 0) return 256;
+  return match_ws_layout(p, n1, n2, nullptr, nullptr, nullptr, nullptr, nullptr);
+}
+
+extern "C" pcr_status pcr_mutual_nn_match(const float* f1, const float* f2, int p, int n1, int n2,
+                                          int c, int* corr12, int* corr21, int* idx1, int* idx2,
+                                          int* count, void* workspace, size_t workspace_bytes,
+                                          void* stream) {
+  PCR_REQUIRE(p >= 0 && n1 >= 1 && n2 >= 1 && c >= 1, "mutual_nn_match: invalid sizes");
+  PCR_REQUIRE(p <= 65535, "mutual_nn_match: too many pairs (%d)", p);
+  if (p == 0) return PCR_OK;
+  float *sq1, *sq2;
+  unsigned long long *rb, *cb;
+  const size_t need = match_ws_layout(p, n1, n2, &sq1, &sq2, &rb, &cb, (char*)workspace);
+  PCR_REQUIRE(workspace != nullptr && workspace_bytes >= need,
+              "mutual_nn_match: workspace too small (%zu < %zu)", workspace_bytes, need);
+  hipStream_t st = as_stream(stream);
+  if (hipMemsetAsync(rb, 0xFF, (size_t)p * n1 * 8, st) != hipSuccess ||
+      hipMemsetAsync(cb, 0xFF, (size_t)p * n2 * 8, st) != hipSuccess)
+    return launch_status("mutual_nn_match memset");
+  hipLaunchKernelGGL(match_sqnorm_kernel, dim3((unsigned)ceil_div64((int64_t)p * n1, 256)),
+                     dim3(256), 0, st, f1, p * n1, c, sq1);
+  hipLaunchKernelGGL(match_sqnorm_kernel, dim3((unsigned)ceil_div64((int64_t)p * n2, 256)),
+                     dim3(256), 0, st, f2, p * n2, c, sq2);
+  hipLaunchKernelGGL(match_tile_kernel, dim3(ceil_div(n2, kMT), ceil_div(n1, kMT), p), dim3(256),
+                     0, st, f1, f2, n1, n2, c, sq1, sq2, rb, cb);
+  hipLaunchKernelGGL(match_finalize_kernel, dim3(p), dim3(1024), 0, st, rb, cb, n1, n2, corr12,
+                     corr21, idx1, idx2, count);
+  return launch_status("mutual_nn_match");
+}

@@ -1499,15 +1499,23 @@ extern "C" pcr_status pcr_extractor_voxel_means_devox(const float* features, int
   const int tile = ((r3 + 31) / 32) * 32;
   const int nw = tile / 32 + 1;
   static const int mv = getenv("PCR_MEANS_V") ? atoi(getenv("PCR_MEANS_V")) : 3;
+  static const int mg = getenv("PCR_MEANS_G") ? atoi(getenv("PCR_MEANS_G")) : 2;
   if (mv == 3 && n <= kMeansMaxN) {
-    // two channels per workgroup: ~24 KB of LDS, so it fits beside the
-    // KNN selection's workgroups
-    constexpr int G = 2;
-    const int ngrp = ceil_div(c, G);
-    const size_t smem = ((size_t)G * n + (size_t)G * (n + 1) + n + (n + 1)) * 4;
-    allow_big_lds(vox_means_kernel<G>, smem);
-    hipLaunchKernelGGL((vox_means_kernel<G>), dim3(ngrp * b), dim3(kMeansNT), smem,
-                       as_stream(stream), features, c, n, ws, dwgts, devox, desc, ngrp);
+    // G channels per workgroup (G = 2: ~24 KB of LDS, so it fits beside the
+    // KNN selection's workgroups); every workgroup of a cloud reads the
+    // cloud's corner data, so a larger G reads less of it in all
+#define PCR_LAUNCH_MEANS(GV)                                                                  \
+  do {                                                                                       \
+    const int ngrp = ceil_div(c, GV);                                                        \
+    const size_t smem = ((size_t)GV * n + (size_t)GV * (n + 1) + n + (n + 1)) * 4;           \
+    allow_big_lds(vox_means_kernel<GV>, smem);                                               \
+    hipLaunchKernelGGL((vox_means_kernel<GV>), dim3(ngrp * b), dim3(kMeansNT), smem,         \
+                       as_stream(stream), features, c, n, ws, dwgts, devox, desc, ngrp);     \
+  } while (0)
+    if (mg == 4) PCR_LAUNCH_MEANS(4);
+    else if (mg == 8) PCR_LAUNCH_MEANS(8);
+    else PCR_LAUNCH_MEANS(2);
+#undef PCR_LAUNCH_MEANS
     return launch_status(name);
   }
   int G = 1;

@@ -51,6 +51,8 @@ SIGNATURES = {
     "pcr_extractor_voxel_means_devox": (ST, [P, I, I, I, I, P, P, P, P, P, SZ, P]),
     "pcr_extractor_voxel_stream": (ST, [I, I, I, I, P, P, P, SZ, P]),
     "pcr_extractor_run": (ST, [P, I, I, P, P, P, P, P]),
+    "pcr_mutual_nn_workspace_size": (SZ, [I, I, I]),
+    "pcr_mutual_nn_match": (ST, [P, P, I, I, I, I, P, P, P, P, P, P, SZ, P]),
     "pcr_selftest_math": (ST, [I, P, P, I, I, P, P, P]),
     "pcr_selftest_math_d": (ST, [I, P, P, I, P, P]),
 }

@@ -349,3 +349,39 @@ three_nearest_neighbors_interpolate_forward = _out_of_scope(
     "three_nearest_neighbors_interpolate_forward")
 three_nearest_neighbors_interpolate_backward = _out_of_scope(
     "three_nearest_neighbors_interpolate_backward")
+
+
+def mutual_nn_match(feat1, feat2):
+    """Feature-space mutual nearest neighbours of p registration pairs
+    (datasets/deepgmr_mn40.py:232-244, batched): feat1 [p, n1, c],
+    feat2 [p, n2, c] -> (corr12 [p, n1], corr21 [p, n2], idx1 [p, n1],
+    idx2 [p, n1], count [p]); the first count[q] entries of idx1[q] / idx2[q]
+    are the mutual pairs in ascending idx1, the rest -1."""
+    _check(feat1, "feat1")
+    _check(feat2, "feat2")
+    if feat1.dim() != 3 or feat2.dim() != 3 or feat1.shape[0] != feat2.shape[0] or \
+            feat1.shape[2] != feat2.shape[2]:
+        raise RuntimeError("mutual_nn_match: expected feat1 [p, n1, c] and feat2 [p, n2, c]")
+    p, n1, c = feat1.shape
+    n2 = feat2.shape[1]
+    dev = feat1.device
+    i32 = dict(dtype=torch.int32, device=dev)
+    corr12, corr21 = torch.empty((p, n1), **i32), torch.empty((p, n2), **i32)
+    idx1, idx2 = torch.empty((p, n1), **i32), torch.empty((p, n1), **i32)
+    count = torch.empty((p,), **i32)
+    lib = _lib.load()
+    ws = torch.empty(max(256, lib.pcr_mutual_nn_workspace_size(p, n1, n2)), dtype=torch.uint8,
+                     device=dev)
+    _lib.check(lib.pcr_mutual_nn_match(
+        _ptr(feat1), _ptr(feat2), p, n1, n2, c, _ptr(corr12), _ptr(corr21), _ptr(idx1),
+        _ptr(idx2), _ptr(count), _ptr(ws), ws.numel(), _stream()), "mutual_nn_match")
+    return corr12, corr21, idx1, idx2, count
+
+
+def find_correspondence_one_pair(feat1, feat2):
+    """datasets/deepgmr_mn40.py:232-244 on the GPU: feat1 [n1, c],
+    feat2 [n2, c] -> (idx1, idx2), the mutual nearest neighbours in feature
+    space (int64 tensors on the features' device, ascending idx1)."""
+    _, _, idx1, idx2, count = mutual_nn_match(feat1.unsqueeze(0), feat2.unsqueeze(0))
+    n = int(count[0].item())
+    return idx1[0, :n].long(), idx2[0, :n].long()
