@@ -256,6 +256,48 @@ pcr_status pcr_mutual_nn_match(const float *f1, const float *f2, int p, int n1, 
                                int *corr12, int *corr21, int *idx1, int *idx2, int *count,
                                void *workspace, size_t workspace_bytes, void *stream);
 
+/* ------------------------------------ LRF change_coords (8f f2) ----------
+ * models/pvcnn_classify.py:153-184 (rot_invariant_preprocess ==
+ * 'change_coords'), one cloud per workgroup, no host round trip.
+ * Per cloud: nc = coords - mean (the fp64 mean reduction order is given in
+ * oracle/pcr_oracle.c orc_lrf); base_x = the point of largest norm; base_y =
+ * the next point in descending-norm rank with norm >= 1e-5 and
+ * |<base_x, p/|p|>| < 0.9; Gram-Schmidt, base_z = x cross y; new_coords =
+ * basis . nc.  Rank ties go to the lower index.
+ *   coords [b,3,n] -> new_coords [b,3,n], basis [b,3,3] (rows x, y, z),
+ *   picks [b,2] (base_x, base_y point indices), status [b]: 0 ok, 1 base_x
+ *   norm <= 1e-5, 2 no base_y, 3 degenerate Gram-Schmidt.  These are the
+ *   reference's asserts; the host shim raises on them. */
+pcr_status pcr_lrf_change_coords(const float *coords, int b, int n, float *new_coords,
+                                 float *basis, int *picks, int *status, void *stream);
+
+/* --------------------------------- PointNet++ ops (8f f4) ----------------
+ * sampling/sampling.cpp:6-58 gather_features_forward / _backward and
+ * furthest_point_sampling_forward; interpolate/neighbor_interpolate.cpp:
+ * 6-65 three_nearest_neighbors_interpolate_forward / _backward. */
+/* features [b,c,n], indices [b,m] -> out [b,c,m] (indices outside [0,n)
+ * read 0; the reference reads out of bounds there) */
+pcr_status pcr_gather_features_forward(const float *features, const int *indices, int b, int c,
+                                       int n, int m, float *out, void *stream);
+/* grad_y [b,c,m] -> grad_x [b,c,n] (zeroed here, then scatter-added) */
+pcr_status pcr_gather_features_backward(const float *grad_y, const int *indices, int b, int c,
+                                        int n, int m, float *grad_x, void *stream);
+/* coords [b,3,n] -> indices [b,m].  Tie order as the reference's
+ * 512-thread reduction (pcr_fps_key).  workspace: pcr_fps_workspace_size. */
+size_t pcr_fps_workspace_size(int b, int n);
+pcr_status pcr_furthest_point_sampling(const float *coords, int b, int n, int m, int *indices,
+                                       void *workspace, size_t workspace_bytes, void *stream);
+/* points [b,3,n], centers [b,3,m], centers_features [b,c,m] ->
+ * out [b,c,n], indices [b,3,n], weights [b,3,n] */
+pcr_status pcr_three_nn_interpolate_forward(const float *points, const float *centers,
+                                            const float *centers_features, int b, int c, int m,
+                                            int n, float *out, int *indices, float *weights,
+                                            void *stream);
+/* grad_y [b,c,n] -> grad_x [b,c,m] (zeroed here, then scatter-added) */
+pcr_status pcr_three_nn_interpolate_backward(const float *grad_y, const int *indices,
+                                             const float *weights, int b, int c, int n, int m,
+                                             float *grad_x, void *stream);
+
 /* ------------------------------------------------ native step runner ----
  * `steps` consecutive extractor steps (the pipelined schedule bench.py
  * measures), enqueued from native code: every launch and cross-stream event

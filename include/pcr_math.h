@@ -410,4 +410,130 @@ PCR_HD unsigned long long pcr_match_key(float v, int idx) {
   return ((unsigned long long)u << 32) | (unsigned)idx;
 }
 
+/* ---- furthest point sampling (sampling/sampling.cu:87-173).  Each sample
+ * step keeps min(d, dist) per point and picks the farthest point.  The
+ * reference's 512 threads each take points t, t+512, ... and keep the first
+ * strict maximum; the LDS tree keeps the left entry on ties.  The winner is
+ * therefore the largest d2, then the smallest k % 512, then the smallest k.
+ * This key orders exactly that way under an unsigned max (d2 >= 0). ---- */
+PCR_HD unsigned long long pcr_fps_key(float d2, int k) {
+  unsigned u, rank = ((unsigned)(k & 511) << 22) | ((unsigned)k >> 9);
+  __builtin_memcpy(&u, &d2, 4);
+  return ((unsigned long long)u << 32) | (unsigned)(0xFFFFFFFFu - rank);
+}
+PCR_HD int pcr_fps_key_index(unsigned long long key) {
+  unsigned rank = 0xFFFFFFFFu - (unsigned)(key & 0xFFFFFFFFull);
+  return (int)(((rank & 0x3FFFFFu) << 9) | (rank >> 22));
+}
+
+/* ---- three nearest neighbours (interpolate/neighbor_interpolate.cu:21-76).
+ * The reference keeps best0..2 in double, but they only ever hold fp32
+ * distances or the 1e40 init.  Its clamp and the double products of two
+ * floats rounded back to float equal fp32 min/max and multiplies. So the
+ * weights are computed in fp32 here, with +inf for "no centre yet". ---- */
+PCR_HD void pcr_three_nn_insert(float d, int k, float best[3], int besti[3]) {
+  if (d < best[2]) {
+    best[2] = d;
+    besti[2] = k;
+    if (d < best[1]) {
+      best[2] = best[1];
+      besti[2] = besti[1];
+      best[1] = d;
+      besti[1] = k;
+      if (d < best[0]) {
+        best[1] = best[0];
+        besti[1] = besti[0];
+        best[0] = d;
+        besti[0] = k;
+      }
+    }
+  }
+}
+PCR_HD void pcr_three_nn_weights(const float best[3], float w[3]) {
+  float b0 = best[0] < 1e10f ? best[0] : 1e10f;
+  float b1 = best[1] < 1e10f ? best[1] : 1e10f;
+  float b2 = best[2] < 1e10f ? best[2] : 1e10f;
+  float d0d1, d0d2, d1d2, inv;
+  b0 = b0 > 1e-10f ? b0 : 1e-10f;
+  b1 = b1 > 1e-10f ? b1 : 1e-10f;
+  b2 = b2 > 1e-10f ? b2 : 1e-10f;
+  d0d1 = b0 * b1;
+  d0d2 = b0 * b2;
+  d1d2 = b1 * b2;
+  inv = 1.0f / ((d0d1 + d0d2) + d1d2);
+  w[0] = d1d2 * inv;
+  w[1] = d0d2 * inv;
+  w[2] = d0d1 * inv;
+}
+/* f1*w1 + f2*w2 + f3*w3 (neighbor_interpolate.cu:112-114, nvcc-FMA) */
+PCR_HD float pcr_wsum3(float f0, float w0, float f1, float w1, float f2, float w2) {
+  return __builtin_fmaf(f2, w2, __builtin_fmaf(f0, w0, f1 * w1));
+}
+
+/* ---- LRF "change_coords" (models/pvcnn_classify.py:153-184).  PyTorch
+ * elementwise ops do not contract, so the basis arithmetic below is unfused.
+ * Rank order is descending norm, ties by ascending index (the reference's
+ * unstable argsort leaves ties open). ---- */
+PCR_HD float pcr_norm3f(float x, float y, float z) {
+  return __builtin_sqrtf(pcr_sumsq3f_nofma(x, y, z));
+}
+PCR_HD float pcr_dot3f_nofma(float a0, float a1, float a2, float b0, float b1, float b2) {
+  float p0 = a0 * b0, p1 = a1 * b1, p2 = a2 * b2;
+  float s = p0 + p1;
+  return s + p2;
+}
+/* larger key = earlier in the descending-norm rank; NaN norms never win */
+PCR_HD unsigned long long pcr_rank_key(float nrm, int idx) {
+  unsigned u;
+  if (!(nrm >= 0.0f)) return 0ull;
+  __builtin_memcpy(&u, &nrm, 4);
+  return ((unsigned long long)(u + 1u) << 32) | (unsigned)(0xFFFFFFFFu - (unsigned)idx);
+}
+PCR_HD int pcr_rank_key_index(unsigned long long key) {
+  return (int)(0xFFFFFFFFu - (unsigned)(key & 0xFFFFFFFFull));
+}
+/* Does rank entry p (norm nrm) qualify as base_y for base_x bx?
+ * (pvcnn_classify.py:163-168).  Python floats compare against the fp32
+ * tensors in fp32. */
+PCR_HD int pcr_lrf_base_y_ok(float px, float py, float pz, float nrm, const float bx[3]) {
+  float lam;
+  if (nrm < 1e-5f) return 0;
+  lam = pcr_dot3f_nofma(bx[0], bx[1], bx[2], px / nrm, py / nrm, pz / nrm);
+  return lam < 0.9f && lam > -0.9f;
+}
+/* Gram-Schmidt + cross (pvcnn_classify.py:176-182): basis rows x, y, z.
+ * Returns 0, or 3 when the reference's orthogonality assert would fire. */
+PCR_HD int pcr_lrf_basis(const float p0[3], float n0, const float p1[3], float n1,
+                         float basis[9]) {
+  float bx[3], by[3], bz[3], t, nx, nz;
+  int a;
+  for (a = 0; a < 3; a++) {
+    bx[a] = p0[a] / n0;
+    by[a] = p1[a] / n1;
+  }
+  t = pcr_dot3f_nofma(bx[0], bx[1], bx[2], by[0], by[1], by[2]);
+  for (a = 0; a < 3; a++) {
+    float m = by[a] * t;
+    bx[a] = bx[a] - m;
+  }
+  nx = __builtin_sqrtf(pcr_sumsq3f_nofma(bx[0], bx[1], bx[2]));
+  if (nx < 1e-5f) return 3;
+  for (a = 0; a < 3; a++) bx[a] = bx[a] / nx;
+  {
+    float c0a = bx[1] * by[2], c0b = bx[2] * by[1];
+    float c1a = bx[2] * by[0], c1b = bx[0] * by[2];
+    float c2a = bx[0] * by[1], c2b = bx[1] * by[0];
+    bz[0] = c0a - c0b;
+    bz[1] = c1a - c1b;
+    bz[2] = c2a - c2b;
+  }
+  nz = __builtin_sqrtf(pcr_sumsq3f_nofma(bz[0], bz[1], bz[2]));
+  for (a = 0; a < 3; a++) {
+    basis[a] = bx[a];
+    basis[3 + a] = by[a];
+    basis[6 + a] = bz[a] / nz;
+  }
+  return 0;
+}
+
 #endif /* PCR_MATH_H */

@@ -50,6 +50,12 @@ _SIGS = {
     "orc_acos_d_v": [_i, _f64p, _f64p],
     "orc_sph_index_v": [_i, _f32p, _i, _i, _i32p],
     "orc_mutual_nn": [_i, _i, _i, _i, _f32p, _f32p, _i32p, _i32p, _i32p, _i32p, _i32p],
+    "orc_lrf": [_i, _i, _f32p, _f32p, _f32p, _i32p, _i32p],
+    "orc_gather": [_i, _i, _i, _i, _f32p, _i32p, _f32p],
+    "orc_gather_grad": [_i, _i, _i, _i, _f32p, _i32p, _f32p],
+    "orc_fps": [_i, _i, _i, _f32p, _i32p],
+    "orc_three_nn": [_i, _i, _i, _i, _f32p, _f32p, _f32p, _f32p, _i32p, _f32p],
+    "orc_three_nn_grad": [_i, _i, _i, _i, _f32p, _i32p, _f32p, _f32p],
     "orc_num_threads": [],
     "orc_set_num_threads": [_i],
 }
@@ -298,3 +304,65 @@ def mutual_nn(f1, f2):
     count = np.empty((p,), np.int32)
     lib().orc_mutual_nn(p, n1, n2, c, f1, f2, corr12, corr21, idx1, idx2, count)
     return corr12, corr21, idx1, idx2, count
+
+
+# ------------------------------------------------ LRF change_coords (f2)
+def lrf_change_coords(coords):
+    """models/pvcnn_classify.py:153-184: coords [b, 3, n] -> (new_coords
+    [b, 3, n], basis [b, 3, 3] rows x/y/z, picks [b, 2], status [b])."""
+    coords = _f32(coords)
+    b, _, n = coords.shape
+    out = np.empty_like(coords)
+    basis = np.empty((b, 3, 3), np.float32)
+    picks = np.empty((b, 2), np.int32)
+    status = np.empty((b,), np.int32)
+    lib().orc_lrf(b, n, coords, out, basis, picks, status)
+    return out, basis, picks, status
+
+
+# ------------------------------------------------ PointNet++ ops (f4)
+def gather_features_forward(features, indices):
+    """sampling.cpp gather_features_forward: [b, c, n] x [b, m] -> [b, c, m]."""
+    features, indices = _f32(features), _i32(indices)
+    b, c, n = features.shape
+    m = indices.shape[1]
+    out = np.empty((b, c, m), np.float32)
+    lib().orc_gather(b, c, n, m, features, indices, out)
+    return out
+
+
+def gather_features_backward(grad_y, indices, n):
+    grad_y, indices = _f32(grad_y), _i32(indices)
+    b, c, m = grad_y.shape
+    gx = np.empty((b, c, n), np.float32)
+    lib().orc_gather_grad(b, c, n, m, grad_y, indices, gx)
+    return gx
+
+
+def furthest_point_sampling(coords, m):
+    coords = _f32(coords)
+    b, _, n = coords.shape
+    idx = np.zeros((b, m), np.int32)
+    lib().orc_fps(b, n, m, coords, idx)
+    return idx
+
+
+def three_nearest_neighbors_interpolate_forward(points, centers, centers_features):
+    """neighbor_interpolate.cpp: -> (out [b, c, n], indices [b, 3, n],
+    weights [b, 3, n])."""
+    points, centers, cf = _f32(points), _f32(centers), _f32(centers_features)
+    b, c, m = cf.shape
+    n = points.shape[2]
+    out = np.empty((b, c, n), np.float32)
+    inds = np.empty((b, 3, n), np.int32)
+    wgts = np.empty((b, 3, n), np.float32)
+    lib().orc_three_nn(b, c, m, n, points, centers, cf, out, inds, wgts)
+    return out, inds, wgts
+
+
+def three_nearest_neighbors_interpolate_backward(grad_y, indices, weights, m):
+    grad_y, indices, weights = _f32(grad_y), _i32(indices), _f32(weights)
+    b, c, n = grad_y.shape
+    gx = np.empty((b, c, m), np.float32)
+    lib().orc_three_nn_grad(b, c, n, m, grad_y, indices, weights, gx)
+    return gx

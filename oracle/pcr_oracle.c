@@ -548,6 +548,227 @@ void orc_mutual_nn(int p, int n1, int n2, int c, const float *f1, const float *f
   }
 }
 
+/* ------------------------------------------------ LRF change_coords (f2) */
+/* models/pvcnn_classify.py:153-184, restated literally: a stable descending
+ * sort of the norms (ties by ascending index; the reference's argsort leaves
+ * ties open), then the Python loop over the ranking, then Gram-Schmidt and the
+ * projection.  The GPU kernel (csrc/lrf.hip) replaces the sort by two
+ * arg-max passes.  This restatement is the independent check of that.  The mean
+ * uses the kernel's fixed fp64 order: lane t of 256 sums points t, t+256, ...;
+ * each group of 64 lanes is halved (l += l+s, s = 32..1); the 4 group sums
+ * combine as (g0 + g2) + (g1 + g3).  status: 0 ok, 1/2/3 = the asserts at
+ * :159, :169, :177. */
+static double lrf_axis_sum(const float *x, int n) {
+  double part[256], g[4];
+  int t, s, w;
+  for (t = 0; t < 256; t++) {
+    double acc = 0.0;
+    int i;
+    for (i = t; i < n; i += 256) acc += (double)x[i];
+    part[t] = acc;
+  }
+  for (w = 0; w < 4; w++) {
+    double *l = part + 64 * w;
+    for (s = 32; s > 0; s >>= 1)
+      for (t = 0; t < s; t++) l[t] += l[t + s];
+    g[w] = l[0];
+  }
+  return (g[0] + g[2]) + (g[1] + g[3]);
+}
+
+static const float *lrf_sort_norms;
+static int lrf_rank_cmp(const void *pa, const void *pb) {
+  int a = *(const int *)pa, b = *(const int *)pb;
+  float na = lrf_sort_norms[a], nb = lrf_sort_norms[b];
+  int a_nan = !(na == na), b_nan = !(nb == nb);
+  if (a_nan != b_nan) return a_nan - b_nan; /* NaN last */
+  if (!a_nan && na != nb) return na > nb ? -1 : 1;
+  return a - b;
+}
+
+void orc_lrf(int b, int n, const float *coords, float *new_coords, float *basis, int *picks,
+             int *status) {
+  int bi;
+#pragma omp parallel for schedule(dynamic)
+  for (bi = 0; bi < b; bi++) {
+    const float *X = coords + (size_t)bi * 3 * n;
+    float *O = new_coords + (size_t)bi * 3 * n;
+    float *nc = (float *)malloc(sizeof(float) * 3 * n), *nr = (float *)malloc(sizeof(float) * n);
+    int *rank = (int *)malloc(sizeof(int) * n);
+    float mean[3], B[9], p0[3], p1[3], n0, n1 = 0.0f, bx[3];
+    int a, i, j, st = 0, i0 = -1, i1 = -1;
+    for (a = 0; a < 3; a++) mean[a] = (float)(lrf_axis_sum(X + (size_t)a * n, n) / (double)n);
+    for (i = 0; i < n; i++) {
+      for (a = 0; a < 3; a++) nc[i + a * n] = X[i + a * n] - mean[a];
+      nr[i] = pcr_norm3f(nc[i], nc[i + n], nc[i + 2 * n]);
+      rank[i] = i;
+    }
+#pragma omp critical(lrf_sort)
+    {
+      lrf_sort_norms = nr;
+      qsort(rank, n, sizeof(int), lrf_rank_cmp);
+    }
+    for (a = 0; a < 9; a++) B[a] = 0.0f;
+    i0 = rank[0];
+    if (!(nr[i0] == nr[i0])) i0 = -1; /* every norm NaN */
+    if (i0 < 0) {
+      st = 1;
+    } else {
+      for (a = 0; a < 3; a++) p0[a] = nc[i0 + a * n];
+      n0 = nr[i0];
+      if (!(n0 > 1e-5f)) st = 1;
+      for (a = 0; a < 3; a++) bx[a] = p0[a] / n0;
+    }
+    if (st == 0) {
+      for (j = 1; j < n; j++) {
+        int q = rank[j];
+        if (!(nr[q] == nr[q])) break; /* NaN ranks after every number */
+        if (pcr_lrf_base_y_ok(nc[q], nc[q + n], nc[q + 2 * n], nr[q], bx)) {
+          i1 = q;
+          break;
+        }
+      }
+      if (i1 < 0) {
+        st = 2;
+      } else {
+        for (a = 0; a < 3; a++) p1[a] = nc[i1 + a * n];
+        n1 = nr[i1];
+        st = pcr_lrf_basis(p0, n0, p1, n1, B);
+      }
+    }
+    if (st != 0)
+      for (a = 0; a < 9; a++) B[a] = 0.0f;
+    for (i = 0; i < n; i++)
+      for (a = 0; a < 3; a++)
+        O[i + a * n] = pcr_dot3f_nofma(B[3 * a], B[3 * a + 1], B[3 * a + 2], nc[i], nc[i + n],
+                                       nc[i + 2 * n]);
+    for (a = 0; a < 9; a++) basis[(size_t)bi * 9 + a] = B[a];
+    picks[2 * bi] = i0;
+    picks[2 * bi + 1] = i1;
+    status[bi] = st;
+    free(nc);
+    free(nr);
+    free(rank);
+  }
+}
+
+/* ------------------------------------------------ PointNet++ ops (f4) */
+/* sampling.cu:18-32 (indices outside [0, n) give 0 here) */
+void orc_gather(int b, int c, int n, int m, const float *feat, const int *idx, float *out) {
+  int bi, ch, j;
+  for (bi = 0; bi < b; bi++)
+    for (ch = 0; ch < c; ch++)
+      for (j = 0; j < m; j++) {
+        int i = idx[(size_t)bi * m + j];
+        out[((size_t)bi * c + ch) * m + j] =
+            (i >= 0 && i < n) ? feat[((size_t)bi * c + ch) * n + i] : 0.0f;
+      }
+}
+/* sampling.cu:53-67, accumulated in ascending j */
+void orc_gather_grad(int b, int c, int n, int m, const float *gy, const int *idx, float *gx) {
+  int bi, ch, j;
+  memset(gx, 0, sizeof(float) * (size_t)b * c * n);
+  for (bi = 0; bi < b; bi++)
+    for (ch = 0; ch < c; ch++)
+      for (j = 0; j < m; j++) {
+        int i = idx[(size_t)bi * m + j];
+        if (i >= 0 && i < n) gx[((size_t)bi * c + ch) * n + i] += gy[((size_t)bi * c + ch) * m + j];
+      }
+}
+/* sampling.cu:87-173 with its 512-thread structure kept: thread t scans
+ * points t, t+512, ... keeping the first strict maximum of min(d, dist)
+ * (best starts at -1); the LDS tree keeps the left entry unless it is
+ * strictly smaller.  The GPU encodes the same order in pcr_fps_key. */
+void orc_fps(int b, int n, int m, const float *coords, int *indices) {
+  int bi;
+#pragma omp parallel for schedule(dynamic)
+  for (bi = 0; bi < b; bi++) {
+    const float *X = coords + (size_t)bi * 3 * n;
+    int *out = indices + (size_t)bi * m;
+    float *dist = (float *)malloc(sizeof(float) * n), best[512];
+    int bidx[512], i, j, t, u, old = 0;
+    if (m <= 0) {
+      free(dist);
+      continue;
+    }
+    for (i = 0; i < n; i++) dist[i] = 1e38f;
+    out[0] = 0;
+    for (j = 1; j < m; j++) {
+      float x1 = X[old], y1 = X[old + n], z1 = X[old + 2 * n];
+      for (t = 0; t < 512; t++) {
+        int k;
+        best[t] = -1.0f;
+        bidx[t] = 0;
+        for (k = t; k < n; k += 512) {
+          float d = pcr_sumsq3f(X[k] - x1, X[k + n] - y1, X[k + 2 * n] - z1);
+          float d2 = (d < dist[k] || dist[k] != dist[k]) ? d : dist[k]; /* fminf */
+          if (d != d) d2 = dist[k];
+          dist[k] = d2;
+          if (d2 > best[t]) {
+            best[t] = d2;
+            bidx[t] = k;
+          }
+        }
+      }
+      for (u = 0; (1 << u) < 512; u++)
+        for (t = 0; t < (512 >> (u + 1)); t++) {
+          int a = (t * 2) << u, c2 = (t * 2 + 1) << u;
+          if (best[a] < best[c2]) {
+            best[a] = best[c2];
+            bidx[a] = bidx[c2];
+          }
+        }
+      old = bidx[0];
+      out[j] = old;
+    }
+    free(dist);
+  }
+}
+/* neighbor_interpolate.cu:21-76 (3-NN + weights) and :91-117 (interpolate) */
+void orc_three_nn(int b, int c, int m, int n, const float *points, const float *centers,
+                  const float *cfeat, float *out, int *inds, float *wgts) {
+  int bi;
+#pragma omp parallel for schedule(dynamic)
+  for (bi = 0; bi < b; bi++) {
+    const float *P = points + (size_t)bi * 3 * n, *C = centers + (size_t)bi * 3 * m;
+    const float *F = cfeat + (size_t)bi * c * m;
+    int j, q, ch, a;
+    for (j = 0; j < n; j++) {
+      float best[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()}, w[3];
+      int besti[3] = {0, 0, 0};
+      for (q = 0; q < m; q++) {
+        float d = pcr_sumsq3f(P[j] - C[q], P[j + n] - C[q + m], P[j + 2 * n] - C[q + 2 * m]);
+        pcr_three_nn_insert(d, q, best, besti);
+      }
+      pcr_three_nn_weights(best, w);
+      for (a = 0; a < 3; a++) {
+        wgts[(size_t)bi * 3 * n + a * n + j] = w[a];
+        inds[(size_t)bi * 3 * n + a * n + j] = besti[a];
+      }
+      for (ch = 0; ch < c; ch++) {
+        const float *f = F + (size_t)ch * m;
+        out[((size_t)bi * c + ch) * n + j] =
+            m > 0 ? pcr_wsum3(f[besti[0]], w[0], f[besti[1]], w[1], f[besti[2]], w[2]) : 0.0f;
+      }
+    }
+  }
+}
+/* neighbor_interpolate.cu:146-171, accumulated in ascending point order */
+void orc_three_nn_grad(int b, int c, int n, int m, const float *gy, const int *inds,
+                       const float *wgts, float *gx) {
+  int bi, ch, j, a;
+  memset(gx, 0, sizeof(float) * (size_t)b * c * m);
+  for (bi = 0; bi < b; bi++)
+    for (ch = 0; ch < c; ch++)
+      for (j = 0; j < n; j++)
+        for (a = 0; a < 3; a++) {
+          int i = inds[(size_t)bi * 3 * n + a * n + j];
+          if (i >= 0 && i < m)
+            gx[((size_t)bi * c + ch) * m + i] +=
+                wgts[(size_t)bi * 3 * n + a * n + j] * gy[((size_t)bi * c + ch) * n + j];
+        }
+}
+
 int orc_num_threads(void) {
 #ifdef _OPENMP
   return omp_get_max_threads();

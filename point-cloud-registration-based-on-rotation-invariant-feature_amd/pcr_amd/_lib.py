@@ -53,6 +53,13 @@ SIGNATURES = {
     "pcr_extractor_run": (ST, [P, I, I, P, P, P, P, P]),
     "pcr_mutual_nn_workspace_size": (SZ, [I, I, I]),
     "pcr_mutual_nn_match": (ST, [P, P, I, I, I, I, P, P, P, P, P, P, SZ, P]),
+    "pcr_lrf_change_coords": (ST, [P, I, I, P, P, P, P, P]),
+    "pcr_gather_features_forward": (ST, [P, P, I, I, I, I, P, P]),
+    "pcr_gather_features_backward": (ST, [P, P, I, I, I, I, P, P]),
+    "pcr_fps_workspace_size": (SZ, [I, I]),
+    "pcr_furthest_point_sampling": (ST, [P, I, I, I, P, P, SZ, P]),
+    "pcr_three_nn_interpolate_forward": (ST, [P, P, P, I, I, I, I, P, P, P, P]),
+    "pcr_three_nn_interpolate_backward": (ST, [P, P, P, I, I, I, I, P, P]),
     "pcr_selftest_math": (ST, [I, P, P, I, I, P, P, P]),
     "pcr_selftest_math_d": (ST, [I, P, P, I, P, P]),
 }

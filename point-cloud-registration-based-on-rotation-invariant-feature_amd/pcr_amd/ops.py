@@ -332,23 +332,118 @@ def dgcnn_center_gather(features, avg_grid, ind):
     return out
 
 
-# ----------------------------------------------------------- not in scope
-def _out_of_scope(name):
-    def fn(*args, **kwargs):
-        raise NotImplementedError(
-            "%s (PointNet++ op, unused by the sph-dg/cu-dg configs) is outside this "
-            "build's hot-path scope (SURVEY.md 8f, row f4)" % name)
-    fn.__name__ = name
-    return fn
+# ---------------------------------------------- PointNet++ ops (8f f4)
+def gather_features_forward(features, indices):
+    """sampling/sampling.cpp:6-23 -> out [b, c, m]."""
+    _check(features, "features")
+    _check(indices, "indices", "int")
+    b, c, n = features.shape
+    m = indices.shape[1]
+    out = torch.empty((b, c, m), dtype=torch.float32, device=features.device)
+    _lib.check(_lib.load().pcr_gather_features_forward(
+        _ptr(features), _ptr(indices), b, c, n, m, _ptr(out), _stream()),
+        "gather_features_forward")
+    return out
 
 
-gather_features_forward = _out_of_scope("gather_features_forward")
-gather_features_backward = _out_of_scope("gather_features_backward")
-furthest_point_sampling = _out_of_scope("furthest_point_sampling")
-three_nearest_neighbors_interpolate_forward = _out_of_scope(
-    "three_nearest_neighbors_interpolate_forward")
-three_nearest_neighbors_interpolate_backward = _out_of_scope(
-    "three_nearest_neighbors_interpolate_backward")
+def gather_features_backward(grad_y, indices, n):
+    """sampling/sampling.cpp:25-41 -> grad_x [b, c, n]."""
+    _check(grad_y, "grad_y")
+    _check(indices, "indices", "int")
+    b, c, m = grad_y.shape
+    n = int(n)
+    gx = torch.empty((b, c, n), dtype=torch.float32, device=grad_y.device)
+    _lib.check(_lib.load().pcr_gather_features_backward(
+        _ptr(grad_y), _ptr(indices), b, c, n, m, _ptr(gx), _stream()),
+        "gather_features_backward")
+    return gx
+
+
+def furthest_point_sampling(coords, num_samples):
+    """sampling/sampling.cpp:43-58 (bound as ``furthest_point_sampling``,
+    bindings.cpp:18) -> indices [b, num_samples] int32."""
+    _check(coords, "coords")
+    b, _, n = coords.shape
+    m = int(num_samples)
+    dev = coords.device
+    idx = torch.empty((b, m), dtype=torch.int32, device=dev)
+    lib = _lib.load()
+    ws = _workspace(lib.pcr_fps_workspace_size(b, n), dev)
+    _lib.check(lib.pcr_furthest_point_sampling(
+        _ptr(coords), b, n, m, _ptr(idx), _ptr(ws), ws.numel(), _stream()),
+        "furthest_point_sampling")
+    return idx
+
+
+def three_nearest_neighbors_interpolate_forward(points_coords, centers_coords, centers_features):
+    """interpolate/neighbor_interpolate.cpp:6-40 -> [out, indices, weights]."""
+    _check(points_coords, "points_coords")
+    _check(centers_coords, "centers_coords")
+    _check(centers_features, "centers_features")
+    b, c, m = centers_features.shape
+    n = points_coords.shape[2]
+    dev = points_coords.device
+    out = torch.empty((b, c, n), dtype=torch.float32, device=dev)
+    inds = torch.empty((b, 3, n), dtype=torch.int32, device=dev)
+    wgts = torch.empty((b, 3, n), dtype=torch.float32, device=dev)
+    _lib.check(_lib.load().pcr_three_nn_interpolate_forward(
+        _ptr(points_coords), _ptr(centers_coords), _ptr(centers_features), b, c, m, n,
+        _ptr(out), _ptr(inds), _ptr(wgts), _stream()),
+        "three_nearest_neighbors_interpolate_forward")
+    return [out, inds, wgts]
+
+
+def three_nearest_neighbors_interpolate_backward(grad_y, indices, weights, m):
+    """interpolate/neighbor_interpolate.cpp:42-65 -> grad_x [b, c, m]."""
+    _check(grad_y, "grad_y")
+    _check(indices, "indices", "int")
+    _check(weights, "weights")
+    b, c, n = grad_y.shape
+    m = int(m)
+    gx = torch.empty((b, c, m), dtype=torch.float32, device=grad_y.device)
+    _lib.check(_lib.load().pcr_three_nn_interpolate_backward(
+        _ptr(grad_y), _ptr(indices), _ptr(weights), b, c, n, m, _ptr(gx), _stream()),
+        "three_nearest_neighbors_interpolate_backward")
+    return gx
+
+
+# ------------------------------------------ LRF change_coords (8f f2)
+class LRFAssertionError(AssertionError):
+    """One of the reference's change_coords asserts (pvcnn_classify.py:159,
+    :169, :177) fired for some cloud."""
+
+
+_LRF_MSG = {1: "base_x.norm() <= 1e-5 (pvcnn_classify.py:159)",
+            2: "no base_y with |lambda| < 0.9 (pvcnn_classify.py:169)",
+            3: "degenerate Gram-Schmidt, |base_x| < 1e-5 (pvcnn_classify.py:177)"}
+
+
+def lrf_change_coords(coords, check=True, return_basis=False):
+    """rot_invariant_preprocess == 'change_coords' (models/pvcnn_classify.py:
+    153-184): coords [b, 3, n] -> new_coords [b, 3, n] in each cloud's local
+    frame.  With ``check`` the per-cloud status is read back (one host sync,
+    as the reference's asserts) and LRFAssertionError raised on a failure.
+    ``return_basis`` also returns (basis [b, 3, 3], picks [b, 2], status [b])."""
+    _check(coords, "coords")
+    if coords.dim() != 3 or coords.shape[1] != 3:
+        raise RuntimeError("lrf_change_coords: expected coords [b, 3, n]")
+    b, _, n = coords.shape
+    dev = coords.device
+    out = torch.empty_like(coords)
+    basis = torch.empty((b, 3, 3), dtype=torch.float32, device=dev)
+    picks = torch.empty((b, 2), dtype=torch.int32, device=dev)
+    status = torch.empty((b,), dtype=torch.int32, device=dev)
+    _lib.check(_lib.load().pcr_lrf_change_coords(
+        _ptr(coords), b, n, _ptr(out), _ptr(basis), _ptr(picks), _ptr(status), _stream()),
+        "lrf_change_coords")
+    if check and b > 0:
+        st = status.cpu()
+        bad = torch.nonzero(st).flatten().tolist()
+        if bad:
+            raise LRFAssertionError("change_coords: cloud %d: %s" % (bad[0], _LRF_MSG[int(st[bad[0]])]))
+    if return_basis:
+        return out, (basis, picks, status)
+    return out
 
 
 def mutual_nn_match(feat1, feat2):

@@ -31,6 +31,7 @@ def test_library_is_gfx950_code_object():
     data = open(_lib.LIB_PATH, "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in data  # offload bundle target id
     assert b"vox_grid_kernel" in data and b"knn_kernel" in data
+    assert b"fps_reg_kernel" in data and b"lrf_kernel" in data and b"three_nn_kernel" in data
 
 
 def test_backend_names_match_reference_bindings():
@@ -55,7 +56,8 @@ def test_python_api_surface():
     for name in ["ball_query", "trilinear_devoxelize", "grouping", "avg_voxelize",
                  "spherical_avg_voxelize", "spherical_trilinear_devoxelize", "ppf",
                  "k_nearest_neighbor", "nearest_neighbor_interpolate", "gather",
-                 "furthest_point_sample", "logits_mask", "kl_loss", "huber_loss"]:
+                 "furthest_point_sample", "logits_mask", "kl_loss", "huber_loss",
+                 "change_coords"]:
         assert hasattr(F, name), name
     del BallQuery, PVConv, SE3d, SharedMLP, Spherical_Voxelization, Voxelization, knnModule
 
@@ -68,8 +70,12 @@ def test_cpu_tensors_rejected_like_reference():
         ops.spherical_avg_voxelize_forward(x, x, 4)
     with pytest.raises(RuntimeError, match="must be a CUDA tensor"):
         ops.knn_forward_cuda(x, x, 2)
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(RuntimeError, match="must be a CUDA tensor"):
         ops.furthest_point_sampling(x, 4)
+    with pytest.raises(RuntimeError, match="must be a CUDA tensor"):
+        ops.three_nearest_neighbors_interpolate_forward(x, x, x)
+    with pytest.raises(RuntimeError, match="must be a CUDA tensor"):
+        ops.lrf_change_coords(x)
 
 
 def test_workspace_size_query():
