@@ -298,6 +298,25 @@ pcr_status pcr_three_nn_interpolate_backward(const float *grad_y, const int *ind
                                              const float *weights, int b, int c, int n, int m,
                                              float *grad_x, void *stream);
 
+/* ------------------------------------------- normal estimation (8f f3) ----
+ * utils/open3d_func.py:77-83 get_normals (Open3D estimate_normals with
+ * KDTreeSearchParamRadius(radius) + orient_normals_towards_camera_location()
+ * + normalize_normals()), batched on the GPU: points [b,3,n] -> normals
+ * [b,3,n] (unit, facing the origin; (0,0,1) with < 3 neighbours),
+ * counts [b,n] = neighbours within radius incl. the point (may be NULL).
+ * Arithmetic: pcr_estimate_normal of include/pcr_math.h, in fp64. */
+pcr_status pcr_estimate_normals(const float *points, int b, int n, double radius, float *normals,
+                                int *counts, void *stream);
+
+/* ----------------------------------------- on-disk point rows (8f f3) ----
+ * datasets/modelnet40.py:30 np.loadtxt(<sample>.txt, delimiter=',') for the
+ * ModelNet40 normal-resampled files ("x,y,z,nx,ny,nz" per line): every
+ * value parsed as double, then rounded to float (= loadtxt + astype float32).
+ * HOST memory, host code.  pcr_txt_shape counts rows/columns; pcr_read_xyzn_txt
+ * fills a row-major [rows, cols] float buffer. */
+pcr_status pcr_txt_shape(const char *path, long long *rows, int *cols);
+pcr_status pcr_read_xyzn_txt(const char *path, float *out, long long rows, int cols);
+
 /* ------------------------------------------------ native step runner ----
  * `steps` consecutive extractor steps (the pipelined schedule bench.py
  * measures), enqueued from native code: every launch and cross-stream event

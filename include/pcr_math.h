@@ -536,4 +536,226 @@ PCR_HD int pcr_lrf_basis(const float p0[3], float n0, const float p1[3], float n
   return 0;
 }
 
+/* ---- normal estimation (utils/open3d_func.py:77-83,
+ * Open3D PointCloud.estimate_normals(KDTreeSearchParamRadius(0.1)) +
+ * orient_normals_towards_camera_location() + normalize_normals()).  Open3D
+ * is not installed and its version is unpinned, so this is a restatement of
+ * its published algorithm in double precision: neighbour cumulants ->
+ * covariance -> the smallest eigenvector from the robust closed-form 3x3
+ * solver (Eberly, "A Robust Eigensolver for 3x3 Symmetric Matrices"), which
+ * Open3D's FastEigen3x3 implements.  Parity against Open3D is UNPINNED.
+ * Every operation is explicit, so host and device agree bit for bit. ---- */
+/* cos(x) for x in [0, pi]: Taylor series through x^22 in Horner form on
+ * [0, pi/2] (truncation < 1e-19), with cos(x) = -cos(pi - x) above pi/2 */
+PCR_HD double pcr_cos_d(double x) {
+  double s = 1.0, z, p;
+  if (x > PCR_PIO2) {
+    x = PCR_PI - x;
+    s = -1.0;
+  }
+  z = x * x;
+  p = -8.896791392450574e-22; /* -1/22! */
+  p = __builtin_fma(p, z, 4.110317623312165e-19); /* 1/20! */
+  p = __builtin_fma(p, z, -1.5619206968586225e-16); /* -1/18! */
+  p = __builtin_fma(p, z, 4.779477332387385e-14); /* 1/16! */
+  p = __builtin_fma(p, z, -1.1470745597729725e-11); /* -1/14! */
+  p = __builtin_fma(p, z, 2.08767569878681e-09); /* 1/12! */
+  p = __builtin_fma(p, z, -2.755731922398589e-07); /* -1/10! */
+  p = __builtin_fma(p, z, 2.48015873015873e-05); /* 1/8! */
+  p = __builtin_fma(p, z, -0.001388888888888889); /* -1/6! */
+  p = __builtin_fma(p, z, 0.041666666666666664); /* 1/4! */
+  p = __builtin_fma(p, z, -0.5); /* -1/2! */
+  p = __builtin_fma(p, z, 1.0); /* 1/0! */
+  return s * p;
+}
+PCR_HD void pcr_cross_d(const double a[3], const double b[3], double o[3]) {
+  o[0] = a[1] * b[2] - a[2] * b[1];
+  o[1] = a[2] * b[0] - a[0] * b[2];
+  o[2] = a[0] * b[1] - a[1] * b[0];
+}
+PCR_HD double pcr_dot_d(const double a[3], const double b[3]) {
+  return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2];
+}
+/* A = {a00, a01, a02, a11, a12, a22} */
+PCR_HD void pcr_eigvec0_d(const double A[6], double ev, double out[3]) {
+  double r0[3] = {A[0] - ev, A[1], A[2]}, r1[3] = {A[1], A[3] - ev, A[4]};
+  double r2[3] = {A[2], A[4], A[5] - ev};
+  double c01[3], c02[3], c12[3], d0, d1, d2, dmax, s;
+  const double *c;
+  int imax = 0, a;
+  pcr_cross_d(r0, r1, c01);
+  pcr_cross_d(r0, r2, c02);
+  pcr_cross_d(r1, r2, c12);
+  d0 = pcr_dot_d(c01, c01);
+  d1 = pcr_dot_d(c02, c02);
+  d2 = pcr_dot_d(c12, c12);
+  dmax = d0;
+  if (d1 > dmax) {
+    dmax = d1;
+    imax = 1;
+  }
+  if (d2 > dmax) imax = 2;
+  c = imax == 0 ? c01 : (imax == 1 ? c02 : c12);
+  s = __builtin_sqrt(imax == 0 ? d0 : (imax == 1 ? d1 : d2));
+  for (a = 0; a < 3; a++) out[a] = c[a] / s;
+}
+PCR_HD void pcr_eigvec1_d(const double A[6], const double e0[3], double ev, double out[3]) {
+  double U[3], V[3], AU[3], AV[3], m00, m01, m11, am00, am01, am11, inv;
+  int a;
+  if (__builtin_fabs(e0[0]) > __builtin_fabs(e0[1])) {
+    inv = 1.0 / __builtin_sqrt(e0[0] * e0[0] + e0[2] * e0[2]);
+    U[0] = -e0[2] * inv;
+    U[1] = 0.0;
+    U[2] = e0[0] * inv;
+  } else {
+    inv = 1.0 / __builtin_sqrt(e0[1] * e0[1] + e0[2] * e0[2]);
+    U[0] = 0.0;
+    U[1] = e0[2] * inv;
+    U[2] = -e0[1] * inv;
+  }
+  pcr_cross_d(e0, U, V);
+  AU[0] = (A[0] * U[0] + A[1] * U[1]) + A[2] * U[2];
+  AU[1] = (A[1] * U[0] + A[3] * U[1]) + A[4] * U[2];
+  AU[2] = (A[2] * U[0] + A[4] * U[1]) + A[5] * U[2];
+  AV[0] = (A[0] * V[0] + A[1] * V[1]) + A[2] * V[2];
+  AV[1] = (A[1] * V[0] + A[3] * V[1]) + A[4] * V[2];
+  AV[2] = (A[2] * V[0] + A[4] * V[1]) + A[5] * V[2];
+  m00 = pcr_dot_d(U, AU) - ev;
+  m01 = pcr_dot_d(U, AV);
+  m11 = pcr_dot_d(V, AV) - ev;
+  am00 = __builtin_fabs(m00);
+  am01 = __builtin_fabs(m01);
+  am11 = __builtin_fabs(m11);
+  if (am00 >= am11) {
+    if ((am00 > am01 ? am00 : am01) > 0.0) {
+      if (am00 >= am01) {
+        m01 /= m00;
+        m00 = 1.0 / __builtin_sqrt(1.0 + m01 * m01);
+        m01 *= m00;
+      } else {
+        m00 /= m01;
+        m01 = 1.0 / __builtin_sqrt(1.0 + m00 * m00);
+        m00 *= m01;
+      }
+      for (a = 0; a < 3; a++) out[a] = m01 * U[a] - m00 * V[a];
+      return;
+    }
+  } else {
+    if ((am11 > am01 ? am11 : am01) > 0.0) {
+      if (am11 >= am01) {
+        m01 /= m11;
+        m11 = 1.0 / __builtin_sqrt(1.0 + m01 * m01);
+        m01 *= m11;
+      } else {
+        m11 /= m01;
+        m01 = 1.0 / __builtin_sqrt(1.0 + m11 * m11);
+        m11 *= m01;
+      }
+      for (a = 0; a < 3; a++) out[a] = m11 * U[a] - m01 * V[a];
+      return;
+    }
+  }
+  for (a = 0; a < 3; a++) out[a] = U[a];
+}
+/* eigenvector of the smallest eigenvalue of the symmetric C (6 entries as
+ * above); (0,0,0) when the largest entry is 0 (FastEigen3x3) */
+PCR_HD void pcr_fast_eigen3x3(const double C[6], double out[3]) {
+  double A[6], mx = C[0], nrm;
+  int a;
+  for (a = 1; a < 6; a++) mx = C[a] > mx ? C[a] : mx;
+  if (mx == 0.0) {
+    out[0] = out[1] = out[2] = 0.0;
+    return;
+  }
+  for (a = 0; a < 6; a++) A[a] = C[a] / mx;
+  nrm = (A[1] * A[1] + A[2] * A[2]) + A[4] * A[4];
+  if (nrm > 0.0) {
+    double q = ((A[0] + A[3]) + A[5]) / 3.0;
+    double b00 = A[0] - q, b11 = A[3] - q, b22 = A[5] - q;
+    double p = __builtin_sqrt(((((b00 * b00 + b11 * b11) + b22 * b22) + nrm * 2.0)) / 6.0);
+    double c00 = b11 * b22 - A[4] * A[4];
+    double c01 = A[1] * b22 - A[4] * A[2];
+    double c02 = A[1] * A[4] - b11 * A[2];
+    double det = ((b00 * c00 - A[1] * c01) + A[2] * c02) / ((p * p) * p);
+    double hd = det * 0.5, ang, beta0, beta1, beta2, ev0, ev1, ev2, e0[3], e1[3];
+    hd = hd < -1.0 ? -1.0 : (hd > 1.0 ? 1.0 : hd);
+    ang = pcr_acos_d(hd) / 3.0;
+    beta2 = pcr_cos_d(ang) * 2.0;
+    beta0 = pcr_cos_d(ang + 2.09439510239319549) * 2.0;
+    beta1 = -(beta0 + beta2);
+    ev0 = q + p * beta0;
+    ev1 = q + p * beta1;
+    ev2 = q + p * beta2;
+    if (hd >= 0.0) {
+      pcr_eigvec0_d(A, ev2, e0); /* evec2 */
+      if (ev2 < ev0 && ev2 < ev1) {
+        for (a = 0; a < 3; a++) out[a] = e0[a];
+        return;
+      }
+      pcr_eigvec1_d(A, e0, ev1, e1);
+      if (ev1 < ev0 && ev1 < ev2) {
+        for (a = 0; a < 3; a++) out[a] = e1[a];
+        return;
+      }
+      pcr_cross_d(e1, e0, out);
+    } else {
+      pcr_eigvec0_d(A, ev0, e0);
+      if (ev0 < ev1 && ev0 < ev2) {
+        for (a = 0; a < 3; a++) out[a] = e0[a];
+        return;
+      }
+      pcr_eigvec1_d(A, e0, ev1, e1);
+      if (ev1 < ev0 && ev1 < ev2) {
+        for (a = 0; a < 3; a++) out[a] = e1[a];
+        return;
+      }
+      pcr_cross_d(e0, e1, out);
+    }
+    return;
+  }
+  if (C[0] < C[3] && C[0] < C[5]) {
+    out[0] = 1.0;
+    out[1] = out[2] = 0.0;
+  } else if (C[3] < C[0] && C[3] < C[5]) {
+    out[1] = 1.0;
+    out[0] = out[2] = 0.0;
+  } else {
+    out[2] = 1.0;
+    out[0] = out[1] = 0.0;
+  }
+}
+/* One point's normal from its neighbour cumulants
+ * cum = {sx, sy, sz, sxx, sxy, sxz, syy, syz, szz} over cnt neighbours
+ * (itself included): fewer than 3 -> (0,0,1); zero eigenvector -> (0,0,1);
+ * flip towards the camera at the origin (dot(n, -p) < 0 -> -n; a zero
+ * normal cannot reach here); normalise; round to float. */
+PCR_HD void pcr_estimate_normal(const double cum[9], int cnt, float px, float py, float pz,
+                                float out[3]) {
+  double n[3], C[6], m[9], ref[3], len;
+  int a;
+  if (cnt < 3) {
+    out[0] = out[1] = 0.0f;
+    out[2] = 1.0f;
+    return;
+  }
+  for (a = 0; a < 9; a++) m[a] = cum[a] / (double)cnt;
+  C[0] = m[3] - m[0] * m[0];
+  C[1] = m[4] - m[0] * m[1];
+  C[2] = m[5] - m[0] * m[2];
+  C[3] = m[6] - m[1] * m[1];
+  C[4] = m[7] - m[1] * m[2];
+  C[5] = m[8] - m[2] * m[2];
+  pcr_fast_eigen3x3(C, n);
+  if (n[0] == 0.0 && n[1] == 0.0 && n[2] == 0.0) {
+    n[2] = 1.0;
+  }
+  ref[0] = -(double)px;
+  ref[1] = -(double)py;
+  ref[2] = -(double)pz;
+  if (pcr_dot_d(n, ref) < 0.0)
+    for (a = 0; a < 3; a++) n[a] = -n[a];
+  len = __builtin_sqrt(pcr_dot_d(n, n));
+  for (a = 0; a < 3; a++) out[a] = (float)(n[a] / len);
+}
+
 #endif /* PCR_MATH_H */

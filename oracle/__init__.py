@@ -56,6 +56,7 @@ _SIGS = {
     "orc_fps": [_i, _i, _i, _f32p, _i32p],
     "orc_three_nn": [_i, _i, _i, _i, _f32p, _f32p, _f32p, _f32p, _i32p, _f32p],
     "orc_three_nn_grad": [_i, _i, _i, _i, _f32p, _i32p, _f32p, _f32p],
+    "orc_normals": [_i, _i, ctypes.c_double, _f32p, _f32p, _i32p],
     "orc_num_threads": [],
     "orc_set_num_threads": [_i],
 }
@@ -366,3 +367,15 @@ def three_nearest_neighbors_interpolate_backward(grad_y, indices, weights, m):
     gx = np.empty((b, c, m), np.float32)
     lib().orc_three_nn_grad(b, c, n, m, grad_y, indices, weights, gx)
     return gx
+
+
+# ------------------------------------------- normal estimation (f3)
+def estimate_normals(points, radius=0.1):
+    """utils/open3d_func.py:77-83 restated: points [b, 3, n] -> (normals
+    [b, 3, n], counts [b, n])."""
+    points = _f32(points)
+    b, _, n = points.shape
+    normals = np.empty_like(points)
+    counts = np.empty((b, n), np.int32)
+    lib().orc_normals(b, n, float(radius), points, normals, counts)
+    return normals, counts

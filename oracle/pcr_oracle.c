@@ -769,6 +769,47 @@ void orc_three_nn_grad(int b, int c, int n, int m, const float *gy, const int *i
         }
 }
 
+/* ------------------------------------------- normal estimation (f3) */
+/* utils/open3d_func.py:77-83 (Open3D radius-neighbourhood PCA, oriented to
+ * the origin).  Neighbours in ascending index order, |q - p|^2 < radius^2 in
+ * double; per-point arithmetic in pcr_estimate_normal (pcr_math.h). */
+void orc_normals(int b, int n, double radius, const float *pts, float *normals, int *counts) {
+  int bi;
+  const double r2 = radius * radius;
+#pragma omp parallel for schedule(dynamic)
+  for (bi = 0; bi < b; bi++) {
+    const float *P = pts + (size_t)bi * 3 * n;
+    float *N = normals + (size_t)bi * 3 * n;
+    int j, q, a;
+    for (j = 0; j < n; j++) {
+      double cum[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+      const double qx = P[j], qy = P[j + n], qz = P[j + 2 * n];
+      int cnt = 0;
+      float nv[3];
+      for (q = 0; q < n; q++) {
+        const double x = P[q], y = P[q + n], z = P[q + 2 * n];
+        const double dx = qx - x, dy = qy - y, dz = qz - z;
+        const double d2 = (dx * dx + dy * dy) + dz * dz;
+        if (d2 < r2) {
+          cum[0] += x;
+          cum[1] += y;
+          cum[2] += z;
+          cum[3] += x * x;
+          cum[4] += x * y;
+          cum[5] += x * z;
+          cum[6] += y * y;
+          cum[7] += y * z;
+          cum[8] += z * z;
+          cnt++;
+        }
+      }
+      pcr_estimate_normal(cum, cnt, P[j], P[j + n], P[j + 2 * n], nv);
+      for (a = 0; a < 3; a++) N[j + a * n] = nv[a];
+      counts[(size_t)bi * n + j] = cnt;
+    }
+  }
+}
+
 int orc_num_threads(void) {
 #ifdef _OPENMP
   return omp_get_max_threads();

@@ -60,6 +60,10 @@ SIGNATURES = {
     "pcr_furthest_point_sampling": (ST, [P, I, I, I, P, P, SZ, P]),
     "pcr_three_nn_interpolate_forward": (ST, [P, P, P, I, I, I, I, P, P, P, P]),
     "pcr_three_nn_interpolate_backward": (ST, [P, P, P, I, I, I, I, P, P]),
+    "pcr_estimate_normals": (ST, [P, I, I, ctypes.c_double, P, P, P]),
+    "pcr_txt_shape": (ST, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_longlong),
+                           ctypes.POINTER(ctypes.c_int)]),
+    "pcr_read_xyzn_txt": (ST, [ctypes.c_char_p, P, ctypes.c_longlong, I]),
     "pcr_selftest_math": (ST, [I, P, P, I, I, P, P, P]),
     "pcr_selftest_math_d": (ST, [I, P, P, I, P, P]),
 }

@@ -446,6 +446,26 @@ def lrf_change_coords(coords, check=True, return_basis=False):
     return out
 
 
+# ------------------------------------------ normal estimation (8f f3)
+def estimate_normals(points, radius=0.1, return_counts=False):
+    """get_normals (utils/open3d_func.py:77-83) for a batch on the GPU:
+    points [b, 3, n] -> unit normals [b, 3, n] from the PCA of each point's
+    radius neighbourhood, flipped to face the origin (Open3D's
+    orient_normals_towards_camera_location default), (0, 0, 1) with fewer
+    than 3 neighbours.  ``return_counts`` also returns the neighbour counts
+    [b, n] int32."""
+    _check(points, "points")
+    if points.dim() != 3 or points.shape[1] != 3:
+        raise RuntimeError("estimate_normals: expected points [b, 3, n]")
+    b, _, n = points.shape
+    normals = torch.empty_like(points)
+    counts = torch.empty((b, n), dtype=torch.int32, device=points.device)
+    _lib.check(_lib.load().pcr_estimate_normals(
+        _ptr(points), b, n, float(radius), _ptr(normals), _ptr(counts), _stream()),
+        "estimate_normals")
+    return (normals, counts) if return_counts else normals
+
+
 def mutual_nn_match(feat1, feat2):
     """Feature-space mutual nearest neighbours of p registration pairs
     (datasets/deepgmr_mn40.py:232-244, batched): feat1 [p, n1, c],
