@@ -27,15 +27,52 @@ __global__ __launch_bounds__(256) void match_sqnorm_kernel(const float* __restri
 }
 
 constexpr int kMT = 128;  // tile rows (f1) and columns (f2)
-constexpr int kKC = 16;   // channels per LDS stage
+constexpr int kKC = 32;   // channels per LDS stage
 constexpr int kMPad = kMT + 4;
 
+// One stage of the operands: thread t holds 16 consecutive channels of row
+// t / 2 of A and of B (float4 loads when the stage is full and c % 4 == 0).
+__device__ inline void match_load_stage(const float* __restrict__ A, const float* __restrict__ B,
+                                        int i0, int j0, int n1, int n2, int c, int k0, int lr,
+                                        int lk, float (&va)[16], float (&vb)[16]) {
+  const int ka = k0 + lk;
+  const bool ra = i0 + lr < n1, rb = j0 + lr < n2;
+  if (ka + 16 <= c && (c & 3) == 0) {
+    const float4* pa = reinterpret_cast<const float4*>(A + (size_t)(i0 + lr) * c + ka);
+    const float4* pb = reinterpret_cast<const float4*>(B + (size_t)(j0 + lr) * c + ka);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const float4 x = ra ? pa[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 y = rb ? pb[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+      va[4 * q] = x.x;
+      va[4 * q + 1] = x.y;
+      va[4 * q + 2] = x.z;
+      va[4 * q + 3] = x.w;
+      vb[4 * q] = y.x;
+      vb[4 * q + 1] = y.y;
+      vb[4 * q + 2] = y.z;
+      vb[4 * q + 3] = y.w;
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 16; e++) {
+      const int k = ka + e;
+      va[e] = (ra && k < c) ? A[(size_t)(i0 + lr) * c + k] : 0.0f;
+      vb[e] = (rb && k < c) ? B[(size_t)(j0 + lr) * c + k] : 0.0f;
+    }
+  }
+}
+
+// Channels run through LDS in stages of 32, double-buffered: the next
+// stage's global loads are in flight while the MFMAs consume this one, and
+// one barrier per stage suffices (a buffer is rewritten two stages later,
+// after every wave passed the barrier in between).
 __global__ __launch_bounds__(256) void match_tile_kernel(
     const float* __restrict__ f1, const float* __restrict__ f2, int n1, int n2, int c,
     const float* __restrict__ sq1, const float* __restrict__ sq2,
     unsigned long long* __restrict__ rowbest, unsigned long long* __restrict__ colbest) {
-  __shared__ float a_s[kKC][kMPad];  // [k][i]
-  __shared__ float b_s[kKC][kMPad];  // [k][j]
+  __shared__ float a_s[2][kKC][kMPad];  // [buf][k][i]
+  __shared__ float b_s[2][kKC][kMPad];  // [buf][k][j]
   const int p = blockIdx.z;
   const int i0 = blockIdx.y * kMT, j0 = blockIdx.x * kMT;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -49,36 +86,33 @@ __global__ __launch_bounds__(256) void match_tile_kernel(
     for (int tj = 0; tj < 2; tj++)
 #pragma unroll
       for (int v = 0; v < 16; v++) acc[ti][tj][v] = 0.0f;
-  // staging: thread t loads 8 consecutive channels of row t / 2
-  const int lr = tid >> 1, lk = (tid & 1) * 8;
-  for (int k0 = 0; k0 < c; k0 += kKC) {
-    float va[8], vb[8];
+  const int lr = tid >> 1, lk = (tid & 1) * 16;
+  float va[16], vb[16];
+  match_load_stage(A, B, i0, j0, n1, n2, c, 0, lr, lk, va, vb);
+  int buf = 0;
+  for (int k0 = 0; k0 < c; k0 += kKC, buf ^= 1) {
 #pragma unroll
-    for (int e = 0; e < 8; e++) {
-      const int k = k0 + lk + e;
-      va[e] = (i0 + lr < n1 && k < c) ? A[(size_t)(i0 + lr) * c + k] : 0.0f;
-      vb[e] = (j0 + lr < n2 && k < c) ? B[(size_t)(j0 + lr) * c + k] : 0.0f;
+    for (int e = 0; e < 16; e++) {
+      a_s[buf][lk + e][lr] = va[e];
+      b_s[buf][lk + e][lr] = vb[e];
     }
-    __syncthreads();  // the previous stage's reads are done
-#pragma unroll
-    for (int e = 0; e < 8; e++) {
-      a_s[lk + e][lr] = va[e];
-      b_s[lk + e][lr] = vb[e];
-    }
-    __syncthreads();
+    lds_barrier();
+    if (k0 + kKC < c) match_load_stage(A, B, i0, j0, n1, n2, c, k0 + kKC, lr, lk, va, vb);
     // k ascending: every product enters its accumulator in channel order
 #pragma unroll
     for (int kk = 0; kk < kKC; kk += 2) {
       const int kr = kk + (lane >> 5);
+      float a[2], bq[2];
 #pragma unroll
-      for (int ti = 0; ti < 2; ti++) {
-        const float a = a_s[kr][wi * 64 + ti * 32 + (lane & 31)];
-#pragma unroll
-        for (int tj = 0; tj < 2; tj++) {
-          const float bq = b_s[kr][wj * 64 + tj * 32 + (lane & 31)];
-          acc[ti][tj] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bq, acc[ti][tj], 0, 0, 0);
-        }
+      for (int t = 0; t < 2; t++) {
+        a[t] = a_s[buf][kr][wi * 64 + t * 32 + (lane & 31)];
+        bq[t] = b_s[buf][kr][wj * 64 + t * 32 + (lane & 31)];
       }
+#pragma unroll
+      for (int ti = 0; ti < 2; ti++)
+#pragma unroll
+        for (int tj = 0; tj < 2; tj++)
+          acc[ti][tj] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[ti], bq[tj], acc[ti][tj], 0, 0, 0);
     }
   }
   // epilogue: C/D layout col = lane & 31, row = (v & 3) + 8 (v >> 2) + 4 (lane >> 5)
