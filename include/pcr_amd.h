@@ -128,6 +128,11 @@ pcr_status pcr_grouping_backward(const float *grad_y, const int *indices, int b,
  * Scratch for the voxelizers: per-cloud sort permutation, occupied-voxel
  * segments and an occupancy bitmap with word prefix counts. */
 size_t pcr_voxelize_workspace_size(int b, int n, int r);
+/* The same for c feature channels.  Clouds of more than 4096 points use the
+ * sorted large-cloud path; with this size it also keeps a point-major copy
+ * of the features, so each voxel reads its points' channels contiguously
+ * (several times faster).  The results are identical either way. */
+size_t pcr_voxelize_workspace_size_c(int b, int c, int n, int r);
 
 /* spherical_avg_voxelize_forward (spherical_voxelization/spherical_vox.cpp:17-46,
  * kernels spherical_vox.cu:19-125): features [b,c,n], normalised coords

@@ -26,6 +26,8 @@
 //      per-cloud max-pooled descriptor.
 #include "common.hpp"
 
+#include <hipcub/hipcub.hpp>
+
 namespace pcr {
 
 constexpr int kPrepThreads = kSortBlock;
@@ -1166,16 +1168,74 @@ __global__ __launch_bounds__(kPrepThreads) void sph_normalize_kernel(
 }
 
 // ------------------------------------------------- clouds of > 4096 points
-// The reference algorithm as such (spherical_vox.cu:19-125, vox.cu:18-73):
-// per-point voxel index + count (global atomics), then every valid point adds
-// feature * (1 / count) to its voxel with global atomics.  The summation
-// order inside a voxel is arbitrary, as in the reference (parity within the
-// fp32 sum-order tolerance); indices and counts are exact.
+// Sort-based, like the small path, at any size: (1) per-point voxel index,
+// count atomics and a 64-bit key (cloud | voxel | point); (2) a device radix
+// sort of the keys (hipCUB), so every voxel's points are contiguous and in
+// ascending point order; (3) an exclusive scan of the counts locates each
+// voxel's segment; (4) one thread per voxel sums its segment in that order
+// and writes all C channels, so the dense grid is written once, coalesced,
+// zeros included.  The reference scatters C fp32 atomics per point into a
+// memset grid (spherical_vox.cu:103-123); here the order is the oracle's
+// ascending point order, bit-exact.  Dropped points (ind = -1) get the
+// voxel field r^3 and sort after every voxel of their cloud.
+struct BigVoxWs {
+  unsigned long long *keys_in, *keys_out;
+  int* scan;
+  float* featT;  // [b][n][c] point-major copy of the features (nullptr: c == 0)
+  void* temp;
+  size_t temp_bytes;
+  int pb, vb, end_bit;
+};
+
+static int bits_for(uint64_t v) {  // bits needed to hold 0..v
+  int nb = 1;
+  while (nb < 64 && (v >> nb) != 0) nb++;
+  return nb;
+}
+
+static size_t big_ws_layout(int b, int n, int r, BigVoxWs* ws, void* base, int c = 0) {
+  const int64_t r3 = (int64_t)r * r * r;
+  const size_t nk = (size_t)b * n, nr = (size_t)b * r3;
+  const int pb = bits_for((uint64_t)(n - 1)), vb = bits_for((uint64_t)r3),
+            cb = bits_for((uint64_t)(b > 1 ? b - 1 : 1));
+  size_t s1 = 0, s2 = 0;
+  (void)hipcub::DeviceRadixSort::SortKeys(nullptr, s1, (unsigned long long*)nullptr,
+                                          (unsigned long long*)nullptr, (int)nk, 0, pb + vb + cb);
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, s2, (int*)nullptr, (int*)nullptr, (int)nr);
+  size_t off = 0;
+  char* p = (char*)base;
+  auto take = [&](size_t bytes) {
+    char* q = p ? p + off : nullptr;
+    off = align_up(off + bytes, 256);
+    return q;
+  };
+  auto* ki = (unsigned long long*)take(nk * 8);
+  auto* ko = (unsigned long long*)take(nk * 8);
+  int* scan = (int*)take(nr * 4);
+  const size_t tb = s1 > s2 ? s1 : s2;
+  void* temp = take(tb);
+  float* ft = c > 0 ? (float*)take(nk * (size_t)c * 4) : nullptr;
+  if (ws) {
+    ws->featT = ft;
+    ws->keys_in = ki;
+    ws->keys_out = ko;
+    ws->scan = scan;
+    ws->temp = temp;
+    ws->temp_bytes = tb;
+    ws->pb = pb;
+    ws->vb = vb;
+    ws->end_bit = pb + vb + cb;
+  }
+  return off;
+}
+
 template <int MODE>
-__global__ __launch_bounds__(256) void vox_index_big_kernel(const float* __restrict__ coords_f,
-                                                            const int* __restrict__ coords_i,
-                                                            int n, int r, int* __restrict__ ind,
-                                                            int* __restrict__ cnt) {
+__global__ __launch_bounds__(256) void vox_key_big_kernel(const float* __restrict__ coords_f,
+                                                          const int* __restrict__ coords_i, int n,
+                                                          int r, int pb, int vb,
+                                                          int* __restrict__ ind,
+                                                          int* __restrict__ cnt,
+                                                          unsigned long long* __restrict__ keys) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   const int b = blockIdx.y;
   if (i >= n) return;
@@ -1193,22 +1253,43 @@ __global__ __launch_bounds__(256) void vox_index_big_kernel(const float* __restr
   }
   ind[(size_t)b * n + i] = v;
   if (valid) atomicAdd(&cnt[(size_t)b * r3 + v], 1);
+  const unsigned long long vv = (unsigned long long)(valid ? v : r3);
+  keys[(size_t)b * n + i] = ((unsigned long long)b << (pb + vb)) | (vv << pb) | (unsigned)i;
 }
 
-__global__ __launch_bounds__(256) void vox_scatter_big_kernel(const float* __restrict__ feat,
-                                                              const int* __restrict__ ind,
-                                                              const int* __restrict__ cnt, int c,
-                                                              int n, int r3, int cg,
-                                                              float* __restrict__ out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const int b = blockIdx.z;
-  if (i >= n) return;
-  const int v = ind[(size_t)b * n + i];
-  if (v < 0 || v >= r3) return;
-  const float inv = pcr_inv_count(cnt[(size_t)b * r3 + v]);
-  const int c0 = blockIdx.y * cg, c1 = min(c, c0 + cg);
-  for (int j = c0; j < c1; j++)
-    atomicAdd(&out[((size_t)b * c + j) * r3 + v], feat[((size_t)b * c + j) * n + i] * inv);
+// one thread per voxel: its segment of the sorted keys, summed per channel
+// in ascending point order (acc += f * inv, the product rounded first)
+__global__ __launch_bounds__(256) void vox_gather_big_kernel(
+    const float* __restrict__ feat, const int* __restrict__ cnt, const int* __restrict__ scan,
+    const unsigned long long* __restrict__ keys, int c, int n, int r3, int pb,
+    float* __restrict__ out) {
+  const int v = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (v >= r3) return;
+  const size_t vi = (size_t)b * r3 + v;
+  const int m = cnt[vi];
+  const size_t start = (size_t)b * n + (size_t)(scan[vi] - scan[(size_t)b * r3]);
+  const unsigned long long pmask = (1ull << pb) - 1;
+  const float* F = feat + (size_t)b * c * n;
+  float* O = out + (size_t)b * c * r3 + v;
+  if (m == 0) {
+    for (int ch = 0; ch < c; ch++) O[(size_t)ch * r3] = 0.0f;
+    return;
+  }
+  const float inv = pcr_inv_count(m);
+  constexpr int kHold = 8;
+  int pts[kHold];
+#pragma unroll
+  for (int s = 0; s < kHold; s++) pts[s] = s < m ? (int)(keys[start + s] & pmask) : 0;
+  for (int ch = 0; ch < c; ch++) {
+    const float* f = F + (size_t)ch * n;
+    float acc = 0.0f;
+#pragma unroll
+    for (int s = 0; s < kHold; s++)
+      if (s < m) acc += f[pts[s]] * inv;
+    for (int s = kHold; s < m; s++) acc += f[(int)(keys[start + s] & pmask)] * inv;
+    O[(size_t)ch * r3] = acc;
+  }
 }
 
 // Fixed-order normalisation for any n (same order as cloud_mean: thread t
@@ -1270,24 +1351,134 @@ __global__ __launch_bounds__(kPrepThreads) void sph_normalize_big_kernel(
   }
 }
 
+// [c][n] -> [n][c] per cloud through a 64 x 64 LDS tile (coalesced both ways)
+__global__ __launch_bounds__(256) void feat_transpose_kernel(const float* __restrict__ feat,
+                                                             int c, int n,
+                                                             float* __restrict__ featT) {
+  __shared__ float t[64][65];
+  const int b = blockIdx.z, n0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const float* F = feat + (size_t)b * c * n;
+  float* T = featT + (size_t)b * n * c;
+  for (int y = ty; y < 64; y += 4)
+    if (c0 + y < c && n0 + tx < n) t[y][tx] = F[(size_t)(c0 + y) * n + n0 + tx];
+  __syncthreads();
+  for (int y = ty; y < 64; y += 4)
+    if (n0 + y < n && c0 + tx < c) T[(size_t)(n0 + y) * c + c0 + tx] = t[tx][y];
+}
+
+// vox_gather_big_kernel on the point-major copy: a voxel's point reads 16
+// consecutive channels (64 B) at a time instead of 16 scattered lines
+template <int CH>
+__global__ __launch_bounds__(256) void vox_gather_big_t_kernel(
+    const float* __restrict__ featT, const int* __restrict__ cnt, const int* __restrict__ scan,
+    const unsigned long long* __restrict__ keys, int c, int n, int r3, int pb,
+    float* __restrict__ out) {
+  const int v = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (v >= r3) return;
+  const size_t vi = (size_t)b * r3 + v;
+  const int m = cnt[vi];
+  float* O = out + (size_t)b * c * r3 + v;
+  const size_t start = (size_t)b * n + (size_t)(m > 0 ? scan[vi] - scan[(size_t)b * r3] : 0);
+  const unsigned long long pmask = (1ull << pb) - 1;
+  const float* FT = featT + (size_t)b * n * c;
+  const float inv = m > 0 ? pcr_inv_count(m) : 0.0f;
+  constexpr int kHold = 4;  // the first points' rows, read once for every chunk
+  const float* rows[kHold];
+#pragma unroll
+  for (int s = 0; s < kHold; s++) rows[s] = s < m ? FT + (size_t)(keys[start + s] & pmask) * c : FT;
+  const bool vec = (c & 3) == 0;
+  // every lane runs the same chunk loop and stores (empty voxels add nothing
+  // and store zeros), so the stores stay whole-wave and coalesced
+  for (int c0 = 0; c0 < c; c0 += CH) {
+    float acc[CH];
+#pragma unroll
+    for (int q = 0; q < CH; q++) acc[q] = 0.0f;
+    if (vec && c0 + CH <= c) {
+#pragma unroll
+      for (int s = 0; s < kHold; s++) {
+        if (s < m) {
+#pragma unroll
+          for (int q = 0; q < CH; q += 4) {
+            const float4 x = *reinterpret_cast<const float4*>(rows[s] + c0 + q);
+            acc[q] += x.x * inv;
+            acc[q + 1] += x.y * inv;
+            acc[q + 2] += x.z * inv;
+            acc[q + 3] += x.w * inv;
+          }
+        }
+      }
+      for (int s = kHold; s < m; s++) {
+        const float* row = FT + (size_t)(keys[start + s] & pmask) * c + c0;
+#pragma unroll
+        for (int q = 0; q < CH; q += 4) {
+          const float4 x = *reinterpret_cast<const float4*>(row + q);
+          acc[q] += x.x * inv;
+          acc[q + 1] += x.y * inv;
+          acc[q + 2] += x.z * inv;
+          acc[q + 3] += x.w * inv;
+        }
+      }
+    } else {
+      for (int s = 0; s < m; s++) {
+        const float* row = FT + (size_t)(keys[start + s] & pmask) * c + c0;
+#pragma unroll
+        for (int q = 0; q < CH; q++)
+          if (c0 + q < c) acc[q] += row[q] * inv;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < CH; q++)
+      if (c0 + q < c) O[(size_t)(c0 + q) * r3] = acc[q];
+  }
+}
+
 template <int MODE>
 static pcr_status run_voxelize_big(const float* features, const float* coords_f,
                                    const int* coords_i, int b, int c, int n, int r, float* out,
-                                   int* ind, int* cnt, hipStream_t stream, const char* name) {
+                                   int* ind, int* cnt, void* workspace, size_t ws_bytes,
+                                   hipStream_t stream, const char* name) {
   const int r3 = r * r * r;
   PCR_REQUIRE(cnt != nullptr && ind != nullptr, "%s: ind and cnt required", name);
-  if (hipMemsetAsync(cnt, 0, (size_t)b * r3 * sizeof(int), stream) != hipSuccess ||
-      (c > 0 && out &&
-       hipMemsetAsync(out, 0, (size_t)b * c * r3 * sizeof(float), stream) != hipSuccess)) {
+  PCR_REQUIRE((int64_t)b * n < (1ll << 31) && (int64_t)b * r3 < (1ll << 31),
+              "%s: batch too large for the sorted path", name);
+  BigVoxWs ws;
+  // with room for the point-major feature copy the coalesced gather runs,
+  // else the direct one (same results)
+  size_t need = big_ws_layout(b, n, r, &ws, workspace, c);
+  if (workspace == nullptr || ws_bytes < need) need = big_ws_layout(b, n, r, &ws, workspace, 0);
+  PCR_REQUIRE(ws.end_bit <= 64, "%s: key does not fit 64 bits", name);
+  PCR_REQUIRE(workspace != nullptr && ws_bytes >= need, "%s: workspace too small (%zu < %zu)",
+              name, ws_bytes, need);
+  if (hipMemsetAsync(cnt, 0, (size_t)b * r3 * sizeof(int), stream) != hipSuccess) {
     set_error("%s: memset failed", name);
     return PCR_ERR_LAUNCH;
   }
-  hipLaunchKernelGGL(vox_index_big_kernel<MODE>, dim3(ceil_div(n, 256), b), dim3(256), 0, stream,
-                     coords_f, coords_i, n, r, ind, cnt);
+  hipLaunchKernelGGL(vox_key_big_kernel<MODE>, dim3(ceil_div(n, 256), b), dim3(256), 0, stream,
+                     coords_f, coords_i, n, r, ws.pb, ws.vb, ind, cnt, ws.keys_in);
   if (c > 0 && out) {
-    const int cg = 8;
-    hipLaunchKernelGGL(vox_scatter_big_kernel, dim3(ceil_div(n, 256), ceil_div(c, cg), b),
-                       dim3(256), 0, stream, features, ind, cnt, c, n, r3, cg, out);
+    size_t tb = ws.temp_bytes;
+    if (hipcub::DeviceRadixSort::SortKeys(ws.temp, tb, ws.keys_in, ws.keys_out, b * n, 0,
+                                          ws.end_bit, stream) != hipSuccess) {
+      set_error("%s: radix sort failed", name);
+      return PCR_ERR_LAUNCH;
+    }
+    tb = ws.temp_bytes;
+    if (hipcub::DeviceScan::ExclusiveSum(ws.temp, tb, cnt, ws.scan, b * r3, stream) !=
+        hipSuccess) {
+      set_error("%s: count scan failed", name);
+      return PCR_ERR_LAUNCH;
+    }
+    if (ws.featT) {
+      hipLaunchKernelGGL(feat_transpose_kernel, dim3(ceil_div(n, 64), ceil_div(c, 64), b),
+                         dim3(256), 0, stream, features, c, n, ws.featT);
+      hipLaunchKernelGGL(vox_gather_big_t_kernel<32>, dim3(ceil_div(r3, 256), b), dim3(256), 0,
+                         stream, ws.featT, cnt, ws.scan, ws.keys_out, c, n, r3, ws.pb, out);
+    } else {
+      hipLaunchKernelGGL(vox_gather_big_kernel, dim3(ceil_div(r3, 256), b), dim3(256), 0, stream,
+                         features, cnt, ws.scan, ws.keys_out, c, n, r3, ws.pb, out);
+    }
   }
   return launch_status(name);
 }
@@ -1324,8 +1515,8 @@ static pcr_status run_voxelize(const float* features, const float* coords_f, con
   PCR_REQUIRE((int64_t)r * r * r <= (1 << 24), "%s: resolution %d too large", name, r);
   if (b == 0) return PCR_OK;
   if (n > kMaxSortN && MODE != kSphNormalize && what == 3 && devox == nullptr)
-    return run_voxelize_big<MODE>(features, coords_f, coords_i, b, c, n, r, out, ind, cnt, stream,
-                                  name);
+    return run_voxelize_big<MODE>(features, coords_f, coords_i, b, c, n, r, out, ind, cnt,
+                                  workspace, ws_bytes, stream, name);
   PCR_REQUIRE(n >= 1 && n <= kMaxSortN,
               "%s: n=%d points per cloud unsupported on this path (1..%d)", name, n, kMaxSortN);
   const int r3 = r * r * r;
@@ -1416,6 +1607,13 @@ using namespace pcr;
 
 extern "C" size_t pcr_voxelize_workspace_size(int b, int n, int r) {
   if (b <= 0 || n <= 0 || r <= 0) return 256;
+  if (n > kMaxSortN) return big_ws_layout(b, n, r, nullptr, nullptr);
+  return vox_ws_layout(b, n, r, nullptr, nullptr);
+}
+
+extern "C" size_t pcr_voxelize_workspace_size_c(int b, int c, int n, int r) {
+  if (b <= 0 || n <= 0 || r <= 0) return 256;
+  if (n > kMaxSortN) return big_ws_layout(b, n, r, nullptr, nullptr, c > 0 ? c : 0);
   return vox_ws_layout(b, n, r, nullptr, nullptr);
 }
 

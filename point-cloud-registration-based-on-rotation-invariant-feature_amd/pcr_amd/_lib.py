@@ -34,6 +34,7 @@ SIGNATURES = {
     "pcr_grouping_forward": (ST, [P, P, I, I, I, I, I, P, P]),
     "pcr_grouping_backward": (ST, [P, P, I, I, I, I, I, P, P]),
     "pcr_voxelize_workspace_size": (SZ, [I, I, I]),
+    "pcr_voxelize_workspace_size_c": (SZ, [I, I, I, I]),
     "pcr_spherical_avg_voxelize_forward": (ST, [P, P, I, I, I, I, P, P, P, P, SZ, P]),
     "pcr_avg_voxelize_forward": (ST, [P, P, I, I, I, I, P, P, P, P, SZ, P]),
     "pcr_avg_voxelize_backward": (ST, [P, P, P, I, I, I, I, P, P]),

@@ -198,8 +198,7 @@ def spherical_avg_voxelize_forward(features, coords, resolution):
     ind = torch.empty((b, n), dtype=torch.int32, device=dev)
     cnt = torch.empty((b, r3), dtype=torch.int32, device=dev)
     lib = _lib.load()
-    ws_bytes = lib.pcr_voxelize_workspace_size(b, n, r)
-    ws = _workspace(ws_bytes, dev)
+    ws = _workspace(lib.pcr_voxelize_workspace_size_c(b, c, n, r), dev)
     _lib.check(lib.pcr_spherical_avg_voxelize_forward(
         _ptr(features), _ptr(coords), b, c, n, r, _ptr(out), _ptr(ind), _ptr(cnt), _ptr(ws),
         ws.numel(), _stream()), "spherical_avg_voxelize_forward")
@@ -218,7 +217,7 @@ def avg_voxelize_forward(features, coords, resolution):
     ind = torch.empty((b, n), dtype=torch.int32, device=dev)
     cnt = torch.empty((b, r3), dtype=torch.int32, device=dev)
     lib = _lib.load()
-    ws = _workspace(lib.pcr_voxelize_workspace_size(b, n, r), dev)
+    ws = _workspace(lib.pcr_voxelize_workspace_size_c(b, c, n, r), dev)
     _lib.check(lib.pcr_avg_voxelize_forward(
         _ptr(features), _ptr(coords), b, c, n, r, _ptr(out), _ptr(ind), _ptr(cnt), _ptr(ws),
         ws.numel(), _stream()), "avg_voxelize_forward")

@@ -2,7 +2,9 @@
 65,536 points, k = 64, r = 64): normalisation, spherical / cube
 voxelisation on the global-atomic path, devoxelisation and KNN, against the
 oracle at sizes it finishes in seconds, plus size-independent properties at
-the full c5 cloud size."""
+the full c5 cloud size.  The large-cloud voxelisers sort the points by voxel
+(hipCUB radix sort) and sum each voxel in ascending point order, the oracle's
+order, so their grids are bit-exact."""
 import numpy as np
 import pytest
 
@@ -40,7 +42,7 @@ def test_sph_vox_large(dev):
     eo, ei, ec = oracle.spherical_avg_voxelize_forward(feat, nc, 64)
     assert np.array_equal(N(ind), ei)
     assert np.array_equal(N(cnt), ec.reshape(N(cnt).shape))
-    assert np.abs(N(out).reshape(eo.shape) - eo).max() <= SUM_ORDER_TOL
+    assert np.array_equal(N(out).reshape(eo.shape), eo)
 
 
 def test_cube_vox_large(dev):
@@ -54,7 +56,7 @@ def test_cube_vox_large(dev):
     eo, ei, ec = oracle.avg_voxelize_forward(feat, coords, r)
     assert np.array_equal(N(ind), ei)
     assert np.array_equal(N(cnt), ec.reshape(N(cnt).shape))
-    assert np.abs(N(out).reshape(eo.shape) - eo).max() <= SUM_ORDER_TOL
+    assert np.array_equal(N(out).reshape(eo.shape), eo)
 
 
 def test_sph_devox_large(dev):
@@ -133,3 +135,29 @@ def test_c5_cloud_properties(dev):
     grid = N(out).reshape(1, c, -1)
     assert (grid[:, :, cnt_[0] == 0] == 0).all()
     torch.cuda.synchronize()
+
+
+def test_sph_vox_large_without_feature_copy(dev):
+    """Workspace sized by pcr_voxelize_workspace_size (no channel count):
+    the direct-gather variant, same bits as the point-major one."""
+    import torch
+    from pcr_amd import _lib, ops
+    from pcr_amd.ops import _ptr
+    xyz, _, feat = gaussian_clouds(2, 9000, seed=47, c=6)
+    nc = oracle.normalize_sph(xyz)
+    b, c, n, r = 2, 6, 9000, 32
+    lib = _lib.load()
+    small = lib.pcr_voxelize_workspace_size(b, n, r)
+    assert lib.pcr_voxelize_workspace_size_c(b, c, n, r) > small
+    ws = torch.empty(small, dtype=torch.uint8, device=dev)
+    tf, tc = T(feat, dev), T(nc, dev)
+    out = torch.empty((b, c, r ** 3), device=dev)
+    ind = torch.empty((b, n), dtype=torch.int32, device=dev)
+    cnt = torch.empty((b, r ** 3), dtype=torch.int32, device=dev)
+    _lib.check(lib.pcr_spherical_avg_voxelize_forward(
+        _ptr(tf), _ptr(tc), b, c, n, r, _ptr(out), _ptr(ind), _ptr(cnt), _ptr(ws), ws.numel(),
+        torch.cuda.current_stream().cuda_stream), "vox")
+    ref = ops.spherical_avg_voxelize_forward(tf, tc, r)
+    eo, _, _ = oracle.spherical_avg_voxelize_forward(feat, nc, r)
+    assert np.array_equal(N(out).reshape(eo.shape), eo)
+    assert torch.equal(out, ref[0]) and torch.equal(ind, ref[1]) and torch.equal(cnt, ref[2])
