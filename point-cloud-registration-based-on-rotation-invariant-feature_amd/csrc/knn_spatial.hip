@@ -709,6 +709,8 @@ constexpr int kNB = 24;
 constexpr int kCap = 88;
 constexpr int kSelCache = 1024;  // candidates staged in LDS per workgroup
 constexpr int kSelMaxK = 32;
+constexpr int kCap64 = 176;  // the same selection for 32 < k <= 64 (large clouds)
+constexpr int kSelMaxK64 = 64;
 
 typedef float pf2 __attribute__((ext_vector_type(2)));
 
@@ -761,7 +763,7 @@ __device__ inline unsigned field_sum(unsigned v) {
   return (v & 0xFFFFu) + (v >> 16);
 }
 
-template <int NW, int CB, bool CL, bool PPF>
+template <int NW, int CB, bool CL, bool PPF, int CAP = kCap, int KSEL = kSelMaxK>
 __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     KnnSet qs, KnnSet cs, int k, float* __restrict__ dist, int* __restrict__ idx,
     const float* __restrict__ qxyz, const float* __restrict__ qnrm,
@@ -771,13 +773,14 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
   constexpr int NG = (NW + FPD - 1) / FPD;  // counter dwords per (bin, lane)
   // the histogram is dead once the cut is chosen: the collected keys reuse it
   constexpr int kHistBytes = NG * (kNB + 1) * kBlk * 4;
-  constexpr int kBufBytes = (kCap + 1) * kBlk * 8;  // row kCap: sink of masked writes
+  constexpr int kBufBytes = (CAP + 1) * kBlk * 8;  // row CAP: sink of masked writes
   __shared__ __align__(16) unsigned char sel_u[kHistBytes > kBufBytes ? kHistBytes : kBufBytes];
   unsigned* hist_s = (unsigned*)sel_u;
   kkey* buf_s = (kkey*)sel_u;
   __shared__ unsigned dest_s[kBlk];
   __shared__ __align__(16) float cand_s[CL ? 3 * kSelCache : 4];  // x | y | z
   __shared__ __align__(16) int cand_j[CL ? kSelCache : 4];
+  __shared__ __align__(16) float cand_w[CL ? 1 : NW][CL ? 4 : 3 * kBlk];  // a block per wave
   const int b = blockIdx.y;
   const int qblk = blockIdx.x;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -812,6 +815,37 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
   // LDS reads are issued before f runs, so their wait never covers the LDS
   // atomics / stores f issues.  Larger clouds: whole blocks round-robin over
   // the waves, skipped when no lane's box distance is below `lim`.
+  int nvisit = 0;  // candidate blocks this wave processed (diagnostics)
+  // Large clouds: the boxes of this wave's blocks (wv + NW (64 j + lane)) sit
+  // in registers and reach the whole wave by v_readlane, so the per-block
+  // tests never wait on memory; a processed block is loaded one candidate
+  // per lane (coalesced) into the wave's LDS slot and read back as
+  // broadcast ds_read_b128, as the cached path does.
+  constexpr int kBoxJ = 2;
+  const bool breg = !CL && nblk <= NW * kBlk * kBoxJ;
+  float bl[kBoxJ][6];
+#pragma unroll
+  for (int j = 0; j < kBoxJ; j++) {
+    const int blk = wv + NW * (j * kBlk + lane);
+    const bool ok = breg && blk < nblk;
+#pragma unroll
+    for (int a = 0; a < 6; a++) bl[j][a] = ok ? boxes[(size_t)blk * 8 + a] : 0.0f;
+  }
+  // visits this wave's blocks in order: g(blk, box[6]) (register boxes only)
+  auto for_blocks = [&](auto&& g) {
+#pragma unroll
+    for (int j = 0; j < kBoxJ; j++) {
+      for (int l = 0; l < kBlk; l++) {
+        const int blk = wv + NW * (j * kBlk + l);
+        if (blk >= nblk) return;
+        float b6[6];
+#pragma unroll
+        for (int a = 0; a < 6; a++) b6[a] = readlane_f(bl[j][a], l);
+        g(blk, b6);
+      }
+    }
+  };
+  int cj_cur = 0;  // original index of candidate `lane` of the block in process
   auto visit = [&](float lim, auto&& f) {
     if (CL) {
       constexpr int S = kBlk / NW;
@@ -850,9 +884,74 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
         if (g + 2 < ng) eval(g + 2, BX0, BY0, BZ0);
         if (g + 3 < ng) eval(g + 3, BX1, BY1, BZ1);
       }
+    } else if (breg) {
+      // which of this wave's blocks does any query lane need?  Lane l tests
+      // block wv + NW (64 j + l) against the 64 queries (read by v_readlane):
+      // one ballot per 64 blocks instead of one box test + ballot per block
+      unsigned long long vm[kBoxJ];
+#pragma unroll
+      for (int j = 0; j < kBoxJ; j++) {
+        bool need = false;
+        for (int q = 0; q < kBlk; q++) {
+          const float lq = readlane_f(lim, q);
+          const float lb = box_lb(readlane_f(qx, q), readlane_f(qy, q), readlane_f(qz, q), bl[j]);
+          need |= lb < lq;
+        }
+        need &= wv + NW * (j * kBlk + lane) < nblk;
+        vm[j] = __ballot(need);
+      }
+      // the visited blocks in order, the next one's candidates loaded (one
+      // per lane) while the current one is evaluated from the wave's LDS slot
+      int jc = 0;
+      auto next = [&]() {
+        while (jc < kBoxJ && vm[jc] == 0ull) jc++;
+        if (jc >= kBoxJ) return -1;
+        const int l = __builtin_ctzll(vm[jc]);
+        vm[jc] &= vm[jc] - 1ull;
+        return wv + NW * (jc * kBlk + l);
+      };
+      float* cw = cand_w[CL ? 0 : wv];
+      int cur = next();
+      float px = 0.0f, py = 0.0f, pz = 0.0f;
+      int pj = 0;
+      if (cur >= 0) {
+        const size_t cp = cbase + (size_t)cur * kBlk + lane;
+        px = cs.x[cp];
+        py = cs.y[cp];
+        pz = cs.z[cp];
+        pj = cs.j[cp];
+      }
+      while (cur >= 0) {
+        nvisit++;
+        const int nxt = next();
+        // the wave's previous block is fully read (LDS is in order per wave)
+        cw[lane] = px;
+        cw[kBlk + lane] = py;
+        cw[2 * kBlk + lane] = pz;
+        cj_cur = pj;
+        if (nxt >= 0) {
+          const size_t cp = cbase + (size_t)nxt * kBlk + lane;
+          px = cs.x[cp];
+          py = cs.y[cp];
+          pz = cs.z[cp];
+          pj = cs.j[cp];
+        }
+#pragma unroll 4
+        for (int t = 0; t < kBlk; t += 4) {
+          const float4 X = *(const float4*)(cw + t);
+          const float4 Y = *(const float4*)(cw + kBlk + t);
+          const float4 Z = *(const float4*)(cw + 2 * kBlk + t);
+          const pf2 d0 = cand_dist2(qx2, qy2, qz2, pf2{X.x, X.y}, pf2{Y.x, Y.y}, pf2{Z.x, Z.y});
+          const pf2 d1 = cand_dist2(qx2, qy2, qz2, pf2{X.z, X.w}, pf2{Y.z, Y.w}, pf2{Z.z, Z.w});
+          const float d[4] = {d0[0], d0[1], d1[0], d1[1]};
+          f(cur * kBlk + t, d);
+        }
+        cur = nxt;
+      }
     } else {
       for (int blk = wv; blk < nblk; blk += NW) {
         if (!__any(box_lb(qx, qy, qz, boxes + (size_t)blk * 8) < lim)) continue;
+        nvisit++;
         const float* bx = cs.x + cbase + (size_t)blk * kBlk;
         const float* by = cs.y + cbase + (size_t)blk * kBlk;
         const float* bz = cs.z + cbase + (size_t)blk * kBlk;
@@ -872,6 +971,12 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
   // original indices of the four candidates at sorted position pos
   auto cand_idx4 = [&](int pos) {
     if (CL) return *(const int4*)(cand_j + pos);
+    if (breg) {
+      const int t = pos & (kBlk - 1);
+      return int4{__builtin_amdgcn_readlane(cj_cur, t), __builtin_amdgcn_readlane(cj_cur, t + 1),
+                  __builtin_amdgcn_readlane(cj_cur, t + 2),
+                  __builtin_amdgcn_readlane(cj_cur, t + 3)};
+    }
     const int* bj = cs.j + cbase + pos;
     return int4{bj[0], bj[1], bj[2], bj[3]};
   };
@@ -881,9 +986,16 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
   // 1. bound
   {
     float dq = __builtin_inff();
-    for (int blk = wv; blk < nblk; blk += NW) {
-      const int real = min(kBlk, m - blk * kBlk);
-      if (real >= k) dq = fminf(dq, box_ub(qx, qy, qz, boxes + (size_t)blk * 8));
+    if (breg) {
+      for_blocks([&](int blk, const float (&b6)[6]) {
+        const int real = min(kBlk, m - blk * kBlk);
+        if (real >= k) dq = fminf(dq, box_ub(qx, qy, qz, b6));
+      });
+    } else {
+      for (int blk = wv; blk < nblk; blk += NW) {
+        const int real = min(kBlk, m - blk * kBlk);
+        if (real >= k) dq = fminf(dq, box_ub(qx, qy, qz, boxes + (size_t)blk * 8));
+      }
     }
     atomicMin(&dest_s[lane], __float_as_uint(dq));  // NaN never wins: fminf drops it
   }
@@ -950,7 +1062,7 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
         for (int g = 0; g < NG; g++) cut[g] = cum[g];
       }
     }
-    fallback = __any(qlive && (bstar < 0 || total > kCap));
+    fallback = __any(qlive && (bstar < 0 || total > CAP));
     if (qlive && !fallback) ucut = (unsigned)(ebase + bstar + 1) << 21;
     // slots of the waves before this one
     const int mg = wv / FPD;
@@ -964,8 +1076,10 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
   if (threadIdx.x == 0 && PCR_WG_LINEAR < 1024) {
     pcr_diag_stamps[PCR_WG_LINEAR][8] = fallback ? 1 : 0;
     pcr_diag_stamps[PCR_WG_LINEAR][9] = (unsigned long long)total;
+    pcr_diag_stamps[PCR_WG_LINEAR][10] = (unsigned long long)nvisit;
   }
 #endif
+  (void)nvisit;
 
   if (!fallback) {
     // 4. collect
@@ -981,7 +1095,7 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
 #pragma unroll
         for (int h = 0; h < 4; h++) {
 #if defined(KNN_EXP) && KNN_EXP == 9
-          buf_s[(take[h] ? slot : kCap) * kBlk + lane] = make_key(d[h], j4[h]);
+          buf_s[(take[h] ? slot : CAP) * kBlk + lane] = make_key(d[h], j4[h]);
           slot += take[h] ? 1 : 0;
 #else
           // exec-masked: only the taking lanes store (few lanes of a wave)
@@ -1006,7 +1120,7 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     //    and counts, for each, the keys below it in one sweep of all tmax
     //    rows; the sweep is compiled for a few key counts so that no compare
     //    is wasted on empty key slots and none needs a guard
-    constexpr int kE = kCap / NW;  // collected keys ranked per wave (max)
+    constexpr int kE = CAP / NW;  // collected keys ranked per wave (max)
     kkey key[kE];
     int rank[kE];
     const int ne = (tmax - wv + NW - 1) / NW;  // keys this wave holds: wv + e * NW < tmax
@@ -1033,6 +1147,10 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
       sweep(std::integral_constant<int, 7>());
     else if (ne <= 9)
       sweep(std::integral_constant<int, 9>());
+    else if (ne <= 13 && kE > 13)
+      sweep(std::integral_constant<int, (kE > 13 ? 13 : kE)>());
+    else if (ne <= 17 && kE > 17)
+      sweep(std::integral_constant<int, (kE > 17 ? 17 : kE)>());
     else
       sweep(std::integral_constant<int, kE>());
     PCR_STAMP(4);
@@ -1047,7 +1165,7 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     if (!qlive) return;
 
     // output slots wv, wv + NW, ...
-    constexpr int SPW = (kSelMaxK + NW - 1) / NW;
+    constexpr int SPW = (KSEL + NW - 1) / NW;
     const int n = qs.n;
     int jn[SPW];
 #pragma unroll
@@ -1147,7 +1265,7 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
   }
 }
 
-template <int NW, bool PPF>
+template <int NW, bool PPF, int CAP = kCap, int KSEL = kSelMaxK>
 static void launch_select(const KnnSet& qs, const KnnSet& cs, int b, int k, float* dist,
                           int* idx, const float* qxyz, const float* qnrm, const float* cxyz,
                           const float* cnrm, int relative, float* ppf, hipStream_t st) {
@@ -1155,14 +1273,14 @@ static void launch_select(const KnnSet& qs, const KnnSet& cs, int b, int k, floa
   const int per_wave = ceil_div(cs.nblk, NW) * kBlk;
   const dim3 grid(qs.nblk, b), blk(NW * 64);
   if (per_wave <= 255 && cs.npad <= kSelCache)
-    hipLaunchKernelGGL((knn_select_kernel<NW, 8, true, PPF>), grid, blk, 0, st, qs, cs, k, dist,
-                       idx, qxyz, qnrm, cxyz, cnrm, relative, ppf);
+    hipLaunchKernelGGL((knn_select_kernel<NW, 8, true, PPF, CAP, KSEL>), grid, blk, 0, st, qs, cs,
+                       k, dist, idx, qxyz, qnrm, cxyz, cnrm, relative, ppf);
   else if (per_wave <= 255)
-    hipLaunchKernelGGL((knn_select_kernel<NW, 8, false, PPF>), grid, blk, 0, st, qs, cs, k, dist,
-                       idx, qxyz, qnrm, cxyz, cnrm, relative, ppf);
+    hipLaunchKernelGGL((knn_select_kernel<NW, 8, false, PPF, CAP, KSEL>), grid, blk, 0, st, qs,
+                       cs, k, dist, idx, qxyz, qnrm, cxyz, cnrm, relative, ppf);
   else
-    hipLaunchKernelGGL((knn_select_kernel<NW, 16, false, PPF>), grid, blk, 0, st, qs, cs, k, dist,
-                       idx, qxyz, qnrm, cxyz, cnrm, relative, ppf);
+    hipLaunchKernelGGL((knn_select_kernel<NW, 16, false, PPF, CAP, KSEL>), grid, blk, 0, st, qs,
+                       cs, k, dist, idx, qxyz, qnrm, cxyz, cnrm, relative, ppf);
 }
 
 size_t knn_ws_size(int b, int n, int m) {
@@ -1224,6 +1342,11 @@ static pcr_status launch_block(const KnnSet& qs, const KnnSet& cs, int b, int k,
 #endif
   if (k <= kSelMaxK && impl == 0) {
     launch_select<8, PPF>(qs, cs, b, k, dist, idx, qxyz, qnrm, cxyz, cnrm, relative, ppf, st);
+  } else if (k <= kSelMaxK64 && cs.npad > kSelCache && impl == 0) {
+    // large clouds (BASELINE c5, k = 64): the pruned threshold selection with
+    // room for 2.75 k collected keys per query
+    launch_select<8, PPF, kCap64, kSelMaxK64>(qs, cs, b, k, dist, idx, qxyz, qnrm, cxyz, cnrm,
+                                              relative, ppf, st);
   } else if (k <= 16)
     launch_block_k<16, PPF>(qs, cs, b, k, dist, idx, qxyz, qnrm, cxyz, cnrm, relative, ppf, st);
   else if (k <= 32)

@@ -28,9 +28,16 @@ lib.pcr_diag_read_knn(buf)
 a = np.frombuffer(buf, dtype=np.uint64).reshape(1024, 16).astype(np.int64)
 ok = a[:, 1] > 0
 d = a[ok, 1] - a[ok, 0]
+for p in range(1, 7):
+    okp = (a[:, p] > 0) & (a[:, p - 1] > 0)
+    if okp.any():
+        print("phase %d->%d: median %d cycles" % (p - 1, p, np.median(a[okp, p] - a[okp, p - 1])))
 print("workgroups with stamps", ok.sum())
 print("scan cycles: median %d  p90 %d  max %d" % (np.median(d), np.percentile(d, 90), d.max()))
-for name, col in (("flushes", 8), ("blocks processed", 9)):
+names = (("flushes", 8), ("blocks processed", 9)) if os.environ.get("IMPL") == "block" else \
+    (("fallback (select)", 8), ("collected keys (select)", 9),
+     ("blocks visited by wave 0 in the count pass (select)", 10))
+for name, col in names:
     v = a[ok, col]
     print("%s per wave: median %d  p90 %d  max %d  (of %d blocks)" %
           (name, np.median(v), np.percentile(v, 90), v.max(), (n + 63) // 64))
