@@ -763,7 +763,8 @@ __device__ inline unsigned field_sum(unsigned v) {
   return (v & 0xFFFFu) + (v >> 16);
 }
 
-template <int NW, int CB, bool CL, bool PPF, int CAP = kCap, int KSEL = kSelMaxK>
+template <int NW, int CB, bool CL, bool PPF, int CAP = kCap, int KSEL = kSelMaxK,
+          int CACHE = kSelCache>
 __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     KnnSet qs, KnnSet cs, int k, float* __restrict__ dist, int* __restrict__ idx,
     const float* __restrict__ qxyz, const float* __restrict__ qnrm,
@@ -778,8 +779,8 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
   unsigned* hist_s = (unsigned*)sel_u;
   kkey* buf_s = (kkey*)sel_u;
   __shared__ unsigned dest_s[kBlk];
-  __shared__ __align__(16) float cand_s[CL ? 3 * kSelCache : 4];  // x | y | z
-  __shared__ __align__(16) int cand_j[CL ? kSelCache : 4];
+  __shared__ __align__(16) float cand_s[CL ? 3 * CACHE : 4];  // x | y | z
+  __shared__ __align__(16) int cand_j[CL ? CACHE : 4];
   __shared__ __align__(16) float cand_w[CL ? 1 : NW][CL ? 4 : 3 * kBlk];  // a block per wave
   const int b = blockIdx.y;
   const int qblk = blockIdx.x;
@@ -802,15 +803,15 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     for (int i = threadIdx.x; i < np; i += NW * kBlk) {
       cand_s[i] = cs.x[cbase + i];
       cand_j[i] = cs.j[cbase + i];
-      cand_s[kSelCache + i] = cs.y[cbase + i];
-      cand_s[2 * kSelCache + i] = cs.z[cbase + i];
+      cand_s[CACHE + i] = cs.y[cbase + i];
+      cand_s[2 * CACHE + i] = cs.z[cbase + i];
     }
   }
   // Visit every group of four candidates this wave owns: f(pos, d[4]), pos =
   // sorted position of the group's first candidate.  Cached clouds: wave w
   // owns candidates [64 b + w S, 64 b + w S + S) of every block b (S = 64 /
   // NW), so the candidates near the queries -- the ones the collect pass
-  // keeps -- are spread over all waves; no pruning (at <= kSelCache points a
+  // keeps -- are spread over all waves; no pruning (at <= CACHE points a
   // 64-query block reaches nearly every candidate block).  The next group's
   // LDS reads are issued before f runs, so their wait never covers the LDS
   // atomics / stores f issues.  Larger clouds: whole blocks round-robin over
@@ -821,8 +822,10 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
   // tests never wait on memory; a processed block is loaded one candidate
   // per lane (coalesced) into the wave's LDS slot and read back as
   // broadcast ds_read_b128, as the cached path does.
+  // (only for clouds of more than 32k points: with fewer blocks per wave the
+  // per-block tests are cheaper than the 64-query ballot sweep)
   constexpr int kBoxJ = 2;
-  const bool breg = !CL && nblk <= NW * kBlk * kBoxJ;
+  const bool breg = !CL && nblk > NW * kBlk && nblk <= NW * kBlk * kBoxJ;
   float bl[kBoxJ][6];
 #pragma unroll
   for (int j = 0; j < kBoxJ; j++) {
@@ -857,8 +860,8 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
       auto rd = [&](int g, float4& X, float4& Y, float4& Z) {
         const int o = off(g);
         X = *(const float4*)(cand_s + o);
-        Y = *(const float4*)(cand_s + kSelCache + o);
-        Z = *(const float4*)(cand_s + 2 * kSelCache + o);
+        Y = *(const float4*)(cand_s + CACHE + o);
+        Z = *(const float4*)(cand_s + 2 * CACHE + o);
       };
       auto eval = [&](int g, const float4& X, const float4& Y, const float4& Z) {
         const pf2 d0 = cand_dist2(qx2, qy2, qz2, pf2{X.x, X.y}, pf2{Y.x, Y.y}, pf2{Z.x, Z.y});
@@ -1272,15 +1275,16 @@ static void launch_select(const KnnSet& qs, const KnnSet& cs, int b, int k, floa
   // a wave sees ceil(nblk / NW) * 64 candidates: byte fields when that fits
   const int per_wave = ceil_div(cs.nblk, NW) * kBlk;
   const dim3 grid(qs.nblk, b), blk(NW * 64);
+#define PCR_SEL(CBV, CLV, CACHEV)                                                             \
+  hipLaunchKernelGGL((knn_select_kernel<NW, CBV, CLV, PPF, CAP, KSEL, CACHEV>), grid, blk, 0, st, \
+                     qs, cs, k, dist, idx, qxyz, qnrm, cxyz, cnrm, relative, ppf)
   if (per_wave <= 255 && cs.npad <= kSelCache)
-    hipLaunchKernelGGL((knn_select_kernel<NW, 8, true, PPF, CAP, KSEL>), grid, blk, 0, st, qs, cs,
-                       k, dist, idx, qxyz, qnrm, cxyz, cnrm, relative, ppf);
+    PCR_SEL(8, true, kSelCache);
   else if (per_wave <= 255)
-    hipLaunchKernelGGL((knn_select_kernel<NW, 8, false, PPF, CAP, KSEL>), grid, blk, 0, st, qs,
-                       cs, k, dist, idx, qxyz, qnrm, cxyz, cnrm, relative, ppf);
+    PCR_SEL(8, false, kSelCache);
   else
-    hipLaunchKernelGGL((knn_select_kernel<NW, 16, false, PPF, CAP, KSEL>), grid, blk, 0, st, qs,
-                       cs, k, dist, idx, qxyz, qnrm, cxyz, cnrm, relative, ppf);
+    PCR_SEL(16, false, kSelCache);
+#undef PCR_SEL
 }
 
 size_t knn_ws_size(int b, int n, int m) {

@@ -42,10 +42,19 @@ def test_select_k_values(dev, k):
     check_self(dev, xyz, k)
 
 
-@pytest.mark.parametrize("n", [1000, 65, 129, 700])
+@pytest.mark.parametrize("n", [1000, 65, 129, 700, 1025, 2048, 3001, 4096])
 def test_select_ragged_sizes(dev, n):
+    """<= 1024 points: the LDS candidate cache; beyond (BASELINE c3: 2048):
+    the global-memory sweep with per-block box tests and 16-bit fields."""
     xyz, _, _ = gaussian_clouds(2, n, seed=n)
     check_self(dev, xyz, 32)
+
+
+def test_select_cached_2k_duplicates_and_k16(dev):
+    xyz, _, _ = gaussian_clouds(2, 2048, seed=77)
+    xyz[0, :, 500:700] = xyz[0, :, 500:501]  # fallback blocks past the LDS cache
+    check_self(dev, xyz, 32)
+    check_self(dev, xyz, 16)
 
 
 def test_select_lattice_ties(dev):
