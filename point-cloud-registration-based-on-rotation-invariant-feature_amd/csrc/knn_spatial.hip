@@ -822,10 +822,8 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
   // tests never wait on memory; a processed block is loaded one candidate
   // per lane (coalesced) into the wave's LDS slot and read back as
   // broadcast ds_read_b128, as the cached path does.
-  // (only for clouds of more than 32k points: with fewer blocks per wave the
-  // per-block tests are cheaper than the 64-query ballot sweep)
   constexpr int kBoxJ = 2;
-  const bool breg = !CL && nblk > NW * kBlk && nblk <= NW * kBlk * kBoxJ;
+  const bool breg = !CL && nblk <= NW * kBlk * kBoxJ;
   float bl[kBoxJ][6];
 #pragma unroll
   for (int j = 0; j < kBoxJ; j++) {
@@ -891,17 +889,32 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
       // which of this wave's blocks does any query lane need?  Lane l tests
       // block wv + NW (64 j + l) against the 64 queries (read by v_readlane):
       // one ballot per 64 blocks instead of one box test + ballot per block
+      // (up to 64 blocks per wave, i.e. clouds of <= 32k points: one box
+      // test + ballot per block is cheaper than the 64-query sweep)
       unsigned long long vm[kBoxJ];
+      if (nblk <= NW * kBlk) {
+        vm[0] = 0ull;
 #pragma unroll
-      for (int j = 0; j < kBoxJ; j++) {
-        bool need = false;
-        for (int q = 0; q < kBlk; q++) {
-          const float lq = readlane_f(lim, q);
-          const float lb = box_lb(readlane_f(qx, q), readlane_f(qy, q), readlane_f(qz, q), bl[j]);
-          need |= lb < lq;
+        for (int j = 1; j < kBoxJ; j++) vm[j] = 0ull;
+        for (int l = 0; wv + NW * l < nblk; l++) {
+          float b6[6];
+#pragma unroll
+          for (int a = 0; a < 6; a++) b6[a] = readlane_f(bl[0][a], l);
+          if (__any(box_lb(qx, qy, qz, b6) < lim)) vm[0] |= 1ull << l;
         }
-        need &= wv + NW * (j * kBlk + lane) < nblk;
-        vm[j] = __ballot(need);
+      } else {
+#pragma unroll
+        for (int j = 0; j < kBoxJ; j++) {
+          bool need = false;
+          for (int q = 0; q < kBlk; q++) {
+            const float lq = readlane_f(lim, q);
+            const float lb =
+                box_lb(readlane_f(qx, q), readlane_f(qy, q), readlane_f(qz, q), bl[j]);
+            need |= lb < lq;
+          }
+          need &= wv + NW * (j * kBlk + lane) < nblk;
+          vm[j] = __ballot(need);
+        }
       }
       // the visited blocks in order, the next one's candidates loaded (one
       // per lane) while the current one is evaluated from the wave's LDS slot
