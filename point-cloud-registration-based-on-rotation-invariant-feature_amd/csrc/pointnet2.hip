@@ -67,10 +67,11 @@ __device__ inline unsigned long long wave_max_u64(unsigned long long v) {
 }
 
 // Posts this wave's best (key, xyz) and returns the workgroup's best after
-// the single barrier.  slots[2][kFpsWaves]; parity alternates per step, so a
-// slot is rewritten only after every wave has passed the next barrier.
+// the single barrier.  slots[2][NWV]; parity alternates per step, so a slot
+// is rewritten only after every wave has passed the next barrier.
+template <int NWV = kFpsWaves>
 __device__ inline FpsSlot fps_block_best(unsigned long long key, float x, float y, float z,
-                                         FpsSlot (*slots)[kFpsWaves], int parity) {
+                                         FpsSlot (*slots)[NWV], int parity) {
   const unsigned long long wbest = wave_max_u64(key);
   if (key == wbest && wbest != 0ull) {  // keys are unique: exactly one lane
     FpsSlot s;
@@ -86,7 +87,7 @@ __device__ inline FpsSlot fps_block_best(unsigned long long key, float x, float 
   lds_barrier();
   FpsSlot best = slots[parity][0];
 #pragma unroll
-  for (int w = 1; w < kFpsWaves; w++) {
+  for (int w = 1; w < NWV; w++) {
     const FpsSlot s = slots[parity][w];
     if (s.key > best.key) best = s;
   }
@@ -141,23 +142,26 @@ __global__ __launch_bounds__(kFpsThreads) void fps_reg_kernel(const float* __res
 }
 
 // clouds beyond the register path: distances in the workspace, points
-// streamed from global memory (L2-resident) every step
-__global__ __launch_bounds__(kFpsThreads) void fps_big_kernel(const float* __restrict__ coords,
-                                                               int n, int m,
-                                                               float* __restrict__ dist_ws,
-                                                               int* __restrict__ indices) {
-  __shared__ FpsSlot slots[2][kFpsWaves];
+// streamed from global memory (L2-resident) every step; 1024 threads, so a
+// thread walks n / 1024 points per step
+constexpr int kFpsBigThreads = 1024;
+__global__ __launch_bounds__(kFpsBigThreads) void fps_big_kernel(const float* __restrict__ coords,
+                                                                  int n, int m,
+                                                                  float* __restrict__ dist_ws,
+                                                                  int* __restrict__ indices) {
+  constexpr int NWV = kFpsBigThreads / kWave;
+  __shared__ FpsSlot slots[2][NWV];
   const int b = blockIdx.x, tid = threadIdx.x;
   const float* xs = coords + (size_t)b * 3 * n;
   float* dist = dist_ws + (size_t)b * n;
   int* out = indices + (size_t)b * m;
-  for (int k = tid; k < n; k += kFpsThreads) dist[k] = 1e38f;
+  for (int k = tid; k < n; k += kFpsBigThreads) dist[k] = 1e38f;
   float x1 = xs[0], y1 = xs[n], z1 = xs[2 * n];
   if (tid == 0) out[0] = 0;
   for (int j = 1; j < m; j++) {
     unsigned long long key = 0ull;
     float bx = 0.0f, by = 0.0f, bz = 0.0f;
-    for (int k = tid; k < n; k += kFpsThreads) {
+    for (int k = tid; k < n; k += kFpsBigThreads) {
       const float x = xs[k], y = xs[k + n], z = xs[k + 2 * n];
       const float dd = fminf(pcr_sumsq3f(x - x1, y - y1, z - z1), dist[k]);
       dist[k] = dd;  // each thread owns its points: no cross-thread hazard
@@ -169,7 +173,7 @@ __global__ __launch_bounds__(kFpsThreads) void fps_big_kernel(const float* __res
         bz = z;
       }
     }
-    const FpsSlot best = fps_block_best(key, bx, by, bz, slots, j & 1);
+    const FpsSlot best = fps_block_best<NWV>(key, bx, by, bz, slots, j & 1);
     x1 = best.x;
     y1 = best.y;
     z1 = best.z;
@@ -327,8 +331,8 @@ extern "C" pcr_status pcr_furthest_point_sampling(const float* coords, int b, in
     const size_t need = pcr_fps_workspace_size(b, n);
     PCR_REQUIRE(workspace != nullptr && workspace_bytes >= need,
                 "furthest_point_sampling: workspace too small (%zu < %zu)", workspace_bytes, need);
-    hipLaunchKernelGGL(fps_big_kernel, grid, block, 0, st, coords, n, m, (float*)workspace,
-                       indices);
+    hipLaunchKernelGGL(fps_big_kernel, grid, dim3(kFpsBigThreads), 0, st, coords, n, m,
+                       (float*)workspace, indices);
   }
   return launch_status("furthest_point_sampling");
 }
