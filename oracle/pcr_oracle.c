@@ -554,28 +554,8 @@ void orc_mutual_nn(int p, int n1, int n2, int c, const float *f1, const float *f
  * ties open), then the Python loop over the ranking, then Gram-Schmidt and the
  * projection.  The GPU kernel (csrc/lrf.hip) replaces the sort by two
  * arg-max passes.  This restatement is the independent check of that.  The mean
- * uses the kernel's fixed fp64 order: lane t of 256 sums points t, t+256, ...;
- * each group of 64 lanes is halved (l += l+s, s = 32..1); the 4 group sums
- * combine as (g0 + g2) + (g1 + g3).  status: 0 ok, 1/2/3 = the asserts at
- * :159, :169, :177. */
-static double lrf_axis_sum(const float *x, int n) {
-  double part[256], g[4];
-  int t, s, w;
-  for (t = 0; t < 256; t++) {
-    double acc = 0.0;
-    int i;
-    for (i = t; i < n; i += 256) acc += (double)x[i];
-    part[t] = acc;
-  }
-  for (w = 0; w < 4; w++) {
-    double *l = part + 64 * w;
-    for (s = 32; s > 0; s >>= 1)
-      for (t = 0; t < s; t++) l[t] += l[t + s];
-    g[w] = l[0];
-  }
-  return (g[0] + g[2]) + (g[1] + g[3]);
-}
-
+ * uses the fixed fp64 order of cloud_mean_axis (the kernel's order, below).
+ * status: 0 ok, 1/2/3 = the asserts at :159, :169, :177. */
 static const float *lrf_sort_norms;
 static int lrf_rank_cmp(const void *pa, const void *pb) {
   int a = *(const int *)pa, b = *(const int *)pb;
@@ -597,7 +577,7 @@ void orc_lrf(int b, int n, const float *coords, float *new_coords, float *basis,
     int *rank = (int *)malloc(sizeof(int) * n);
     float mean[3], B[9], p0[3], p1[3], n0, n1 = 0.0f, bx[3];
     int a, i, j, st = 0, i0 = -1, i1 = -1;
-    for (a = 0; a < 3; a++) mean[a] = (float)(lrf_axis_sum(X + (size_t)a * n, n) / (double)n);
+    for (a = 0; a < 3; a++) mean[a] = cloud_mean_axis(X + (size_t)a * n, n);
     for (i = 0; i < n; i++) {
       for (a = 0; a < 3; a++) nc[i + a * n] = X[i + a * n] - mean[a];
       nr[i] = pcr_norm3f(nc[i], nc[i + n], nc[i + 2 * n]);

@@ -7,14 +7,14 @@
 // (norm, -index).  base_y is the first qualifying point in rank order, which
 // is the arg-max of the same key over the qualifying points.  So each is one
 // block-wide max over 64-bit keys.  The cloud (12 B per point) is read four
-// times: the mean, the two arg-max passes and the projection.  The last three
-// hit L2, since the cloud is <= 100 KB.
+// times: the mean, the two arg-max passes and the projection; 1024 threads
+// per cloud, so a 65,536-point cloud is 64 points per thread per pass.
 #include "common.hpp"
 
 namespace pcr {
 namespace {
 
-constexpr int kLrfThreads = 256;
+constexpr int kLrfThreads = 1024;
 constexpr int kLrfWaves = kLrfThreads / kWave;
 
 __device__ inline unsigned long long block_max_u64(unsigned long long v,
@@ -43,9 +43,10 @@ __global__ __launch_bounds__(kLrfThreads) void lrf_kernel(const float* __restric
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const float* X = coords + (size_t)b * 3 * n;
 
-  // 1. per-axis mean, fixed order (orc_lrf restates it): thread t sums
-  //    points t, t+256, ... ascending in double; each wave halves its 64
-  //    partials (l += l+s, s = 32..1); then (w0 + w2) + (w1 + w3).
+  // 1. per-axis mean in the fixed order of the voxel prep's cloud_mean (the
+  //    oracle's cloud_mean_axis): thread t of 1024 sums points t, t+1024, ...
+  //    ascending in double; each wave halves its 64 partials (l += l+s,
+  //    s = 32..1); the 16 wave sums are halved the same way (s = 8..1).
   double s[3] = {0.0, 0.0, 0.0};
   for (int k = tid; k < n; k += kLrfThreads) {
     s[0] += (double)X[k];
@@ -65,8 +66,14 @@ __global__ __launch_bounds__(kLrfThreads) void lrf_kernel(const float* __restric
   float mean[3];
 #pragma unroll
   for (int a = 0; a < 3; a++) {
-    const double t = (dred[a][0] + dred[a][2]) + (dred[a][1] + dred[a][3]);
-    mean[a] = (float)(t / (double)n);
+    double v[kLrfWaves];
+#pragma unroll
+    for (int i = 0; i < kLrfWaves; i++) v[i] = dred[a][i];
+#pragma unroll
+    for (int off = kLrfWaves / 2; off > 0; off >>= 1)
+#pragma unroll
+      for (int i = 0; i < off; i++) v[i] += v[i + off];
+    mean[a] = (float)(v[0] / (double)n);
   }
 
   // 2. base_x = rank 0
