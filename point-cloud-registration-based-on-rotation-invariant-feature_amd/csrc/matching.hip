@@ -121,6 +121,11 @@ __global__ __launch_bounds__(256) void match_tile_kernel(
   const float* s1 = sq1 + (size_t)p * n1;
   const float* s2 = sq2 + (size_t)p * n2;
   unsigned long long cmin[2] = {~0ull, ~0ull};
+  // row minima: R[16 ti + v] = min over this lane's two columns, then a
+  // transpose-reduction over the 32 lanes of each half (xor 16, 8, 4, 2, 1:
+  // each step swaps half of the remaining rows with the partner), 31 64-bit
+  // shuffles instead of 5 per row; lane l ends with row s = l & 31
+  unsigned long long R[32];
 #pragma unroll
   for (int ti = 0; ti < 2; ti++) {
 #pragma unroll
@@ -139,14 +144,24 @@ __global__ __launch_bounds__(256) void match_tile_kernel(
           cmin[tj] = kc < cmin[tj] ? kc : cmin[tj];
         }
       }
-      // min over the 32 columns of this lane half
-#pragma unroll
-      for (int off = 16; off > 0; off >>= 1) {
-        const unsigned long long o = shfl_xor_u64(rmin, off);
-        rmin = o < rmin ? o : rmin;
-      }
-      if ((lane & 31) == 0 && row < n1) atomicMin(rb + row, rmin);
+      R[ti * 16 + v] = rmin;
     }
+  }
+#pragma unroll
+  for (int h = 16; h >= 1; h >>= 1) {
+    const bool up = (lane & h) != 0;
+#pragma unroll
+    for (int i = 0; i < h; i++) {
+      const unsigned long long send = up ? R[i] : R[i + h];
+      const unsigned long long keep = up ? R[i + h] : R[i];
+      const unsigned long long recv = shfl_xor_u64(send, h);
+      R[i] = recv < keep ? recv : keep;
+    }
+  }
+  {
+    const int sidx = lane & 31, ti = sidx >> 4, v = sidx & 15;
+    const int row = i0 + wi * 64 + ti * 32 + (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5);
+    if (row < n1) atomicMin(rb + row, R[0]);
   }
 #pragma unroll
   for (int tj = 0; tj < 2; tj++) {
