@@ -189,7 +189,7 @@ __global__ __launch_bounds__(kNnThreads) void three_nn_kernel(
     const float* __restrict__ points, const float* __restrict__ centers,
     const float* __restrict__ cfeat, int c, int m, int n, float* __restrict__ out,
     int* __restrict__ inds, float* __restrict__ wgts) {
-  __shared__ float tile[3][kNnTile];
+  __shared__ __align__(16) float tile[3][kNnTile];
   const int b = blockIdx.y;
   const int j = blockIdx.x * kNnThreads + threadIdx.x;
   const bool active = j < n;
@@ -213,8 +213,27 @@ __global__ __launch_bounds__(kNnThreads) void three_nn_kernel(
     }
     __syncthreads();
     if (active) {
-      for (int q = 0; q < cnt; q++) {
+      // four candidates per broadcast ds_read_b128 of x, y and z; the
+      // distances are computed before the (rarely taken) insertions, which
+      // stay in candidate order
+      const int c4 = cnt & ~3;
+      for (int q = 0; q < c4; q += 4) {
+        const float4 X = *reinterpret_cast<const float4*>(&tile[0][q]);
+        const float4 Y = *reinterpret_cast<const float4*>(&tile[1][q]);
+        const float4 Z = *reinterpret_cast<const float4*>(&tile[2][q]);
         // (ux - x)^2 + (uy - y)^2 + (uz - z)^2 (neighbor_interpolate.cu:42)
+        const float d0 = pcr_sumsq3f(ux - X.x, uy - Y.x, uz - Z.x);
+        const float d1 = pcr_sumsq3f(ux - X.y, uy - Y.y, uz - Z.y);
+        const float d2 = pcr_sumsq3f(ux - X.z, uy - Y.z, uz - Z.z);
+        const float d3 = pcr_sumsq3f(ux - X.w, uy - Y.w, uz - Z.w);
+        if (fminf(fminf(d0, d1), fminf(d2, d3)) < best[2]) {
+          pcr_three_nn_insert(d0, t0 + q, best, besti);
+          pcr_three_nn_insert(d1, t0 + q + 1, best, besti);
+          pcr_three_nn_insert(d2, t0 + q + 2, best, besti);
+          pcr_three_nn_insert(d3, t0 + q + 3, best, besti);
+        }
+      }
+      for (int q = c4; q < cnt; q++) {
         const float d = pcr_sumsq3f(ux - tile[0][q], uy - tile[1][q], uz - tile[2][q]);
         pcr_three_nn_insert(d, t0 + q, best, besti);
       }
@@ -223,16 +242,23 @@ __global__ __launch_bounds__(kNnThreads) void three_nn_kernel(
   if (!active) return;
   float w[3];
   pcr_three_nn_weights(best, w);
-  float* W = wgts + (size_t)b * 3 * n;
-  int* I = inds + (size_t)b * 3 * n;
+  if (blockIdx.z == 0) {
+    float* W = wgts + (size_t)b * 3 * n;
+    int* I = inds + (size_t)b * 3 * n;
 #pragma unroll
-  for (int a = 0; a < 3; a++) {
-    W[j + a * n] = w[a];
-    I[j + a * n] = besti[a];
+    for (int a = 0; a < 3; a++) {
+      W[j + a * n] = w[a];
+      I[j + a * n] = besti[a];
+    }
   }
+  // channel group blockIdx.z: the (cheap) scan is repeated per group so the
+  // gathers of the interpolation spread over gridDim.z times more waves
+  const int cpg = (c + gridDim.z - 1) / gridDim.z;
+  const int ch0 = blockIdx.z * cpg, ch1 = min(c, ch0 + cpg);
   const float* F = cfeat + (size_t)b * c * m;
   float* O = out + (size_t)b * c * n;
-  for (int ch = 0; ch < c; ch++) {
+#pragma unroll 4
+  for (int ch = ch0; ch < ch1; ch++) {
     const float* f = F + (size_t)ch * m;
     // no centres at all: the reference reads feature 0 of an empty tensor
     O[(size_t)ch * n + j] =
@@ -345,7 +371,8 @@ extern "C" pcr_status pcr_three_nn_interpolate_forward(const float* points, cons
   PCR_REQUIRE(b >= 0 && c >= 0 && m >= 0 && n >= 0 && b <= 65535,
               "three_nearest_neighbors_interpolate_forward: invalid sizes");
   if (b == 0 || n == 0) return PCR_OK;
-  hipLaunchKernelGGL(three_nn_kernel, dim3(ceil_div(n, kNnThreads), b), dim3(kNnThreads), 0,
+  const int cgroups = c >= 64 ? 4 : (c >= 16 ? 2 : 1);
+  hipLaunchKernelGGL(three_nn_kernel, dim3(ceil_div(n, kNnThreads), b, cgroups), dim3(kNnThreads), 0,
                      as_stream(stream), points, centers, centers_features, c, m, n, out, indices,
                      weights);
   return launch_status("three_nearest_neighbors_interpolate_forward");
