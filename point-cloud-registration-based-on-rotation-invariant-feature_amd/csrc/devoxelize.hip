@@ -112,6 +112,110 @@ __global__ __launch_bounds__(kBwdThreads) void devox_bwd_kernel(
   float* gx = grad_x + ((size_t)b * c + c0) * r3;
   // 1. accumulate the hot window in LDS; note whether any corner falls outside
   int outside = 0;
+  if (skip_neg) {
+    // Spherical grads: the 64 points of a wave mostly share a handful of
+    // corner sets (the integer-division quirk pins gamma_lo = 0, so every
+    // corner set is one of ~28 (alpha_lo, beta_lo) cells plus three "hi"
+    // flags).  One LDS float atomic per (point, corner, channel) serialises
+    // on those shared addresses, at about 0.44 lane-ops per CU-cycle.  So the
+    // wave sorts its points by corner set (bitonic over lanes), sums w * g
+    // per segment with a segmented shuffle scan, and only the segment tails
+    // add into the window: distinct addresses, no collisions.  Points whose
+    // corners do not follow that pattern take the per-point atomics.
+    const int lane = tid & 63, wv = tid >> 6;
+    constexpr long long kNoKey = (1ll << 57) - 1;  // above every key (ci0 < 2^22)
+    for (int base = wv * kWave; base < n; base += kBwdThreads) {
+      const int i = base + lane;
+      const bool live = i < n && I[i] != -1;
+      int ci[8];
+      float cw[8];
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        ci[q] = live ? I[i + (size_t)q * n] : 0;
+        cw[q] = live ? Wt[i + (size_t)q * n] : 0.0f;
+      }
+      const int d1 = ci[1] - ci[0], d2 = ci[2] - ci[0], d4 = ci[4] - ci[0];
+      // regular corner set: idx1 = idx0 + b, idx2 = idx0 + a, idx4 = idx0 + g,
+      // idx3 = idx2 + b, idx5 = idx4 + b, idx6 = idx4 + a, idx7 = idx6 + b
+      const bool reg = live && (d1 == 0 || d1 == 1) && d2 >= 0 && d4 >= 0 && ci[3] == ci[2] + d1 &&
+            ci[5] == ci[4] + d1 && ci[6] == ci[4] + d2 && ci[7] == ci[6] + d1 && ci[0] >= 0 &&
+            ci[7] < hw && hw < (1 << 22) && d2 < 4096 && d4 < (1 << 22);
+      float gv[kBwdMaxG];
+#pragma unroll
+      for (int g = 0; g < kBwdMaxG; g++) gv[g] = (live && g < gcount) ? gy[(size_t)g * n + i] : 0.0f;
+      if (live && !reg) {  // irregular: per-point atomics (as below)
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+          outside |= (ci[q] >= hw && ci[q] < r3);
+          if (ci[q] >= 0 && ci[q] < hw)
+            for (int g = 0; g < gcount; g++) atomicAdd(&acc_s[g * hw + ci[q]], cw[q] * gv[g]);
+        }
+      }
+      // sort key: corner set (idx0, then the three deltas); ties by lane
+      const long long key0 =
+          reg ? (((long long)ci[0] << 35) | ((long long)d4 << 13) | ((long long)d2 << 1) | d1)
+              : kNoKey;
+      long long k2 = (key0 << 6) | lane;
+#pragma unroll
+      for (int k = 2; k <= kWave; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+          const long long o = (long long)shfl_xor_u64((unsigned long long)k2, j);
+          const bool lower = (lane & j) == 0, asc = (lane & k) == 0;
+          const long long mn = o < k2 ? o : k2, mx = o < k2 ? k2 : o;
+          k2 = (lower == asc) ? mn : mx;
+        }
+      }
+      const int src = (int)(k2 & 63);
+      const long long mykey = k2 >> 6;
+      const bool mine = mykey < kNoKey;
+      float v[8][kBwdMaxG];
+      {
+        float w8[8], g4[kBwdMaxG];
+#pragma unroll
+        for (int q = 0; q < 8; q++) w8[q] = __shfl(cw[q], src, kWave);
+#pragma unroll
+        for (int g = 0; g < kBwdMaxG; g++) g4[g] = __shfl(gv[g], src, kWave);
+#pragma unroll
+        for (int q = 0; q < 8; q++)
+#pragma unroll
+          for (int g = 0; g < kBwdMaxG; g++) v[q][g] = mine ? w8[q] * g4[g] : 0.0f;
+      }
+      const int c0 = __shfl(ci[0], src, kWave);
+      const long long prevk = (long long)__shfl_up((unsigned long long)mykey, 1, kWave);
+      const long long nextk = (long long)__shfl_down((unsigned long long)mykey, 1, kWave);
+      int seg = (lane == 0 || prevk != mykey) ? lane : 0;
+#pragma unroll
+      for (int d = 1; d < kWave; d <<= 1) {
+        const int o = __shfl_up(seg, d, kWave);
+        if (lane >= d) seg = max(seg, o);
+      }
+#pragma unroll
+      for (int d = 1; d < kWave; d <<= 1) {
+        const bool add = lane - d >= seg;
+#pragma unroll
+        for (int q = 0; q < 8; q++)
+#pragma unroll
+          for (int g = 0; g < kBwdMaxG; g++) {
+            const float o = __shfl_up(v[q][g], d, kWave);
+            if (add) v[q][g] += o;
+          }
+      }
+      const bool tail = mine && (lane == kWave - 1 || nextk != mykey);
+      if (tail) {
+        const int e1 = (int)(mykey & 1), e2 = (int)((mykey >> 1) & 0xFFF),
+                  e4 = (int)((mykey >> 13) & 0x3FFFFF);
+        const int cq[8] = {c0, c0 + e1, c0 + e2, c0 + e2 + e1,
+                           c0 + e4, c0 + e4 + e1, c0 + e4 + e2, c0 + e4 + e2 + e1};
+#pragma unroll
+        for (int q = 0; q < 8; q++)
+#pragma unroll
+          for (int g = 0; g < kBwdMaxG; g++)
+            if (g < gcount) atomicAdd(&acc_s[g * hw + cq[q]], v[q][g]);
+      }
+    }
+  }
+  if (!skip_neg)
   for (int i = tid; i < n; i += kBwdThreads) {
     if (skip_neg && I[i] == -1) continue;
     int ci[8];

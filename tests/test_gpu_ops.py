@@ -269,3 +269,25 @@ def test_errors_are_raised(dev):
         ops.knn_forward_cuda(x.transpose(1, 2), x, 4)
     with pytest.raises(RuntimeError, match="too large"):
         ops.spherical_avg_voxelize_forward(x, x, 300)
+
+
+def test_sph_devox_backward_irregular_corners(dev):
+    """The wave-sorted segmented path takes corner sets of the spherical
+    pattern; anything else (arbitrary corners, -1 points, corners past the
+    hot window) falls back to per-point atomics.  Both against the oracle."""
+    from pcr_amd import ops
+    rng = np.random.default_rng(7)
+    b, c, n, r = 2, 5, 3000, 16
+    xyz, _, feat = gaussian_clouds(b, n, seed=8, c=c)
+    nc = oracle.normalize_sph(xyz)
+    grid, gind, _ = oracle.spherical_avg_voxelize_forward(feat, nc, r)
+    _, inds, wgts = oracle.spherical_trilinear_devoxelize_forward(r, nc, grid, gind)
+    inds = inds.copy()
+    wgts = wgts.copy()
+    pick = rng.choice(n, 400, replace=False)
+    inds[0][:, pick[:200]] = rng.integers(0, r ** 3, size=(8, 200))       # arbitrary corners
+    inds[1][:, pick[200:300]] = rng.integers(0, r * r + 8 * r, size=(8, 100))
+    inds[1][0, pick[300:]] = -1                                         # skipped points
+    gy = rng.standard_normal((b, c, n)).astype(np.float32)
+    gx = ops.spherical_trilinear_devoxelize_backward(T(gy, dev), T(inds, dev), T(wgts, dev), r)
+    close(N(gx), oracle.devoxelize_backward(gy, inds, wgts, r, spherical=True), 1e-4)
