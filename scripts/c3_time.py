@@ -41,6 +41,8 @@ ex = SphExtractor(b, n, c, k, r, device=dev)
 t = timeit(lambda: ex.forward(xyz, nrm, feat), it=5)
 print("extractor forward                  %.3f ms/step  %.0f clouds/s" % (t, b / t * 1e3), flush=True)
 out = ex.outputs()
+t = timeit(lambda: ops.knn_local_ppf(xyz, nrm, k))
+print("knn + local ppf alone              %.3f ms" % t, flush=True)
 nc = ops.spherical_normalize(xyz)
 grid, ind, cnt = ops.spherical_avg_voxelize_forward(feat, nc, r)
 _, dinds, dwgts = ops.spherical_trilinear_devoxelize_forward(r, True, nc, grid, ind)
