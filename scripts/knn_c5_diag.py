@@ -16,8 +16,9 @@ from pcr_amd import _lib, ops  # noqa: E402
 dev = torch.device("cuda:0")
 n, k = int(os.environ.get("N", 65536)), int(os.environ.get("K", 64))
 g = torch.Generator(device=dev).manual_seed(0)
-xyz = torch.randn((1, 3, n), generator=g, device=dev)
-nrm = torch.randn((1, 3, n), generator=g, device=dev)
+B = int(os.environ.get("B", 1))
+xyz = torch.randn((B, 3, n), generator=g, device=dev)
+nrm = torch.randn((B, 3, n), generator=g, device=dev)
 lib = _lib.load()
 buf = (ctypes.c_ulonglong * (1024 * 16))()
 ops.knn_local_ppf(xyz, nrm, k)
