@@ -340,8 +340,15 @@ extern "C" pcr_status pcr_devoxelize_backward(const float* grad_y, const int* in
   int hw = skip_neg ? r * r + 8 * r + 8 : 2048;
   if (hw > r3) hw = r3;
   int G = kBwdMaxG;
+  if (!skip_neg && hw < r3 && (size_t)r3 * 4 <= 128 * 1024) {
+    // cube grids up to 32^3: cube corners land anywhere, so a 2048-voxel
+    // window sent nearly every corner to global atomics (10 ms at c3).  One
+    // channel's whole grid fits in LDS (128 KB, one workgroup per CU).
+    hw = r3;
+    G = 1;
+  }
   while (G > 1 && (size_t)G * hw * 4 > 80 * 1024) G >>= 1;
-  if ((size_t)G * hw * 4 > 80 * 1024) hw = 80 * 1024 / 4;
+  if ((size_t)G * hw * 4 > 128 * 1024) hw = 80 * 1024 / 4;
   if (hw > r3) hw = r3;
   allow_big_lds(devox_bwd_kernel, (size_t)G * hw * 4);
   hipLaunchKernelGGL(devox_bwd_kernel, dim3(ceil_div(c, G), b), dim3(kBwdThreads),
