@@ -26,7 +26,8 @@ __global__ __launch_bounds__(kNrmThreads) void normals_kernel(const float* __res
                                                               double r2,
                                                               float* __restrict__ normals,
                                                               int* __restrict__ counts) {
-  __shared__ float tile[3][kNrmTile];
+  __shared__ __align__(16) float tile[3][kNrmTile];
+  const float r2f_hi = (float)(r2 * 1.0001) * 1.0001f;
   const int b = blockIdx.y;
   const int j = blockIdx.x * kNrmThreads + threadIdx.x;
   const bool active = j < n;
@@ -52,8 +53,11 @@ __global__ __launch_bounds__(kNrmThreads) void normals_kernel(const float* __res
     }
     __syncthreads();
     if (active) {
-      for (int q = 0; q < tc; q++) {
-        const double x = tile[0][q], y = tile[1][q], z = tile[2][q];
+      // fp32 prefilter (float4 reads, four candidates per test): the fp32
+      // distance is within ~3e-7 relative of the exact one, so a candidate
+      // above r2f_hi cannot pass the fp64 test, which alone decides
+      auto take = [&](float xf, float yf, float zf) {
+        const double x = xf, y = yf, z = zf;
         const double dx = dqx - x, dy = dqy - y, dz = dqz - z;
         const double d2 = (dx * dx + dy * dy) + dz * dz;
         if (d2 < r2) {
@@ -68,7 +72,21 @@ __global__ __launch_bounds__(kNrmThreads) void normals_kernel(const float* __res
           cum[8] += z * z;
           cnt++;
         }
+      };
+      const int t4 = tc & ~3;
+      for (int q = 0; q < t4; q += 4) {
+        const float4 X = *reinterpret_cast<const float4*>(&tile[0][q]);
+        const float4 Y = *reinterpret_cast<const float4*>(&tile[1][q]);
+        const float4 Z = *reinterpret_cast<const float4*>(&tile[2][q]);
+        const float xs[4] = {X.x, X.y, X.z, X.w}, ys[4] = {Y.x, Y.y, Y.z, Y.w},
+                    zs[4] = {Z.x, Z.y, Z.z, Z.w};
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const float ex = qx - xs[u], ey = qy - ys[u], ez = qz - zs[u];
+          if (pcr_sumsq3f_nofma(ex, ey, ez) <= r2f_hi) take(xs[u], ys[u], zs[u]);
+        }
       }
+      for (int q = t4; q < tc; q++) take(tile[0][q], tile[1][q], tile[2][q]);
     }
   }
   if (!active) return;
