@@ -12,10 +12,14 @@ GPU (torch.distributed, RCCL), the batch is sharded by cloud (weak scaling:
 32 clouds per rank) and the per-cloud descriptors are all-gathered every step
 (registration matching), overlapped on a side stream.
 
-Prints ONE JSON line (rank 0).  `roofline` prices the dominant kernel (the
-voxel kernel of the step, vox_grid_kernel<3>: dense [B,C,r^3] grid + cnt, devox + descriptor) from its HIP-event-timed average duration;
+Prints ONE JSON line (rank 0).  `roofline` is step level: SURVEY 8d's
+algorithmic bytes of the whole step over ms_per_step against the 8 TB/s HBM
+peak; its `kernel` entry prices the dominant kernel (vox_stream_kernel, the
+dense [B,C,r^3] grid + cnt) from its in-step duration, HIP events on its own
+stream around each launch of the timed region's last runner call.
 `cpu_baseline` times the CPU restatement (oracle/, the "port") on a bounded
-sample of the same workload on this box's host cores.
+sample of the same workload on this box's host cores, single-thread and on
+every usable core.
 """
 import argparse
 import json
@@ -48,20 +52,13 @@ def parse():
     ap.add_argument("--kernel-iters", type=int, default=50)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--mode", choices=("native", "native2", "pipelined", "pipelined_split",
-                                       "pipelined3", "pipelined4",
-                                       "pipelined_sv", "pipelined_fs", "pipelined_3s", "pipelined_2s", "graph",
-                                       "eager"),
-                    default="native",
-                    help="native: S steps enqueued by the library (pcr_extractor_run) on three "
-                         "streams -- KNN, prep + means/devox, grid stream; native2: the same "
-                         "runner, two streams with the fused grid kernel; "
-                         "pipelined: S steps on two independent streams (KNN / voxel, fused "
-                         "grid+devox kernel) from Python with no join between them; pipelined_split: "
-                         "separate grid and devox launches; pipelined3/4/_sv: schedules with cross-stream "
-                         "events; graph: one hipGraph replay per step; eager: fork/join per step")
+    ap.add_argument("--schedule", type=int, choices=(0, 1, 2), default=1,
+                    help="pcr_extractor_run schedule (include/pcr_amd.h): 1 = three streams "
+                         "(sort+select+PPF / prep+means+devox / dense-grid stream), 2 = as 1 "
+                         "with the Morton sort on the prep stream, 0 = two streams")
     ap.add_argument("--steps-per-launch", type=int, default=40,
-                    help="pipelined steps per launch group (must divide --steps and --warmup)")
+                    help="most pipelined steps per native runner call; --steps and --warmup "
+                         "are split into calls of at most this many steps")
     return ap.parse_args()
 
 
@@ -75,13 +72,39 @@ def synthetic_inputs(b, n, c, device, seed):
     return xyz, nrm, feat
 
 
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return ""
+
+
+def usable_cores():
+    """Threads this process can really run: its CPU affinity, capped by the
+    cgroup CPU quota when one is set (a container's share of the host)."""
+    aff = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(-(-int(q) // int(p))))
+            if quota < aff:
+                return quota, "affinity %d CPUs, cgroup quota %d" % (aff, quota)
+    except (OSError, ValueError):
+        pass
+    return aff, "affinity %d CPUs" % aff
+
+
 def cpu_baseline(args):
-    """Time the CPU restatement (oracle, OpenMP across clouds) on repeated
-    batches of the same workload for ~args.cpu_seconds."""
-    import numpy as np
+    """Time the CPU restatement (oracle/pcr_oracle.c, OpenMP across clouds)
+    on repeated batches of the same workload: once on one thread and once on
+    every core this process may run on (len(os.sched_getaffinity(0))), each
+    for about args.cpu_seconds.  The all-core figure is `value`."""
     import oracle
-    threads = min(len(os.sched_getaffinity(0)), 16)
-    oracle.set_num_threads(threads)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from clouds import gaussian_clouds
     b, n, c, k, r = args.batch, args.points, args.channels, args.k, args.res
@@ -95,28 +118,26 @@ def cpu_baseline(args):
         dv, _, _ = oracle.spherical_trilinear_devoxelize_forward(r, nc, grid, ind)
         dv.max(axis=2)
 
-    one_batch()  # warm (page-in, thread pool)
-    done, t0 = 0, time.perf_counter()
-    while True:
-        one_batch()
-        done += b
-        el = time.perf_counter() - t0
-        if el >= args.cpu_seconds:
-            break
-    model = ""
-    try:
-        with open("/proc/cpuinfo") as f:
-            for line in f:
-                if line.startswith("model name"):
-                    model = line.split(":", 1)[1].strip()
-                    break
-    except OSError:
-        pass
-    del np
-    return {"value": done / el, "unit": "point-clouds/sec", "cores": threads, "kind": "port",
-            "sample": "%d clouds (%d x batch %d, N=%d, k=%d, r=%d, C=%d) in %.1f s, "
-                      "oracle/pcr_oracle.c OpenMP over clouds, %d threads, %s"
-                      % (done, done // b, b, n, k, r, c, el, threads, model)}
+    def rate(threads, seconds):
+        oracle.set_num_threads(threads)
+        one_batch()  # warm (page-in, thread pool)
+        done, t0 = 0, time.perf_counter()
+        while True:
+            one_batch()
+            done += b
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                return done / el, done, el
+
+    cores, why = usable_cores()
+    r1, d1, e1 = rate(1, args.cpu_seconds / 2)
+    rn, dn, en = rate(cores, args.cpu_seconds)
+    return {"value": rn, "unit": "point-clouds/sec", "cores": cores, "kind": "port",
+            "single_thread": {"value": r1, "cores": 1},
+            "sample": "batches of %d clouds (N=%d, k=%d, r=%d, C=%d): %d clouds in %.1f s on "
+                      "1 thread, %d clouds in %.1f s on %d threads; oracle/pcr_oracle.c, "
+                      "OpenMP over clouds, %s; %s" % (b, n, k, r, c, d1, e1, dn, en, cores,
+                                                       cpu_model(), why)}
 
 
 def main():
@@ -130,60 +151,44 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from pcr_amd.extractor import (SphExtractor, algorithmic_bytes_per_cloud,
-                                   fused_grid_kernel_bytes_per_cloud,
                                    stream_kernel_bytes_per_cloud)
     b, n, c, k, r = args.batch, args.points, args.channels, args.k, args.res
     xyz, nrm, feat = synthetic_inputs(b, n, c, dev, seed=1234 + rank)
     ex = SphExtractor(b, n, c, k, r, device=dev)
 
-    # S pipelined steps per graph launch (one launch = S batches); S must
-    # divide the step counts so exactly --steps steps are timed
-    S = max(1, args.steps_per_launch) if args.mode.startswith(("pipelined", "native")) else 1
-    if args.steps % S or (args.warmup and args.warmup % S):
-        S = 1
+    # the native runner enqueues up to S pipelined steps per call; the step
+    # counts are split into calls of at most S steps (the last call shorter)
+    S = max(1, args.steps_per_launch)
+
+    def chunks(total):
+        return [min(S, total - i) for i in range(0, total, S)]
+
     comm = torch.cuda.Stream(device=dev) if world > 1 else None
     desc_out = [torch.empty((world * S * b, c), device=dev) for _ in range(2)]
     desc_in = [torch.empty((S * b, c), device=dev) for _ in range(2)]
     pending = []
+    desc_steps = {m: torch.empty((m, b, c), device=dev) for m in set(chunks(args.steps)) |
+                  set(chunks(args.warmup))}
 
-    desc_steps = torch.empty((S, b, c), device=dev)
-    if args.mode == "graph":
-        ex.capture(xyz, nrm, feat)
-
-    def launch(i):
-        """Steps i*S .. i*S+S-1."""
-        if args.mode.startswith("native"):
-            ex.run_native(xyz, nrm, feat, S, desc_steps, schedule=0 if args.mode == "native2" else 1)
-            src = desc_steps.view(S * b, c)
-        elif args.mode.startswith("pipelined"):
-            ex.run_pipelined(xyz, nrm, feat, S, desc_steps,
-                             mode={"pipelined": "two_fused", "pipelined_split": "two",
-                                   "pipelined3": "three",
-                                   "pipelined4": "four", "pipelined_sv": "sortvox",
-                                   "pipelined_fs": "four_split", "pipelined_3s": "three_stream",
-                                   "pipelined_2s": "two_stream"}[args.mode])
-            src = desc_steps.view(S * b, c)
-        elif args.mode == "graph":
-            ex.replay()
-            src = ex.desc
-        else:
-            ex.forward(xyz, nrm, feat)
-            src = ex.desc
+    def launch(i, m, timed=False):
+        """One native runner call of m steps (call i of a sequence)."""
+        ex.run_native(xyz, nrm, feat, m, desc_steps[m], schedule=args.schedule, timed=timed)
+        src = desc_steps[m].view(m * b, c)
         if world > 1:
-            # descriptor all-gather of the S batches (registration matching),
+            # descriptor all-gather of the m batches (registration matching),
             # overlapped with the next launch on a side stream; double-buffered:
             # the gather that last read this slot is waited for before the copy
             slot = i & 1
             if len(pending) == 2:
                 pending.pop(0).wait()
-            desc_in[slot].copy_(src)
+            desc_in[slot][:m * b].copy_(src)
             comm.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(comm):
-                pending.append(dist.all_gather_into_tensor(desc_out[slot], desc_in[slot],
-                                                           async_op=True))
+                pending.append(dist.all_gather_into_tensor(
+                    desc_out[slot][:world * m * b], desc_in[slot][:m * b], async_op=True))
 
-    for i in range(args.warmup // S):
-        launch(i)
+    for i, m in enumerate(chunks(args.warmup)):
+        launch(i, m)
     for w in pending:
         w.wait()
     pending.clear()
@@ -192,8 +197,11 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for i in range(args.steps // S):
-        launch(i)
+    timed_chunks = chunks(args.steps)
+    for i, m in enumerate(timed_chunks):
+        # the last call of the timed region also brackets every step's grid
+        # kernel with timing events on its stream (in-step durations)
+        launch(i, m, timed=(i == len(timed_chunks) - 1))
     for w in pending:
         w.wait()
     pending.clear()
@@ -207,45 +215,28 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # dominant kernel, HIP events on the stream it is launched on: the grid
-    # stream kernel of the split voxel stage (native) or the fused grid /
-    # devox kernel (the other schedules)
-    split = args.mode == "native"
-    s_k = ex.s_vox
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.kernel_iters)]
-    with torch.cuda.stream(s_k):
-        for e0, e1 in ev:
-            ex.voxel_prep(xyz, s_k.cuda_stream)
-            if split:
-                ex.voxel_means_devox(feat, s_k.cuda_stream)
-                e0.record(s_k)
-                ex.voxel_stream(s_k.cuda_stream)
-            else:
-                e0.record(s_k)
-                ex.voxel_grid_devox(feat, s_k.cuda_stream)
-            e1.record(s_k)
-    torch.cuda.synchronize(dev)
-    grid_ms = sorted(e0.elapsed_time(e1) for e0, e1 in ev)
-    grid_avg_ms = sum(grid_ms) / len(grid_ms)
-    grid_bytes = (stream_kernel_bytes_per_cloud(r, c) if split
-                  else fused_grid_kernel_bytes_per_cloud(n, r, c)) * b
-    achieved = grid_bytes / (grid_avg_ms * 1e-3) / 1e9
-    kname = ("vox_stream_kernel (sph-vox dense grid + cnt from the voxel means, write-through "
-             "stores)" if split else
-             "vox_grid_kernel<3> (sph-vox dense grid + cnt, sph-devox + descriptor)")
+    # dominant kernel (the dense-grid stream kernel), in step: HIP events on
+    # the stream it is launched on (ex.s_vox) around each of its launches in
+    # the last runner call of the timed region
+    grid_ms = ex.grid_kernel_times()
+    grid_avg_ms = sum(grid_ms) / len(grid_ms) if grid_ms else float("nan")
+    grid_bytes = stream_kernel_bytes_per_cloud(r, c) * b
+    grid_gbs = grid_bytes / (grid_avg_ms * 1e-3) / 1e9
+    kname = "vox_stream_kernel (sph-vox dense grid + cnt from the voxel means)"
 
     total_clouds = b * world * args.steps
     value = total_clouds / elapsed
     step_bytes = algorithmic_bytes_per_cloud(n, k, r, c)["total"] * b
-    traffic = None
+    step_gbs = step_bytes * args.steps / elapsed / 1e9
+    traffic = step_traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc_path):
         try:
             with open(pmc_path) as f:
                 pm = json.load(f)
-            if pm.get("config") == [b, n, k, r, c] and pm.get("kernel", "") in kname:
+            if pm.get("config") == [b, n, k, r, c]:
                 traffic = pm.get("grid_kernel_hbm_bytes_per_launch")
+                step_traffic = pm.get("step_hbm_bytes")
         except (OSError, ValueError):
             traffic = None
 
@@ -266,15 +257,23 @@ def main():
                                "sph-vox r=%d^3 + sph-devox + descriptor" % (k, r),
                    "clouds_per_gpu": b, "points": n, "k": k, "resolution": r, "channels": c,
                    "global_batch": b * world, "parallelism": "dp%d (clouds sharded, "
-                   "descriptor all-gather)" % world, "launch": args.mode,
+                   "descriptor all-gather)" % world, "schedule": args.schedule,
+                   "runner_calls": [len(chunks(args.warmup)), len(timed_chunks)],
                    "steps_per_launch": S},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic,
-                     "kernel": kname,
-                     "kernel_avg_ms": round(grid_avg_ms, 5),
-                     "kernel_bytes_per_launch": grid_bytes},
-        "step_algorithmic_GBps": round(step_bytes * world * args.steps / elapsed / 1e9, 1),
+        # step level (the north-star quantity): SURVEY 8d algorithmic bytes of
+        # the whole step / ms_per_step; per rank, since every rank moves its
+        # own HBM
+        "roofline": {"bound": "hbm", "achieved": round(step_gbs, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(step_gbs / HBM_PEAK_GBS, 4),
+                     "traffic": step_traffic,
+                     "level": "step: %d B/cloud x %d clouds per rank / ms_per_step"
+                              % (step_bytes // b, b),
+                     "kernel": {"name": kname, "avg_ms_in_step": round(grid_avg_ms, 5),
+                                "launches_timed": len(grid_ms),
+                                "bytes_per_launch": grid_bytes,
+                                "achieved": round(grid_gbs, 1),
+                                "frac": round(grid_gbs / HBM_PEAK_GBS, 4),
+                                "traffic": traffic}},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args)

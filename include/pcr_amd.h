@@ -336,7 +336,19 @@ pcr_status pcr_read_xyzn_txt(const char *path, float *out, long long rows, int c
  *               KNN workspace s % 2 after the selection of step s-2 read it),
  *               so s_nbr only selects and computes the local PPF.
  * Buffers with two entries are the alternating sets (schedule 0 uses set 0).
- * desc_steps: [steps][b][c] per-step descriptors, or NULL (then desc). */
+ * desc_steps: [steps][b][c] per-step descriptors, or NULL (then desc).
+ *
+ * `runner` holds the run's cross-stream events, created once by
+ * pcr_runner_create on the current device and reused by every call (NULL:
+ * transient events for this call only).  With timed_steps > 0 the runner
+ * also brackets the grid-stream kernel (pcr_extractor_voxel_stream) of the
+ * first timed_steps steps of each run with timing events on its stream;
+ * pcr_runner_grid_times waits for them and returns the per-step durations
+ * (ms) of the last run -- the dominant kernel's in-step duration. */
+typedef struct pcr_runner pcr_runner;
+pcr_status pcr_runner_create(int timed_steps, pcr_runner **out);
+void pcr_runner_destroy(pcr_runner *runner);
+pcr_status pcr_runner_grid_times(pcr_runner *runner, float *ms, int cap, int *count);
 typedef struct pcr_extractor_args {
   int b, n, c, k, r, relative;
   const float *xyz, *normals, *features;  /* [b,3,n], [b,3,n], [b,c,n] */
@@ -353,9 +365,9 @@ typedef struct pcr_extractor_args {
   void *vox_ws[2];                        /* pcr_extractor_workspace_size(b, n, c, r) */
   size_t vox_ws_bytes;
 } pcr_extractor_args;
-pcr_status pcr_extractor_run(const pcr_extractor_args *args, int steps, int schedule,
-                             float *desc_steps, void *origin, void *s_nbr, void *s_pre,
-                             void *s_vox);
+pcr_status pcr_extractor_run(pcr_runner *runner, const pcr_extractor_args *args, int steps,
+                             int schedule, float *desc_steps, void *origin, void *s_nbr,
+                             void *s_pre, void *s_vox);
 
 /* ------------------------------------------------------ self tests ------
  * Device evaluation of the shared bit-exact math (include/pcr_math.h) for

@@ -78,6 +78,15 @@ static __device__ unsigned long long pcr_diag_stamps[1024][16];  // one copy per
   } while (0)
 #endif
 
+// Experiment knobs (launch shapes, schedule variants) are read from the
+// environment only in the diagnostic build; the product library compiles the
+// default in, so no environment variable can change what a timed run does.
+#ifdef PCR_DIAG
+#define PCR_KNOB(name, dflt) (getenv(name) ? atoi(getenv(name)) : (dflt))
+#else
+#define PCR_KNOB(name, dflt) (dflt)
+#endif
+
 // Issue priority of the latency-bound per-cloud kernels (prep, Morton sort):
 // they share CUs with the other stream's throughput kernels, whose waves
 // would otherwise take most issue slots and stretch them several-fold.

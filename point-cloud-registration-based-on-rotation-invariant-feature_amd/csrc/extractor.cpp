@@ -11,19 +11,35 @@
 namespace pcr {
 namespace {
 
-struct Events {
-  hipEvent_t e[12] = {};
-  int n = 0;
-  hipEvent_t make() {
-    hipEvent_t ev = nullptr;
-    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return nullptr;
-    e[n++] = ev;
-    return ev;
-  }
-  ~Events() {
-    for (int i = 0; i < n; i++) (void)hipEventDestroy(e[i]);  // freed once they complete
+// the runner's events: created once per runner (per SphExtractor), reused by
+// every pcr_extractor_run call.  A wait captures the event's most recent
+// record at the time it is enqueued, so re-recording across steps and calls
+// keeps the same ordering as fresh events.
+constexpr int kSyncEvents = 12;
+}  // namespace
+}  // namespace pcr
+
+struct pcr_runner {
+  int device = 0;
+  hipEvent_t sync[pcr::kSyncEvents] = {};
+  int timed_cap = 0;              // grid-kernel timing pairs (0: untimed)
+  hipEvent_t* t0 = nullptr;       // [timed_cap] before each grid launch
+  hipEvent_t* t1 = nullptr;       // [timed_cap] after it
+  int timed_last = 0;             // pairs recorded by the last run
+  ~pcr_runner() {
+    for (hipEvent_t e : sync)
+      if (e) (void)hipEventDestroy(e);
+    for (int i = 0; i < timed_cap; i++) {
+      if (t0 && t0[i]) (void)hipEventDestroy(t0[i]);
+      if (t1 && t1[i]) (void)hipEventDestroy(t1[i]);
+    }
+    delete[] t0;
+    delete[] t1;
   }
 };
+
+namespace pcr {
+namespace {
 
 #define PCR_TRY(call)                  \
   do {                                 \
@@ -39,21 +55,9 @@ struct Events {
     }                                                                            \
   } while (0)
 
-// diagnostic only (never set in the product): PCR_RUN_SKIP bit mask of
-// launches the runner leaves out -- 1 local PPF, 2 grid stream, 4 prep +
-// means, 8 sort + selection -- to see which chain bounds the step
-static int skip_mask() {
-  static const int m = getenv("PCR_RUN_SKIP") ? atoi(getenv("PCR_RUN_SKIP")) : 0;
-  return m;
-}
-
 // Morton sort of the cloud into KNN workspace q; false when the sorted path
 // does not apply (nothing launched; the selection then runs unsorted)
 pcr_status knn_sort(const pcr_extractor_args* a, int q, hipStream_t st, bool* sorted) {
-  if (skip_mask() & 8) {
-    *sorted = true;
-    return PCR_OK;
-  }
   const pcr_status rc = pcr_knn_prepare(a->xyz, a->b, a->n, a->knn_ws[q], a->knn_ws_bytes, st);
   *sorted = rc == PCR_OK;
   return rc == PCR_ERR_UNSUPPORTED ? PCR_OK : rc;
@@ -64,11 +68,9 @@ pcr_status knn_select_ppf(const pcr_extractor_args* a, int q, bool sorted, hipSt
   if (!sorted)  // no sorted path: the one-call selection + PPF
     return pcr_knn_local_ppf(a->xyz, a->normals, a->b, a->n, a->k, a->relative, a->knn_idx,
                              a->knn_dist, a->local_ppf, a->knn_ws[q], a->knn_ws_bytes, st);
-  if (!(skip_mask() & 8))
-    PCR_TRY(pcr_knn_local_ppf_prepared(a->xyz, a->normals, a->b, a->n, a->k, a->relative,
+  PCR_TRY(pcr_knn_local_ppf_prepared(a->xyz, a->normals, a->b, a->n, a->k, a->relative,
                                        a->knn_idx, a->knn_dist, nullptr, a->knn_ws[q],
                                        a->knn_ws_bytes, st));
-  if (skip_mask() & 1) return PCR_OK;
   return pcr_local_ppf_forward(a->xyz, a->normals, a->xyz, a->normals, a->knn_idx, a->b, a->n,
                                a->n, a->k, 1, a->relative, a->local_ppf, st);
 }
@@ -78,9 +80,51 @@ pcr_status knn_select_ppf(const pcr_extractor_args* a, int q, bool sorted, hipSt
 
 using namespace pcr;
 
-extern "C" pcr_status pcr_extractor_run(const pcr_extractor_args* a, int steps, int schedule,
-                                        float* desc_steps, void* origin, void* s_nbr_p,
-                                        void* s_pre_p, void* s_vox_p) {
+extern "C" pcr_status pcr_runner_create(int timed_steps, pcr_runner** out) {
+  PCR_REQUIRE(out != nullptr && timed_steps >= 0 && timed_steps <= (1 << 16),
+              "runner_create: invalid arguments");
+  *out = nullptr;
+  pcr_runner* rn = new pcr_runner();
+  if (hipGetDevice(&rn->device) != hipSuccess) {
+    delete rn;
+    set_error("runner_create: no HIP device");
+    return PCR_ERR_LAUNCH;
+  }
+  bool ok = true;
+  for (int i = 0; i < kSyncEvents; i++)
+    ok = ok && hipEventCreateWithFlags(&rn->sync[i], hipEventDisableTiming) == hipSuccess;
+  if (ok && timed_steps > 0) {
+    rn->t0 = new hipEvent_t[timed_steps]();
+    rn->t1 = new hipEvent_t[timed_steps]();
+    rn->timed_cap = timed_steps;
+    for (int i = 0; i < timed_steps && ok; i++)
+      ok = hipEventCreate(&rn->t0[i]) == hipSuccess && hipEventCreate(&rn->t1[i]) == hipSuccess;
+  }
+  if (!ok) {
+    delete rn;
+    set_error("runner_create: event creation failed");
+    return PCR_ERR_LAUNCH;
+  }
+  *out = rn;
+  return PCR_OK;
+}
+
+extern "C" void pcr_runner_destroy(pcr_runner* rn) { delete rn; }
+
+extern "C" pcr_status pcr_runner_grid_times(pcr_runner* rn, float* ms, int cap, int* count) {
+  PCR_REQUIRE(rn != nullptr && ms != nullptr && count != nullptr, "runner_grid_times: NULL");
+  const int m = rn->timed_last < cap ? rn->timed_last : cap;
+  for (int i = 0; i < m; i++) {
+    PCR_HIP(hipEventSynchronize(rn->t1[i]), "timing sync");
+    PCR_HIP(hipEventElapsedTime(&ms[i], rn->t0[i], rn->t1[i]), "elapsed");
+  }
+  *count = m;
+  return PCR_OK;
+}
+
+extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_args* a,
+                                        int steps, int schedule, float* desc_steps, void* origin,
+                                        void* s_nbr_p, void* s_pre_p, void* s_vox_p) {
   PCR_REQUIRE(a != nullptr && steps >= 0 && schedule >= 0 && schedule <= 2,
               "extractor_run: invalid arguments");
   PCR_REQUIRE(a->b >= 0 && a->n >= 1 && a->c >= 1 && a->k >= 1 && a->r >= 1,
@@ -92,11 +136,23 @@ extern "C" pcr_status pcr_extractor_run(const pcr_extractor_args* a, int steps, 
   for (int q = 0; q < nslots; q++)
     PCR_REQUIRE(a->vox_ws[q] && a->dinds[q] && a->dwgts[q] && a->knn_ws[schedule == 2 ? q : 0],
                 "extractor_run: buffer set %d missing", q);
-  Events ev;
-  hipEvent_t fork = ev.make(), means_done[2] = {ev.make(), ev.make()},
-             stream_done[2] = {ev.make(), ev.make()}, join[3] = {ev.make(), ev.make(), ev.make()},
-             sort_done[2] = {ev.make(), ev.make()}, sel_done[2] = {ev.make(), ev.make()};
-  PCR_REQUIRE(ev.n == 12 && sel_done[1] != nullptr, "extractor_run: event creation failed");
+  // no runner: a transient one (events created and destroyed in this call;
+  // hipEventDestroy of a pending event is deferred until it completes)
+  pcr_runner* tmp = nullptr;
+  if (runner == nullptr) {
+    PCR_TRY(pcr_runner_create(0, &tmp));
+    runner = tmp;
+  }
+  struct Owned {
+    pcr_runner* p;
+    ~Owned() { delete p; }
+  } owned{tmp};
+  pcr_runner* const rn = runner;
+  rn->timed_last = schedule == 0 ? 0 : steps < rn->timed_cap ? steps : rn->timed_cap;
+  hipEvent_t* e = rn->sync;
+  hipEvent_t fork = e[0], means_done[2] = {e[1], e[2]}, stream_done[2] = {e[3], e[4]},
+             join[3] = {e[5], e[6], e[7]}, sort_done[2] = {e[8], e[9]},
+             sel_done[2] = {e[10], e[11]};
   PCR_HIP(hipEventRecord(fork, org), "fork record");
   for (hipStream_t st : {sn, sp, sv}) PCR_HIP(hipStreamWaitEvent(st, fork, 0), "fork wait");
   const size_t dstride = (size_t)a->b * a->c;
@@ -119,19 +175,19 @@ extern "C" pcr_status pcr_extractor_run(const pcr_extractor_args* a, int steps, 
       PCR_HIP(hipEventRecord(sort_done[q], sp), "sort record");
     }
     if (s >= 2) PCR_HIP(hipStreamWaitEvent(sp, stream_done[q], 0), "slot wait");
-    if (!(skip_mask() & 4))
-      PCR_TRY(pcr_extractor_voxel_prep(a->xyz, a->b, a->n, a->r, a->norm_coords, a->ind,
+    PCR_TRY(pcr_extractor_voxel_prep(a->xyz, a->b, a->n, a->r, a->norm_coords, a->ind,
                                        a->dinds[q], a->dwgts[q], a->vox_ws[q], a->vox_ws_bytes,
                                        sp));
-    if (!(skip_mask() & 4))
-      PCR_TRY(pcr_extractor_voxel_means_devox(a->features, a->b, a->c, a->n, a->r, a->devox,
+    PCR_TRY(pcr_extractor_voxel_means_devox(a->features, a->b, a->c, a->n, a->r, a->devox,
                                             a->dinds[q], a->dwgts[q], desc, a->vox_ws[q],
                                             a->vox_ws_bytes, sp));
     PCR_HIP(hipEventRecord(means_done[q], sp), "means record");
     PCR_HIP(hipStreamWaitEvent(sv, means_done[q], 0), "means wait");
-    if (!(skip_mask() & 2))
-      PCR_TRY(pcr_extractor_voxel_stream(a->b, a->c, a->n, a->r, a->cnt, a->grid, a->vox_ws[q],
-                                         a->vox_ws_bytes, sv));
+    const bool timed = s < rn->timed_cap;
+    if (timed) PCR_HIP(hipEventRecord(rn->t0[s], sv), "timing record");
+    PCR_TRY(pcr_extractor_voxel_stream(a->b, a->c, a->n, a->r, a->cnt, a->grid, a->vox_ws[q],
+                                       a->vox_ws_bytes, sv));
+    if (timed) PCR_HIP(hipEventRecord(rn->t1[s], sv), "timing record");
     PCR_HIP(hipEventRecord(stream_done[q], sv), "stream record");
     if (schedule == 2) {
       PCR_HIP(hipStreamWaitEvent(sn, sort_done[q], 0), "sort wait");

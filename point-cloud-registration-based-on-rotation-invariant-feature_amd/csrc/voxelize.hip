@@ -1084,7 +1084,7 @@ __global__ __launch_bounds__((NS + 1) * 64) void vox_stream_kernel(int c, int n,
 // workgroups of a grid launch: every item its own workgroup unless
 // PCR_GRID_WGS caps the count (then each loops over several items)
 static int grid_wgs(int nitems) {
-  static const int cap = getenv("PCR_GRID_WGS") ? atoi(getenv("PCR_GRID_WGS")) : 0;
+  static const int cap = PCR_KNOB("PCR_GRID_WGS", 0);
   return cap > 0 && cap < nitems ? cap : nitems;
 }
 
@@ -1499,7 +1499,7 @@ static size_t grid_smem_bytes(int G, int n, int nw) {
 
 // issue priority of the prep kernel (PCR_PREP_PRIO=0 turns the boost off)
 static int prep_prio() {
-  static const int p = getenv("PCR_PREP_PRIO") ? atoi(getenv("PCR_PREP_PRIO")) : 1;
+  static const int p = PCR_KNOB("PCR_PREP_PRIO", 1);
   return p;
 }
 
@@ -1533,7 +1533,7 @@ static pcr_status run_voxelize(const float* features, const float* coords_f, con
     const int npad = next_pow2(n < nt ? nt : n);
     size_t prep_smem = (size_t)npad * 8 + (size_t)ws.W * 8 + (size_t)n * 8;
     PCR_REQUIRE(prep_smem <= 150 * 1024, "%s: prep LDS %zu too large", name, prep_smem);
-    static const int exp_nt = getenv("PCR_PREP_NT") ? atoi(getenv("PCR_PREP_NT")) : 256;
+    static const int exp_nt = PCR_KNOB("PCR_PREP_NT", 256);
     if (small && exp_nt == 512 && n > 256) {
       const int npad5 = next_pow2(n < 512 ? 512 : n);
       const size_t sm5 = (size_t)npad5 * 8 + (size_t)ws.W * 8 + (size_t)n * 8;
@@ -1696,8 +1696,8 @@ extern "C" pcr_status pcr_extractor_voxel_means_devox(const float* features, int
   const int r3 = r * r * r;
   const int tile = ((r3 + 31) / 32) * 32;
   const int nw = tile / 32 + 1;
-  static const int mv = getenv("PCR_MEANS_V") ? atoi(getenv("PCR_MEANS_V")) : 3;
-  static const int mg = getenv("PCR_MEANS_G") ? atoi(getenv("PCR_MEANS_G")) : 2;
+  static const int mv = PCR_KNOB("PCR_MEANS_V", 3);
+  static const int mg = PCR_KNOB("PCR_MEANS_G", 2);
   if (mv == 3 && n <= kMeansMaxN) {
     // G channels per workgroup (G = 2: ~24 KB of LDS, so it fits beside the
     // KNN selection's workgroups); every workgroup of a cloud reads the
@@ -1763,19 +1763,19 @@ extern "C" pcr_status pcr_extractor_voxel_stream(int b, int c, int n, int r, int
   const int ngrp = ceil_div(c, kStreamG);
   // a few workgroups per cloud (about one per CU in all), each a contiguous
   // range of channel-pair items of that cloud
-  static const int cap = getenv("PCR_STREAM_WGS") ? atoi(getenv("PCR_STREAM_WGS")) : 0;
+  static const int cap = PCR_KNOB("PCR_STREAM_WGS", 0);
   const int total = cap > 0 ? cap : device_cus();
   int wpc = total / (b > 0 ? b : 1);
   if (wpc < 1) wpc = 1;
   if (wpc > ngrp) wpc = ngrp;
   const int per = ceil_div(ngrp, wpc);
-  static const int dbg = getenv("PCR_STREAM_DBG") ? atoi(getenv("PCR_STREAM_DBG")) : 0;
-  static const int nb = getenv("PCR_STREAM_NB") ? atoi(getenv("PCR_STREAM_NB")) : kStreamNB;
+  static const int dbg = PCR_KNOB("PCR_STREAM_DBG", 0);
+  static const int nb = PCR_KNOB("PCR_STREAM_NB", kStreamNB);
   PCR_REQUIRE(ws.W % 64 == 0, "%s: r^3 %% 2048 != 0 unsupported", name);
-  static const int uu = getenv("PCR_STREAM_U") ? atoi(getenv("PCR_STREAM_U")) : 2;
+  static const int uu = PCR_KNOB("PCR_STREAM_U", 2);
   const size_t smem = (size_t)nb * kStreamNG * 1024 + (size_t)ws.W * 6 +
                       ((size_t)ws.ms * 2 + 255) / 256 * 256;
-  static const int aux = getenv("PCR_STREAM_AUX") ? atoi(getenv("PCR_STREAM_AUX")) : 16;
+  static const int aux = PCR_KNOB("PCR_STREAM_AUX", 16);
 #define PCR_LAUNCH_STREAM(NSV, NBV, UV, AV)                                                    \
   do {                                                                                        \
     allow_big_lds(vox_stream_kernel<NSV, NBV, UV, AV>, smem);                                 \

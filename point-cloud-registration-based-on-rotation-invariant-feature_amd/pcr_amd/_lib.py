@@ -51,7 +51,10 @@ SIGNATURES = {
     "pcr_extractor_voxel_grid_devox": (ST, [P, I, I, I, I, P, P, P, P, P, P, P, SZ, P]),
     "pcr_extractor_voxel_means_devox": (ST, [P, I, I, I, I, P, P, P, P, P, SZ, P]),
     "pcr_extractor_voxel_stream": (ST, [I, I, I, I, P, P, P, SZ, P]),
-    "pcr_extractor_run": (ST, [P, I, I, P, P, P, P, P]),
+    "pcr_runner_create": (ST, [I, ctypes.POINTER(P)]),
+    "pcr_runner_destroy": (None, [P]),
+    "pcr_runner_grid_times": (ST, [P, P, I, ctypes.POINTER(I)]),
+    "pcr_extractor_run": (ST, [P, P, I, I, P, P, P, P, P]),
     "pcr_mutual_nn_workspace_size": (SZ, [I, I, I]),
     "pcr_mutual_nn_match": (ST, [P, P, I, I, I, I, P, P, P, P, P, P, SZ, P]),
     "pcr_lrf_change_coords": (ST, [P, I, I, P, P, P, P, P]),

@@ -16,9 +16,11 @@ features [B,C,N], all resident on the GPU):
       the grid kernel
 
 The streams are forked from and joined back to the caller's stream.
-``capture()`` records one step into a hipGraph; ``run_pipelined()`` enqueues
+``forward()`` enqueues one step from Python; ``capture()`` records one step
+into a hipGraph; ``run_native()`` has the library (pcr_extractor_run) enqueue
 S consecutive steps with no join between them on alternating buffer sets, so
-step i+1's front stage overlaps step i's back stages.
+step i+1's front stages overlap step i's back stages -- the product schedule
+bench.py measures.
 """
 import ctypes
 
@@ -60,6 +62,7 @@ class SphExtractor:
         self.s_vox = torch.cuda.Stream(device=dev)
         self.s_dev = torch.cuda.Stream(device=dev)
         self.graph = None
+        self._runner, self._runner_cap = None, 0
         self._static_in = None
         self._set1 = None
 
@@ -242,13 +245,53 @@ class SphExtractor:
             "dinds": dinds, "dwgts": dwgts, "desc": self.desc,
         }
 
-    def run_native(self, xyz, normals, features, steps, desc_steps=None, schedule=1):
+    def _get_runner(self, timed_steps):
+        """The library runner (its cross-stream events are created once and
+        reused by every run); re-made only to grow its timing capacity."""
+        if self._runner is not None and self._runner_cap >= timed_steps:
+            return self._runner
+        self._free_runner()
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            _lib.check(_lib.load().pcr_runner_create(int(timed_steps), ctypes.byref(h)),
+                       "runner_create")
+        self._runner, self._runner_cap = h, int(timed_steps)
+        return h
+
+    def _free_runner(self):
+        if getattr(self, "_runner", None) is not None:
+            torch.cuda.synchronize(self.device)
+            _lib.load().pcr_runner_destroy(self._runner)
+        self._runner, self._runner_cap = None, 0
+
+    def __del__(self):
+        try:
+            self._free_runner()
+        except Exception:  # interpreter shutdown
+            pass
+
+    def grid_kernel_times(self):
+        """Per-step durations (ms) of the grid-stream kernel in the last
+        run_native(..., timed=True) call, from HIP events on its stream."""
+        if self._runner is None or self._runner_cap == 0:
+            return []
+        ms = (ctypes.c_float * self._runner_cap)()
+        cnt = ctypes.c_int(0)
+        _lib.check(_lib.load().pcr_runner_grid_times(self._runner, ms, self._runner_cap,
+                                                     ctypes.byref(cnt)), "runner_grid_times")
+        return list(ms[:cnt.value])
+
+    def run_native(self, xyz, normals, features, steps, desc_steps=None, schedule=1,
+                   timed=False):
         """`steps` pipelined steps enqueued by the library's native runner
         (pcr_extractor_run): schedule 1 = three streams (prep + means / devox
         on s_pre, the grid stream on s_vox, sort + select + PPF on s_nbr,
-        voxel buffer sets alternating), 0 = two streams with the fused grid
-        kernel.  One ctypes call for all steps."""
+        voxel buffer sets alternating), 2 = as 1 with the Morton sort on
+        s_pre, 0 = two streams with the fused grid kernel.  One ctypes call
+        for all steps.  timed: bracket each step's grid-stream kernel with
+        timing events (read back with grid_kernel_times())."""
         self._check_inputs(xyz, normals, features)
+        runner = self._get_runner(steps if timed else 0)
         s1 = self._set(1)
         a = _lib.ExtractorArgs()
         a.b, a.n, a.c, a.k, a.r, a.relative = self.b, self.n, self.c, self.k, self.r, \
@@ -269,284 +312,11 @@ class SphExtractor:
             raise RuntimeError("desc_steps must be [steps, B, C]")
         cur = torch.cuda.current_stream(self.device)
         _lib.check(_lib.load().pcr_extractor_run(
-            ctypes.byref(a), steps, schedule, _ptr(desc_steps), cur.cuda_stream,
+            runner, ctypes.byref(a), steps, schedule, _ptr(desc_steps), cur.cuda_stream,
             self.s_nbr.cuda_stream, self.s_pre.cuda_stream, self.s_vox.cuda_stream),
             "extractor_run")
         last = (steps - 1) & 1 if schedule >= 1 else 0
         return self.outputs(slot=last)
-
-    def run_pipelined(self, xyz, normals, features, steps, desc_steps=None, mode="two_fused"):
-        """Enqueue `steps` consecutive steps with no join between them, forked
-        from and joined back to the current stream once.  Step s writes its
-        descriptor to desc_steps[s] when given.
-
-        mode "two_fused" (default, fastest measured): two independent streams
-        joined once at the end -- s_nbr runs sort + select + PPF of every
-        step, s_vox prep + the fused grid / devox / descriptor kernel.
-        mode "two": the same with separate grid and devox launches ("two_dg":
-        devox before grid).
-        mode "three": s_nbr runs sort + select of every step, s_vox
-        prep + grid, s_dev devox after its step's prep, on alternating buffer
-        sets (prep waits only for the devox two steps back).
-        mode "four": the four-stream schedule of enqueue() on alternating
-        buffer sets (front stages of step i+1 overlap step i's back stages).
-        Eager launches (ROCm's stream capture rejects the cross-step edges)."""
-        self._check_inputs(xyz, normals, features)
-        cur = self._fork()
-        if mode == "three":
-            sn, sv, sd = self.s_nbr.cuda_stream, self.s_vox.cuda_stream, self.s_dev.cuda_stream
-            dev_done = [None, None]
-            for s in range(steps):
-                slot = s & 1
-                d = None if desc_steps is None else desc_steps[s]
-                ok = self.knn_sort(xyz, sn)
-                self.knn_select(xyz, normals, sn, 0, ok)
-                if dev_done[slot] is not None:  # step s-2's devox read this set
-                    self.s_vox.wait_event(dev_done[slot])
-                self.voxel_prep(xyz, sv, slot)
-                e_prep = torch.cuda.Event()
-                e_prep.record(self.s_vox)
-                self.voxel_grid(features, sv, slot)
-                self.s_dev.wait_event(e_prep)
-                self.voxel_devox(features, sd, d, slot)
-                dev_done[slot] = torch.cuda.Event()
-                dev_done[slot].record(self.s_dev)
-            self._join(cur)
-            return self.outputs(slot=(steps - 1) & 1)
-        if mode == "sortvox":
-            # the Morton sort moves to the voxel stream, ahead of prep: s_nbr
-            # only selects (+ PPF); sorted / voxel buffers alternate per step
-            sn, sv, sd = self.s_nbr.cuda_stream, self.s_vox.cuda_stream, self.s_dev.cuda_stream
-            sel_done, dev_done = [None, None], [None, None]
-            for s in range(steps):
-                slot = s & 1
-                d = None if desc_steps is None else desc_steps[s]
-                for ev in (sel_done[slot], dev_done[slot]):  # step s-2's readers
-                    if ev is not None:
-                        self.s_vox.wait_event(ev)
-                ok = self.knn_sort(xyz, sv, slot)
-                e_sort = torch.cuda.Event()
-                e_sort.record(self.s_vox)
-                self.voxel_prep(xyz, sv, slot)
-                e_prep = torch.cuda.Event()
-                e_prep.record(self.s_vox)
-                self.voxel_grid(features, sv, slot)
-                self.s_nbr.wait_event(e_sort)
-                self.knn_select(xyz, normals, sn, slot, ok)
-                sel_done[slot] = torch.cuda.Event()
-                sel_done[slot].record(self.s_nbr)
-                self.s_dev.wait_event(e_prep)
-                self.voxel_devox(features, sd, d, slot)
-                dev_done[slot] = torch.cuda.Event()
-                dev_done[slot].record(self.s_dev)
-            self._join(cur)
-            return self.outputs(slot=(steps - 1) & 1)
-        if mode == "two_sv":
-            # as two_fused, with the Morton sort on the voxel stream ahead of
-            # prep (KNN workspace alternates; two events per step)
-            sn, sv = self.s_nbr.cuda_stream, self.s_vox.cuda_stream
-            sel_done = [None, None]
-            for s in range(steps):
-                slot = s & 1
-                d = None if desc_steps is None else desc_steps[s]
-                if sel_done[slot] is not None:
-                    self.s_vox.wait_event(sel_done[slot])
-                ok = self.knn_sort(xyz, sv, slot)
-                e_sort = torch.cuda.Event()
-                e_sort.record(self.s_vox)
-                self.voxel_stage(xyz, features, sv, d)
-                self.s_nbr.wait_event(e_sort)
-                self.knn_select(xyz, normals, sn, slot, ok)
-                sel_done[slot] = torch.cuda.Event()
-                sel_done[slot].record(self.s_nbr)
-            self._join(cur)
-            return self.outputs()
-        if mode == "two_stream":
-            # s_nbr: sort + select + PPF; s_vox: prep, means / devox /
-            # descriptor, then the small persistent grid-streaming kernel
-            # (it leaves room on every CU for the selection beside it)
-            sn, sv = self.s_nbr.cuda_stream, self.s_vox.cuda_stream
-            for s in range(steps):
-                d = None if desc_steps is None else desc_steps[s]
-                ok = self.knn_sort(xyz, sn)
-                self.knn_select(xyz, normals, sn, 0, ok)
-                self.voxel_prep(xyz, sv)
-                self.voxel_means_devox(features, sv, d)
-                self.voxel_stream(sv)
-            self._join(cur)
-            return self.outputs()
-        if mode == "four_stream":
-            # s_dev: Morton sort of step s+1 (KNN set (s+1) % 2, after the
-            # selection of step s-1 read it); s_nbr: selection + PPF of step s;
-            # s_pre: prep + means / devox / descriptor (voxel set s % 2);
-            # s_vox: the grid stream of step s
-            sa, sn = self.s_dev, self.s_nbr
-            stream_done, sel_done, e_sort, ok = [None, None], [None, None], [None, None], [None, None]
-
-            def rec(st):
-                e_ = torch.cuda.Event()
-                e_.record(st)
-                return e_
-
-            def sort(s):
-                sl = s & 1
-                if sel_done[sl] is not None:
-                    sa.wait_event(sel_done[sl])
-                ok[sl] = self.knn_sort(xyz, sa.cuda_stream, sl)
-                e_sort[sl] = rec(sa)
-
-            sort(0)
-            for s in range(steps):
-                slot = s & 1
-                d = None if desc_steps is None else desc_steps[s]
-                if s + 1 < steps:
-                    sort(s + 1)
-                if stream_done[slot] is not None:
-                    self.s_pre.wait_event(stream_done[slot])
-                self.voxel_prep(xyz, self.s_pre.cuda_stream, slot)
-                self.voxel_means_devox(features, self.s_pre.cuda_stream, d, slot)
-                self.s_vox.wait_event(rec(self.s_pre))
-                self.voxel_stream(self.s_vox.cuda_stream, slot)
-                stream_done[slot] = rec(self.s_vox)
-                sn.wait_event(e_sort[slot])
-                self.knn_select(xyz, normals, sn.cuda_stream, slot, ok[slot])
-                sel_done[slot] = rec(sn)
-            self._join(cur)
-            last = (steps - 1) & 1
-            return self.outputs(slot=last, idx_slot=last)
-        if mode == "three_stream":
-            # s_nbr: sort + select + PPF; s_pre: prep + means / devox /
-            # descriptor of step s into workspace set s % 2 (after the grid
-            # stream of step s-2 read it); s_vox: the grid stream of step s
-            sn = self.s_nbr.cuda_stream
-            stream_done = [None, None]
-            for s in range(steps):
-                slot = s & 1
-                d = None if desc_steps is None else desc_steps[s]
-                if stream_done[slot] is not None:
-                    self.s_pre.wait_event(stream_done[slot])
-                self.voxel_prep(xyz, self.s_pre.cuda_stream, slot)
-                self.voxel_means_devox(features, self.s_pre.cuda_stream, d, slot)
-                e_m = torch.cuda.Event()
-                e_m.record(self.s_pre)
-                self.s_vox.wait_event(e_m)
-                self.voxel_stream(self.s_vox.cuda_stream, slot)
-                stream_done[slot] = torch.cuda.Event()
-                stream_done[slot].record(self.s_vox)
-                ok = self.knn_sort(xyz, sn)
-                self.knn_select(xyz, normals, sn, 0, ok)
-            self._join(cur)
-            return self.outputs(slot=(steps - 1) & 1)
-        if mode == "three_split":
-            # s_nbr: sort + select + PPF of every step; s_pre: voxel prep of
-            # step s into set s % 2 (after step s-2's grid kernel read it);
-            # s_vox: fused grid / devox / descriptor kernel after its prep
-            sn = self.s_nbr.cuda_stream
-            grid_done = [None, None]
-            for s in range(steps):
-                slot = s & 1
-                d = None if desc_steps is None else desc_steps[s]
-                if grid_done[slot] is not None:
-                    self.s_pre.wait_event(grid_done[slot])
-                self.voxel_prep(xyz, self.s_pre.cuda_stream, slot)
-                e_prep = torch.cuda.Event()
-                e_prep.record(self.s_pre)
-                self.s_vox.wait_event(e_prep)
-                self.voxel_grid_devox(features, self.s_vox.cuda_stream, d, slot)
-                grid_done[slot] = torch.cuda.Event()
-                grid_done[slot].record(self.s_vox)
-                ok = self.knn_sort(xyz, sn)
-                self.knn_select(xyz, normals, sn, 0, ok)
-            self._join(cur)
-            return self.outputs(slot=(steps - 1) & 1)
-        if mode == "four_split":
-            # s_pre: Morton sort of step s+1, then local PPF of step s (after
-            # its selection); s_nbr: selections back to back; s_dev: voxel
-            # prep; s_vox: fused grid / devox / descriptor kernel.  KNN
-            # workspace, KNN indices and voxel workspace / corners alternate
-            # between two sets; a set is rewritten only after step s-2's
-            # readers of it are done.
-            sa, sb = self.s_pre, self.s_nbr
-            sc, sd = self.s_dev, self.s_vox
-            lib = _lib.load()
-            ok = [None, None]
-            e_sort = [None, None]
-            ppf_done, sel_done, grid_done = [None, None], [None, None], [None, None]
-
-            def ev(st):
-                e_ = torch.cuda.Event()
-                e_.record(st)
-                return e_
-
-            def sort(s):
-                slot = s & 1
-                if sel_done[slot] is not None:
-                    sa.wait_event(sel_done[slot])
-                ok[slot] = self.knn_sort(xyz, sa.cuda_stream, slot)
-                e_sort[slot] = ev(sa)
-
-            sort(0)
-            for s in range(steps):
-                slot = s & 1
-                d = None if desc_steps is None else desc_steps[s]
-                # voxel side
-                if grid_done[slot] is not None:
-                    sc.wait_event(grid_done[slot])
-                self.voxel_prep(xyz, sc.cuda_stream, slot)
-                sd.wait_event(ev(sc))
-                self.voxel_grid_devox(features, sd.cuda_stream, d, slot)
-                grid_done[slot] = ev(sd)
-                # neighbour side
-                sb.wait_event(e_sort[slot])
-                if ppf_done[slot] is not None:
-                    sb.wait_event(ppf_done[slot])
-                self.knn_select(xyz, normals, sb.cuda_stream, slot, ok[slot], ppf=False)
-                sel_done[slot] = ev(sb)
-                if s + 1 < steps:
-                    sort(s + 1)
-                sa.wait_event(sel_done[slot])
-                idx = self._set(slot)[4]
-                _lib.check(lib.pcr_local_ppf_forward(
-                    _ptr(xyz), _ptr(normals), _ptr(xyz), _ptr(normals), _ptr(idx), self.b,
-                    self.n, self.n, self.k, 1, int(self.relative), _ptr(self.local_ppf),
-                    sa.cuda_stream), "local_ppf_forward")
-                ppf_done[slot] = ev(sa)
-            self._join(cur)
-            last = (steps - 1) & 1
-            return self.outputs(slot=last, idx_slot=last)
-        if mode == "two_fused":
-            # voxel stream: prep, then one kernel for grid + devox + descriptor
-            sn, sv = self.s_nbr.cuda_stream, self.s_vox.cuda_stream
-            for s in range(steps):
-                d = None if desc_steps is None else desc_steps[s]
-                ok = self.knn_sort(xyz, sn)
-                self.knn_select(xyz, normals, sn, 0, ok)
-                self.voxel_stage(xyz, features, sv, d)
-            self._join(cur)
-            return self.outputs()
-        if mode in ("two", "two_dg"):
-            sn, sv = self.s_nbr.cuda_stream, self.s_vox.cuda_stream
-            for s in range(steps):
-                d = None if desc_steps is None else desc_steps[s]
-                ok = self.knn_sort(xyz, sn)
-                self.knn_select(xyz, normals, sn, 0, ok)
-                self.voxel_prep(xyz, sv)
-                if mode == "two":
-                    self.voxel_grid(features, sv)
-                    self.voxel_devox(features, sv, d)
-                else:
-                    self.voxel_devox(features, sv, d)
-                    self.voxel_grid(features, sv)
-            self._join(cur)
-            return self.outputs()
-        pending = [None, None]
-        for s in range(steps):
-            slot = s & 1
-            d = None if desc_steps is None else desc_steps[s]
-            pending[slot] = self.enqueue(xyz, normals, features, desc=d, slot=slot,
-                                         reuse=pending[slot], events=True)
-        self._join(cur)
-        return self.outputs(slot=(steps - 1) & 1)
 
     def capture(self, xyz, normals, features):
         """Capture one step over these input tensors into a hipGraph."""

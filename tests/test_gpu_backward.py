@@ -1,0 +1,143 @@
+"""GPU parity of the backward passes at the resolutions and shapes the models
+run (BASELINE c3: 2048 points, r = 32, C = 64), one test per kernel branch.
+
+Cube trilinear devoxelize backward (trilinear_devox.cu:120-163) has three
+launch shapes in pcr_devoxelize_backward (csrc/devoxelize.hip):
+  * r^3 <= 2048 (r = 8):  the grid window covers r^3, several channels per
+    workgroup (golden fixture, tests/test_gpu_ops.py);
+  * 2048 < r^3 <= 32768 (r = 16, 32): one channel's whole grid in LDS, one
+    channel per workgroup ("lds_whole_grid");
+  * r^3 > 32768 (r = 64): a 20k-voxel LDS window plus global atomics for the
+    corners past it ("window_atomics").
+Scatter results are compared against the oracle with the fp32 sum-order
+bound of tests/sumorder.py; the gather backward (avg voxelize) is bit-exact.
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from clouds import gaussian_clouds
+from sumorder import assert_within_sum_order, devox_backward_bound
+
+pytestmark = pytest.mark.gpu
+
+
+def T(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def N(t):
+    return t.detach().cpu().numpy()
+
+
+def cube_coords(b, n, r, seed):
+    """Continuous voxel coords in [0, r-1] as Voxelization produces them
+    (voxelization.py:18-31), with exact lattice points, the r-1 face and the
+    0 face among them."""
+    rng = np.random.default_rng(seed)
+    cc = rng.uniform(0, r - 1, (b, 3, n)).astype(np.float32)
+    cc[:, :, :16] = rng.integers(0, r, (b, 3, 16)).astype(np.float32)
+    cc[:, 0, 16:24] = r - 1
+    cc[:, 1, 24:32] = 0.0
+    return np.ascontiguousarray(cc)
+
+
+@pytest.mark.parametrize("r,branch", [(16, "lds_whole_grid"), (32, "lds_whole_grid"),
+                                      (64, "window_atomics")])
+def test_cube_devox_backward_branches(dev, r, branch):
+    from pcr_amd import ops
+    b, n = 2, 2048
+    c = 67 if r < 64 else 21  # not a multiple of any channel group
+    cc = cube_coords(b, n, r, seed=r)
+    rng = np.random.default_rng(100 + r)
+    grid = rng.standard_normal((b, c, r ** 3)).astype(np.float32)
+    outs, inds, wgts = ops.trilinear_devoxelize_forward(r, True, T(cc, dev), T(grid, dev))
+    eo, ei, ew = oracle.trilinear_devoxelize_forward(r, cc, grid)
+    assert np.array_equal(N(inds), ei)
+    assert np.array_equal(N(wgts), ew)
+    assert np.abs(N(outs) - eo).max() <= 1e-5
+    gy = rng.standard_normal((b, c, n)).astype(np.float32)
+    gx = ops.trilinear_devoxelize_backward(T(gy, dev), inds, wgts, r)
+    exp = oracle.devoxelize_backward(gy, ei, ew, r, spherical=False)
+    assert_within_sum_order(N(gx), exp, devox_backward_bound(gy, ei, ew, r ** 3))
+
+
+def test_cube_devox_backward_clustered(dev):
+    """r = 32 with every point inside a few voxels: long per-voxel sums (the
+    LDS float-atomic contention case) still within the sum-order bound."""
+    from pcr_amd import ops
+    b, n, c, r = 2, 2048, 64, 32
+    rng = np.random.default_rng(5)
+    cc = (rng.integers(10, 13, (b, 3, n)) + rng.uniform(0, 1, (b, 3, n)) * 0.999).astype(
+        np.float32)
+    _, ei, ew = oracle.trilinear_devoxelize_forward(r, cc, np.zeros((b, c, r ** 3), np.float32))
+    gy = rng.standard_normal((b, c, n)).astype(np.float32)
+    gx = ops.trilinear_devoxelize_backward(T(gy, dev), T(ei, dev), T(ew, dev), r)
+    exp = oracle.devoxelize_backward(gy, ei, ew, r, spherical=False)
+    assert_within_sum_order(N(gx), exp, devox_backward_bound(gy, ei, ew, r ** 3))
+
+
+def _sph_setup(b, n, c, r, seed):
+    xyz, _, feat = gaussian_clouds(b, n, seed=seed, c=c)
+    nc = oracle.normalize_sph(xyz)
+    grid, gind, cnt = oracle.spherical_avg_voxelize_forward(feat, nc, r)
+    return nc, feat, grid, gind, cnt
+
+
+def test_sph_devox_backward_c3_shape(dev):
+    """Spherical devox backward at the c3 per-cloud shape (N = 2048, r = 32,
+    C = 64, B = 4): the wave-sorted segmented path."""
+    from pcr_amd import ops
+    b, n, c, r = 4, 2048, 64, 32
+    nc, _, grid, gind, _ = _sph_setup(b, n, c, r, seed=31)
+    outs, inds, wgts = ops.spherical_trilinear_devoxelize_forward(r, True, T(nc, dev),
+                                                                  T(grid, dev), T(gind, dev))
+    eo, ei, ew = oracle.spherical_trilinear_devoxelize_forward(r, nc, grid, gind)
+    assert np.array_equal(N(inds), ei)
+    assert np.array_equal(N(wgts), ew)
+    assert np.array_equal(N(outs), eo)
+    gy = np.random.default_rng(32).standard_normal((b, c, n)).astype(np.float32)
+    gx = ops.spherical_trilinear_devoxelize_backward(T(gy, dev), inds, wgts, r)
+    exp = oracle.devoxelize_backward(gy, ei, ew, r, spherical=True)
+    assert_within_sum_order(N(gx), exp, devox_backward_bound(gy, ei, ew, r ** 3, skip_neg=True))
+
+
+@pytest.mark.parametrize("b,n,c,r", [(2, 1024, 64, 32), (2, 2048, 16, 16), (1, 4096, 8, 64)])
+def test_sph_devox_backward_sum_order(dev, b, n, c, r):
+    """The shapes of the older 1e-3 test, now at the sum-order bound."""
+    from pcr_amd import ops
+    nc, _, grid, gind, _ = _sph_setup(b, n, c, r, seed=5)
+    _, ei, ew = oracle.spherical_trilinear_devoxelize_forward(r, nc, grid, gind)
+    gy = np.random.default_rng(3).standard_normal((b, c, n)).astype(np.float32)
+    gx = ops.spherical_trilinear_devoxelize_backward(T(gy, dev), T(ei, dev), T(ew, dev), r)
+    exp = oracle.devoxelize_backward(gy, ei, ew, r, spherical=True)
+    assert_within_sum_order(N(gx), exp, devox_backward_bound(gy, ei, ew, r ** 3, skip_neg=True))
+
+
+def test_sph_avg_vox_backward_c3_shape(dev):
+    """spherical_avg_voxelize backward (spherical_vox.cu:139-163) at the c3
+    per-cloud shape: a gather, bit-exact (dropped points get 0)."""
+    from pcr_amd import ops
+    b, n, c, r = 4, 2048, 64, 32
+    nc, feat, _, gind, cnt = _sph_setup(b, n, c, r, seed=33)
+    gy = np.random.default_rng(34).standard_normal((b, c, r ** 3)).astype(np.float32)
+    gx = ops.spherical_avg_voxelize_backward(T(gy, dev), T(gind, dev), T(cnt, dev))
+    assert np.array_equal(N(gx), oracle.avg_voxelize_backward(gy, gind, cnt))
+    assert (N(gx)[np.broadcast_to((gind == -1)[:, None, :], gx.shape)] == 0).all()
+
+
+def test_cube_avg_vox_backward_c3_shape(dev):
+    from pcr_amd import ops
+    b, n, c, r = 4, 2048, 64, 32
+    rng = np.random.default_rng(35)
+    vc = rng.integers(0, r, (b, 3, n)).astype(np.int32)
+    feat = rng.uniform(-1, 1, (b, c, n)).astype(np.float32)
+    out, ind, cnt = ops.avg_voxelize_forward(T(feat, dev), T(vc, dev), r)
+    eo, ei, ec = oracle.avg_voxelize_forward(feat, vc, r)
+    assert np.array_equal(N(ind), ei)
+    assert np.array_equal(N(cnt), ec)
+    assert np.array_equal(N(out), eo)
+    gy = rng.standard_normal((b, c, r ** 3)).astype(np.float32)
+    gx = ops.avg_voxelize_backward(T(gy, dev), ind, cnt)
+    assert np.array_equal(N(gx), oracle.avg_voxelize_backward(gy, ei, ec))

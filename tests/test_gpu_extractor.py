@@ -61,29 +61,6 @@ def test_extractor_graph_replay(dev):
         assert torch.equal(out[key], v) or torch.allclose(out[key], v, equal_nan=True), key
 
 
-def test_extractor_pipelined_graph(dev):
-    """Several steps with no join between them (step i+1's KNN overlaps step
-    i's voxel stage): every step's descriptor and the final outputs equal the
-    single-step results."""
-    from pcr_amd.extractor import SphExtractor
-    b, n, c, k, r = 8, 1024, 64, 32, 32
-    xyz, nrm, feat = gaussian_clouds(b, n, seed=2, c=c)
-    tx, tn, tf = T(xyz, dev), T(nrm, dev), T(feat, dev)
-    ex = SphExtractor(b, n, c, k, r, device=dev)
-    ref = {kk: v.clone() for kk, v in ex.forward(tx, tn, tf).items()}
-    for mode in ("two", "two_dg", "two_fused", "two_sv", "three", "four", "sortvox", "four_split",
-                 "three_split", "two_stream", "three_stream", "four_stream"):
-        desc_steps = torch.empty((5, b, c), device=dev)
-        for _ in range(2):
-            out = ex.run_pipelined(tx, tn, tf, 5, desc_steps, mode=mode)
-        torch.cuda.synchronize()
-        for key, v in ref.items():
-            assert torch.equal(out[key], v) or torch.allclose(out[key], v, equal_nan=True), \
-                (mode, key)
-        for s in range(5):
-            assert torch.equal(desc_steps[s], ref["desc"]), (mode, s)
-
-
 @pytest.mark.parametrize("schedule", [0, 1, 2])
 def test_extractor_native_runner(dev, schedule):
     """pcr_extractor_run (the bench's native multi-step enqueue): every
@@ -94,14 +71,22 @@ def test_extractor_native_runner(dev, schedule):
     tx, tn, tf = T(xyz, dev), T(nrm, dev), T(feat, dev)
     ex = SphExtractor(b, n, c, k, r, device=dev)
     ref = {kk: v.clone() for kk, v in ex.forward(tx, tn, tf).items()}
-    desc_steps = torch.empty((5, b, c), device=dev)
-    for _ in range(2):
-        out = ex.run_native(tx, tn, tf, 5, desc_steps, schedule=schedule)
-    torch.cuda.synchronize()
-    for key, v in ref.items():
-        assert torch.equal(out[key], v) or torch.allclose(out[key], v, equal_nan=True), key
-    for s in range(5):
-        assert torch.equal(desc_steps[s], ref["desc"]), s
+    # the runner's events are reused across calls of different lengths, with
+    # and without grid-kernel timing
+    for steps, timed in ((5, False), (3, True), (5, True), (1, False)):
+        desc_steps = torch.empty((steps, b, c), device=dev)
+        for _ in range(2):
+            out = ex.run_native(tx, tn, tf, steps, desc_steps, schedule=schedule, timed=timed)
+        torch.cuda.synchronize()
+        for key, v in ref.items():
+            assert torch.equal(out[key], v) or torch.allclose(out[key], v, equal_nan=True), \
+                (steps, key)
+        for s in range(steps):
+            assert torch.equal(desc_steps[s], ref["desc"]), (steps, s)
+        if timed:
+            ms = ex.grid_kernel_times()
+            assert len(ms) == (0 if schedule == 0 else steps)
+            assert all(0 < t < 100 for t in ms)
 
 
 def test_extractor_full_size_properties(dev):
