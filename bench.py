@@ -44,7 +44,13 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=40)
-    ap.add_argument("--batch", type=int, default=32, help="clouds per GPU")
+    ap.add_argument("--workload", choices=("extract", "pairs"), default="extract",
+                    help="extract: BASELINE c2, the sph-dg extractor forward over 32 clouds "
+                         "per GPU; pairs: BASELINE c4, 256 clouds (128 registration pairs) "
+                         "per GPU, extractor forward over sources + targets, on-rank mutual-NN "
+                         "matching of their devoxelised features, descriptor all-gather")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="clouds per GPU (default 32 for extract, 256 for pairs)")
     ap.add_argument("--points", type=int, default=1024)
     ap.add_argument("--k", type=int, default=32)
     ap.add_argument("--res", type=int, default=32)
@@ -59,7 +65,12 @@ def parse():
     ap.add_argument("--steps-per-launch", type=int, default=40,
                     help="most pipelined steps per native runner call; --steps and --warmup "
                          "are split into calls of at most this many steps")
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.batch is None:
+        args.batch = 256 if args.workload == "pairs" else 32
+    if args.workload == "pairs" and args.batch % 2:
+        ap.error("--workload pairs needs an even --batch (source + target clouds)")
+    return args
 
 
 def synthetic_inputs(b, n, c, device, seed):
@@ -104,11 +115,14 @@ def cpu_baseline(args):
     on repeated batches of the same workload: once on one thread and once on
     every core this process may run on (len(os.sched_getaffinity(0))), each
     for about args.cpu_seconds.  The all-core figure is `value`."""
+    import numpy as np
     import oracle
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from clouds import gaussian_clouds
-    b, n, c, k, r = args.batch, args.points, args.channels, args.k, args.res
+    # the same workload on a sample batch of at most 32 clouds (16 pairs)
+    b, n, c, k, r = min(args.batch, 32), args.points, args.channels, args.k, args.res
     xyz, nrm, feat = gaussian_clouds(b, n, seed=0, c=c)
+    pairs = args.workload == "pairs"
 
     def one_batch():
         _, ki = oracle.knn_dir(xyz, xyz, k)
@@ -117,6 +131,9 @@ def cpu_baseline(args):
         grid, ind, _ = oracle.spherical_avg_voxelize_forward(feat, nc, r)
         dv, _, _ = oracle.spherical_trilinear_devoxelize_forward(r, nc, grid, ind)
         dv.max(axis=2)
+        if pairs:
+            f = dv.transpose(0, 2, 1)
+            oracle.mutual_nn(np.ascontiguousarray(f[:b // 2]), np.ascontiguousarray(f[b // 2:]))
 
     def rate(threads, seconds):
         oracle.set_num_threads(threads)
@@ -154,7 +171,20 @@ def main():
                                    stream_kernel_bytes_per_cloud)
     b, n, c, k, r = args.batch, args.points, args.channels, args.k, args.res
     xyz, nrm, feat = synthetic_inputs(b, n, c, dev, seed=1234 + rank)
-    ex = SphExtractor(b, n, c, k, r, device=dev)
+    if args.workload == "pairs":
+        # targets = sources rotated by a fixed rotation and permuted
+        rot = torch.linalg.qr(torch.randn(3, 3, generator=torch.Generator().manual_seed(7)))[0]
+        rot = rot.to(dev)
+        perm = torch.randperm(n, generator=torch.Generator().manual_seed(8)).to(dev)
+        p = b // 2
+        xyz[p:] = torch.einsum("ij,bjn->bin", rot, xyz[:p])[:, :, perm]
+        nrm[p:] = torch.einsum("ij,bjn->bin", rot, nrm[:p])[:, :, perm]
+        feat[p:] = feat[:p][:, :, perm]
+    if args.workload == "pairs":
+        from pcr_amd.registration import PairExtractor
+        ex = PairExtractor(b // 2, n, c, k, r, device=dev)
+    else:
+        ex = SphExtractor(b, n, c, k, r, device=dev)
 
     # the native runner enqueues up to S pipelined steps per call; the step
     # counts are split into calls of at most S steps (the last call shorter)
@@ -227,6 +257,10 @@ def main():
     total_clouds = b * world * args.steps
     value = total_clouds / elapsed
     step_bytes = algorithmic_bytes_per_cloud(n, k, r, c)["total"] * b
+    if args.workload == "pairs":
+        # matching: both clouds' [C, N] features read, corr12 / corr21 /
+        # idx1 / idx2 written (4 x 4N), per pair
+        step_bytes += (2 * 4 * c * n + 16 * n) * (b // 2)
     step_gbs = step_bytes * args.steps / elapsed / 1e9
     traffic = step_traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -253,9 +287,15 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (seeded gaussian clouds, unit normals, U(-1,1) features)",
-        "config": {"workload": "sph-dg extractor forward: self-KNN k=%d + local PPF + "
-                               "sph-vox r=%d^3 + sph-devox + descriptor" % (k, r),
-                   "clouds_per_gpu": b, "points": n, "k": k, "resolution": r, "channels": c,
+        "config": {"workload": ("sph-dg extractor forward: self-KNN k=%d + local PPF + "
+                                "sph-vox r=%d^3 + sph-devox + descriptor" % (k, r))
+                   if args.workload == "extract" else
+                   ("registration pairs (BASELINE c4): extractor forward over %d source + %d "
+                    "target clouds (self-KNN k=%d + local PPF + sph-vox r=%d^3 + sph-devox + "
+                    "descriptor), mutual-NN matching of each pair's devox features on-rank, "
+                    "descriptor all-gather" % (b // 2, b // 2, k, r)),
+                   "clouds_per_gpu": b, "pairs_per_gpu": b // 2 if args.workload == "pairs"
+                   else None, "points": n, "k": k, "resolution": r, "channels": c,
                    "global_batch": b * world, "parallelism": "dp%d (clouds sharded, "
                    "descriptor all-gather)" % world, "schedule": args.schedule,
                    "runner_calls": [len(chunks(args.warmup)), len(timed_chunks)],

@@ -260,6 +260,13 @@ size_t pcr_mutual_nn_workspace_size(int p, int n1, int n2);
 pcr_status pcr_mutual_nn_match(const float *f1, const float *f2, int p, int n1, int n2, int c,
                                int *corr12, int *corr21, int *idx1, int *idx2, int *count,
                                void *workspace, size_t workspace_bytes, void *stream);
+/* The same on channel-major per-point features -- f1 [p, c, n1], f2
+ * [p, c, n2], the [B, C, N] layout the extractor / PVConv produce -- so the
+ * registration step matches the devoxelised features in place (same sums,
+ * same results as pcr_mutual_nn_match on the transposes). */
+pcr_status pcr_mutual_nn_match_cm(const float *f1, const float *f2, int p, int n1, int n2, int c,
+                                  int *corr12, int *corr21, int *idx1, int *idx2, int *count,
+                                  void *workspace, size_t workspace_bytes, void *stream);
 
 /* ------------------------------------ LRF change_coords (8f f2) ----------
  * models/pvcnn_classify.py:153-184 (rot_invariant_preprocess ==
@@ -364,6 +371,15 @@ typedef struct pcr_extractor_args {
   size_t knn_ws_bytes;
   void *vox_ws[2];                        /* pcr_extractor_workspace_size(b, n, c, r) */
   size_t vox_ws_bytes;
+  /* registration pairs (BASELINE c4, datasets/deepgmr_mn40.py:71-97,
+   * 232-244): match_pairs = P > 0 with b == 2P makes every step also match
+   * the devoxelised per-point features of cloud i (source) against cloud
+   * P + i (target) by pcr_mutual_nn_match_cm, on the prep stream after the
+   * step's devox; outputs [P, n] (count [P]) as that function's. */
+  int match_pairs;
+  int *corr12, *corr21, *idx1, *idx2, *match_count;
+  void *match_ws;                         /* pcr_mutual_nn_workspace_size(P, n, n) */
+  size_t match_ws_bytes;
 } pcr_extractor_args;
 pcr_status pcr_extractor_run(pcr_runner *runner, const pcr_extractor_args *args, int steps,
                              int schedule, float *desc_steps, void *origin, void *s_nbr,

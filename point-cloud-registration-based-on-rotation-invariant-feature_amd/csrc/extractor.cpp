@@ -75,6 +75,17 @@ pcr_status knn_select_ppf(const pcr_extractor_args* a, int q, bool sorted, hipSt
                                a->n, a->k, 1, a->relative, a->local_ppf, st);
 }
 
+// the step's registration matching (source clouds [0, P) against targets
+// [P, 2P)) on the devox features the step just wrote
+pcr_status match_pairs(const pcr_extractor_args* a, hipStream_t st) {
+  if (a->match_pairs <= 0) return PCR_OK;
+  const int P = a->match_pairs;
+  const float* src = a->devox;
+  const float* tgt = a->devox + (size_t)P * a->c * a->n;
+  return pcr_mutual_nn_match_cm(src, tgt, P, a->n, a->n, a->c, a->corr12, a->corr21, a->idx1,
+                                a->idx2, a->match_count, a->match_ws, a->match_ws_bytes, st);
+}
+
 }  // namespace
 }  // namespace pcr
 
@@ -129,6 +140,9 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
               "extractor_run: invalid arguments");
   PCR_REQUIRE(a->b >= 0 && a->n >= 1 && a->c >= 1 && a->k >= 1 && a->r >= 1,
               "extractor_run: invalid sizes");
+  PCR_REQUIRE(a->match_pairs <= 0 || a->b == 2 * a->match_pairs,
+              "extractor_run: match_pairs %d needs b == 2 * match_pairs (b = %d)",
+              a->match_pairs, a->b);
   if (steps == 0 || a->b == 0) return PCR_OK;
   const hipStream_t org = as_stream(origin), sn = as_stream(s_nbr_p), sp = as_stream(s_pre_p),
                     sv = as_stream(s_vox_p);
@@ -166,6 +180,7 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
                                         a->norm_coords, a->ind, a->cnt, a->grid, a->devox,
                                         a->dinds[0], a->dwgts[0], desc, a->vox_ws[0],
                                         a->vox_ws_bytes, sv));
+      PCR_TRY(match_pairs(a, sv));
       continue;
     }
     const int q = s & 1;
@@ -182,6 +197,7 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
                                             a->dinds[q], a->dwgts[q], desc, a->vox_ws[q],
                                             a->vox_ws_bytes, sp));
     PCR_HIP(hipEventRecord(means_done[q], sp), "means record");
+    PCR_TRY(match_pairs(a, sp));
     PCR_HIP(hipStreamWaitEvent(sv, means_done[q], 0), "means wait");
     const bool timed = s < rn->timed_cap;
     if (timed) PCR_HIP(hipEventRecord(rn->t0[s], sv), "timing record");

@@ -26,6 +26,20 @@ __global__ __launch_bounds__(256) void match_sqnorm_kernel(const float* __restri
   sq[i] = pcr_match_sqnorm(f + i * c, c);
 }
 
+// the same chain over channel-major features [p][c][n] (the extractor's
+// per-point feature layout): consecutive threads read consecutive points
+__global__ __launch_bounds__(256) void match_sqnorm_cm_kernel(const float* __restrict__ f, int n,
+                                                              int c, float* __restrict__ sq) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int p = blockIdx.y;
+  if (i >= n) return;
+  const float* col = f + (size_t)p * c * n + i;
+  float s = 0.0f;
+  for (int k = 0; k < c; k++) s = __builtin_fmaf(col[(size_t)k * n], col[(size_t)k * n], s);
+  const float r = __builtin_sqrtf(s);
+  sq[(size_t)p * n + i] = r * r;  // pcr_match_sqnorm
+}
+
 constexpr int kMT = 128;  // tile rows (f1) and columns (f2)
 constexpr int kKC = 32;   // channels per LDS stage
 constexpr int kMPad = kMT + 4;
@@ -63,10 +77,28 @@ __device__ inline void match_load_stage(const float* __restrict__ A, const float
   }
 }
 
+// Channel-major operands ([c][rows] per pair): thread t holds row t % 128
+// of A and of B, channels 16 (t / 128) .. +15 of the stage, so each channel
+// row is read as 128 consecutive floats.
+__device__ inline void match_load_stage_cm(const float* __restrict__ A,
+                                           const float* __restrict__ B, int i0, int j0, int n1,
+                                           int n2, int c, int k0, int lr, int lk, float (&va)[16],
+                                           float (&vb)[16]) {
+  const int ka = k0 + lk;
+  const bool ra = i0 + lr < n1, rb = j0 + lr < n2;
+#pragma unroll
+  for (int e = 0; e < 16; e++) {
+    const int k = ka + e;
+    va[e] = (ra && k < c) ? A[(size_t)k * n1 + i0 + lr] : 0.0f;
+    vb[e] = (rb && k < c) ? B[(size_t)k * n2 + j0 + lr] : 0.0f;
+  }
+}
+
 // Channels run through LDS in stages of 32, double-buffered: the next
 // stage's global loads are in flight while the MFMAs consume this one, and
 // one barrier per stage suffices (a buffer is rewritten two stages later,
 // after every wave passed the barrier in between).
+template <bool CM>
 __global__ __launch_bounds__(256) void match_tile_kernel(
     const float* __restrict__ f1, const float* __restrict__ f2, int n1, int n2, int c,
     const float* __restrict__ sq1, const float* __restrict__ sq2,
@@ -86,9 +118,16 @@ __global__ __launch_bounds__(256) void match_tile_kernel(
     for (int tj = 0; tj < 2; tj++)
 #pragma unroll
       for (int v = 0; v < 16; v++) acc[ti][tj][v] = 0.0f;
-  const int lr = tid >> 1, lk = (tid & 1) * 16;
+  const int lr = CM ? (tid & (kMT - 1)) : (tid >> 1);
+  const int lk = CM ? (tid / kMT) * 16 : (tid & 1) * 16;
   float va[16], vb[16];
-  match_load_stage(A, B, i0, j0, n1, n2, c, 0, lr, lk, va, vb);
+  auto load = [&](int k0) {
+    if (CM)
+      match_load_stage_cm(A, B, i0, j0, n1, n2, c, k0, lr, lk, va, vb);
+    else
+      match_load_stage(A, B, i0, j0, n1, n2, c, k0, lr, lk, va, vb);
+  };
+  load(0);
   int buf = 0;
   for (int k0 = 0; k0 < c; k0 += kKC, buf ^= 1) {
 #pragma unroll
@@ -97,7 +136,7 @@ __global__ __launch_bounds__(256) void match_tile_kernel(
       b_s[buf][lk + e][lr] = vb[e];
     }
     lds_barrier();
-    if (k0 + kKC < c) match_load_stage(A, B, i0, j0, n1, n2, c, k0 + kKC, lr, lk, va, vb);
+    if (k0 + kKC < c) load(k0 + kKC);
     // k ascending: every product enters its accumulator in channel order
 #pragma unroll
     for (int kk = 0; kk < kKC; kk += 2) {
@@ -239,29 +278,54 @@ extern "C" size_t pcr_mutual_nn_workspace_size(int p, int n1, int n2) {
   return match_ws_layout(p, n1, n2, nullptr, nullptr, nullptr, nullptr, nullptr);
 }
 
-extern "C" pcr_status pcr_mutual_nn_match(const float* f1, const float* f2, int p, int n1, int n2,
-                                          int c, int* corr12, int* corr21, int* idx1, int* idx2,
-                                          int* count, void* workspace, size_t workspace_bytes,
-                                          void* stream) {
-  PCR_REQUIRE(p >= 0 && n1 >= 1 && n2 >= 1 && c >= 1, "mutual_nn_match: invalid sizes");
-  PCR_REQUIRE(p <= 65535, "mutual_nn_match: too many pairs (%d)", p);
+static pcr_status mutual_nn(bool cm, const float* f1, const float* f2, int p, int n1, int n2,
+                            int c, int* corr12, int* corr21, int* idx1, int* idx2, int* count,
+                            void* workspace, size_t workspace_bytes, void* stream,
+                            const char* name) {
+  PCR_REQUIRE(p >= 0 && n1 >= 1 && n2 >= 1 && c >= 1, "%s: invalid sizes", name);
+  PCR_REQUIRE(p <= 65535, "%s: too many pairs (%d)", name, p);
   if (p == 0) return PCR_OK;
   float *sq1, *sq2;
   unsigned long long *rb, *cb;
   const size_t need = match_ws_layout(p, n1, n2, &sq1, &sq2, &rb, &cb, (char*)workspace);
   PCR_REQUIRE(workspace != nullptr && workspace_bytes >= need,
-              "mutual_nn_match: workspace too small (%zu < %zu)", workspace_bytes, need);
+              "%s: workspace too small (%zu < %zu)", name, workspace_bytes, need);
   hipStream_t st = as_stream(stream);
   if (hipMemsetAsync(rb, 0xFF, (size_t)p * n1 * 8, st) != hipSuccess ||
       hipMemsetAsync(cb, 0xFF, (size_t)p * n2 * 8, st) != hipSuccess)
-    return launch_status("mutual_nn_match memset");
-  hipLaunchKernelGGL(match_sqnorm_kernel, dim3((unsigned)ceil_div64((int64_t)p * n1, 256)),
-                     dim3(256), 0, st, f1, p * n1, c, sq1);
-  hipLaunchKernelGGL(match_sqnorm_kernel, dim3((unsigned)ceil_div64((int64_t)p * n2, 256)),
-                     dim3(256), 0, st, f2, p * n2, c, sq2);
-  hipLaunchKernelGGL(match_tile_kernel, dim3(ceil_div(n2, kMT), ceil_div(n1, kMT), p), dim3(256),
-                     0, st, f1, f2, n1, n2, c, sq1, sq2, rb, cb);
+    return launch_status(name);
+  if (cm) {
+    hipLaunchKernelGGL(match_sqnorm_cm_kernel, dim3(ceil_div(n1, 256), p), dim3(256), 0, st, f1,
+                       n1, c, sq1);
+    hipLaunchKernelGGL(match_sqnorm_cm_kernel, dim3(ceil_div(n2, 256), p), dim3(256), 0, st, f2,
+                       n2, c, sq2);
+    hipLaunchKernelGGL(match_tile_kernel<true>, dim3(ceil_div(n2, kMT), ceil_div(n1, kMT), p),
+                       dim3(256), 0, st, f1, f2, n1, n2, c, sq1, sq2, rb, cb);
+  } else {
+    hipLaunchKernelGGL(match_sqnorm_kernel, dim3((unsigned)ceil_div64((int64_t)p * n1, 256)),
+                       dim3(256), 0, st, f1, p * n1, c, sq1);
+    hipLaunchKernelGGL(match_sqnorm_kernel, dim3((unsigned)ceil_div64((int64_t)p * n2, 256)),
+                       dim3(256), 0, st, f2, p * n2, c, sq2);
+    hipLaunchKernelGGL(match_tile_kernel<false>, dim3(ceil_div(n2, kMT), ceil_div(n1, kMT), p),
+                       dim3(256), 0, st, f1, f2, n1, n2, c, sq1, sq2, rb, cb);
+  }
   hipLaunchKernelGGL(match_finalize_kernel, dim3(p), dim3(1024), 0, st, rb, cb, n1, n2, corr12,
                      corr21, idx1, idx2, count);
-  return launch_status("mutual_nn_match");
+  return launch_status(name);
+}
+
+extern "C" pcr_status pcr_mutual_nn_match(const float* f1, const float* f2, int p, int n1, int n2,
+                                          int c, int* corr12, int* corr21, int* idx1, int* idx2,
+                                          int* count, void* workspace, size_t workspace_bytes,
+                                          void* stream) {
+  return mutual_nn(false, f1, f2, p, n1, n2, c, corr12, corr21, idx1, idx2, count, workspace,
+                   workspace_bytes, stream, "mutual_nn_match");
+}
+
+extern "C" pcr_status pcr_mutual_nn_match_cm(const float* f1, const float* f2, int p, int n1,
+                                             int n2, int c, int* corr12, int* corr21, int* idx1,
+                                             int* idx2, int* count, void* workspace,
+                                             size_t workspace_bytes, void* stream) {
+  return mutual_nn(true, f1, f2, p, n1, n2, c, corr12, corr21, idx1, idx2, count, workspace,
+                   workspace_bytes, stream, "mutual_nn_match_cm");
 }

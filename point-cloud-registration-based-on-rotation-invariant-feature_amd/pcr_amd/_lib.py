@@ -57,6 +57,7 @@ SIGNATURES = {
     "pcr_extractor_run": (ST, [P, P, I, I, P, P, P, P, P]),
     "pcr_mutual_nn_workspace_size": (SZ, [I, I, I]),
     "pcr_mutual_nn_match": (ST, [P, P, I, I, I, I, P, P, P, P, P, P, SZ, P]),
+    "pcr_mutual_nn_match_cm": (ST, [P, P, I, I, I, I, P, P, P, P, P, P, SZ, P]),
     "pcr_lrf_change_coords": (ST, [P, I, I, P, P, P, P, P]),
     "pcr_gather_features_forward": (ST, [P, P, I, I, I, I, P, P]),
     "pcr_gather_features_backward": (ST, [P, P, I, I, I, I, P, P]),
@@ -80,7 +81,9 @@ class ExtractorArgs(ctypes.Structure):
                 ("xyz", P), ("normals", P), ("features", P), ("knn_idx", P), ("knn_dist", P),
                 ("local_ppf", P), ("norm_coords", P), ("ind", P), ("cnt", P), ("grid", P),
                 ("devox", P), ("desc", P), ("dinds", P * 2), ("dwgts", P * 2), ("knn_ws", P * 2),
-                ("knn_ws_bytes", SZ), ("vox_ws", P * 2), ("vox_ws_bytes", SZ)]
+                ("knn_ws_bytes", SZ), ("vox_ws", P * 2), ("vox_ws_bytes", SZ),
+                ("match_pairs", I), ("corr12", P), ("corr21", P), ("idx1", P), ("idx2", P),
+                ("match_count", P), ("match_ws", P), ("match_ws_bytes", SZ)]
 
 
 _lib = None

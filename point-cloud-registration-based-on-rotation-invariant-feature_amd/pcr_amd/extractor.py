@@ -282,14 +282,16 @@ class SphExtractor:
         return list(ms[:cnt.value])
 
     def run_native(self, xyz, normals, features, steps, desc_steps=None, schedule=1,
-                   timed=False):
+                   timed=False, match=None):
         """`steps` pipelined steps enqueued by the library's native runner
         (pcr_extractor_run): schedule 1 = three streams (prep + means / devox
         on s_pre, the grid stream on s_vox, sort + select + PPF on s_nbr,
         voxel buffer sets alternating), 2 = as 1 with the Morton sort on
         s_pre, 0 = two streams with the fused grid kernel.  One ctypes call
         for all steps.  timed: bracket each step's grid-stream kernel with
-        timing events (read back with grid_kernel_times())."""
+        timing events (read back with grid_kernel_times()).  match: a
+        registration.PairMatch whose buffers receive, every step, the
+        mutual-NN matching of clouds [0, B/2) against [B/2, B)."""
         self._check_inputs(xyz, normals, features)
         runner = self._get_runner(steps if timed else 0)
         s1 = self._set(1)
@@ -308,6 +310,15 @@ class SphExtractor:
         a.knn_ws_bytes = self.knn_ws.numel()
         a.vox_ws[0], a.vox_ws[1] = _ptr(self.ws), _ptr(s1[1])
         a.vox_ws_bytes = self.ws.numel()
+        if match is not None:
+            if 2 * match.pairs != self.b or match.n != self.n:
+                raise RuntimeError("match buffers are for %d pairs of %d points"
+                                   % (match.pairs, match.n))
+            a.match_pairs = match.pairs
+            a.corr12, a.corr21 = _ptr(match.corr12), _ptr(match.corr21)
+            a.idx1, a.idx2, a.match_count = _ptr(match.idx1), _ptr(match.idx2), \
+                _ptr(match.count)
+            a.match_ws, a.match_ws_bytes = _ptr(match.ws), match.ws.numel()
         if desc_steps is not None and tuple(desc_steps.shape) != (steps, self.b, self.c):
             raise RuntimeError("desc_steps must be [steps, B, C]")
         cur = torch.cuda.current_stream(self.device)

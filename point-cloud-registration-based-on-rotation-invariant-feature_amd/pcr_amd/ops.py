@@ -465,30 +465,39 @@ def estimate_normals(points, radius=0.1, return_counts=False):
     return (normals, counts) if return_counts else normals
 
 
-def mutual_nn_match(feat1, feat2):
+def mutual_nn_match(feat1, feat2, channel_major=False, workspace=None):
     """Feature-space mutual nearest neighbours of p registration pairs
     (datasets/deepgmr_mn40.py:232-244, batched): feat1 [p, n1, c],
     feat2 [p, n2, c] -> (corr12 [p, n1], corr21 [p, n2], idx1 [p, n1],
     idx2 [p, n1], count [p]); the first count[q] entries of idx1[q] / idx2[q]
-    are the mutual pairs in ascending idx1, the rest -1."""
+    are the mutual pairs in ascending idx1, the rest -1.  channel_major:
+    feat1 [p, c, n1], feat2 [p, c, n2] (the extractor's per-point layout),
+    matched in place."""
     _check(feat1, "feat1")
     _check(feat2, "feat2")
-    if feat1.dim() != 3 or feat2.dim() != 3 or feat1.shape[0] != feat2.shape[0] or \
-            feat1.shape[2] != feat2.shape[2]:
-        raise RuntimeError("mutual_nn_match: expected feat1 [p, n1, c] and feat2 [p, n2, c]")
-    p, n1, c = feat1.shape
-    n2 = feat2.shape[1]
+    if feat1.dim() != 3 or feat2.dim() != 3 or feat1.shape[0] != feat2.shape[0]:
+        raise RuntimeError("mutual_nn_match: expected 3-d features with equal pair counts")
+    if channel_major:
+        p, c, n1 = feat1.shape
+        n2, c2 = feat2.shape[2], feat2.shape[1]
+    else:
+        p, n1, c = feat1.shape
+        n2, c2 = feat2.shape[1], feat2.shape[2]
+    if c != c2:
+        raise RuntimeError("mutual_nn_match: channel counts differ (%d vs %d)" % (c, c2))
     dev = feat1.device
     i32 = dict(dtype=torch.int32, device=dev)
     corr12, corr21 = torch.empty((p, n1), **i32), torch.empty((p, n2), **i32)
     idx1, idx2 = torch.empty((p, n1), **i32), torch.empty((p, n1), **i32)
     count = torch.empty((p,), **i32)
     lib = _lib.load()
-    ws = torch.empty(max(256, lib.pcr_mutual_nn_workspace_size(p, n1, n2)), dtype=torch.uint8,
-                     device=dev)
-    _lib.check(lib.pcr_mutual_nn_match(
-        _ptr(feat1), _ptr(feat2), p, n1, n2, c, _ptr(corr12), _ptr(corr21), _ptr(idx1),
-        _ptr(idx2), _ptr(count), _ptr(ws), ws.numel(), _stream()), "mutual_nn_match")
+    need = max(256, lib.pcr_mutual_nn_workspace_size(p, n1, n2))
+    ws = workspace if workspace is not None and workspace.numel() >= need else \
+        torch.empty(need, dtype=torch.uint8, device=dev)
+    fn = lib.pcr_mutual_nn_match_cm if channel_major else lib.pcr_mutual_nn_match
+    _lib.check(fn(_ptr(feat1), _ptr(feat2), p, n1, n2, c, _ptr(corr12), _ptr(corr21),
+                  _ptr(idx1), _ptr(idx2), _ptr(count), _ptr(ws), ws.numel(), _stream()),
+               "mutual_nn_match")
     return corr12, corr21, idx1, idx2, count
 
 

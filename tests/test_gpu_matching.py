@@ -41,3 +41,19 @@ def test_mutual_nn_permutation_and_ties(dev):
     exp = oracle.mutual_nn(f1[None], f2[None])
     for g, e in zip(got, exp):
         assert np.array_equal(g.cpu().numpy(), e)
+
+
+@pytest.mark.parametrize("p,n1,n2,c", [(2, 300, 280, 64), (3, 1024, 1024, 64), (1, 257, 129, 33)])
+def test_mutual_nn_channel_major(dev, p, n1, n2, c):
+    """pcr_mutual_nn_match_cm on [p, c, n] features == the oracle on the
+    transposes (same fmaf chains: bit-exact)."""
+    from pcr_amd import ops
+    rng = np.random.default_rng(p + n1 + 3 * c)
+    f1 = rng.standard_normal((p, c, n1), dtype=np.float32)
+    f2 = rng.standard_normal((p, c, n2), dtype=np.float32)
+    got = ops.mutual_nn_match(torch.from_numpy(f1).to(dev), torch.from_numpy(f2).to(dev),
+                              channel_major=True)
+    exp = oracle.mutual_nn(np.ascontiguousarray(f1.transpose(0, 2, 1)),
+                           np.ascontiguousarray(f2.transpose(0, 2, 1)))
+    for g, e, name in zip(got, exp, ("corr12", "corr21", "idx1", "idx2", "count")):
+        assert np.array_equal(g.cpu().numpy(), e), name
