@@ -998,6 +998,10 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
   };
   __syncthreads();
   PCR_STAMP(0);
+#ifdef PCR_DIAG
+  if (threadIdx.x == 0 && PCR_WG_LINEAR < 1024)
+    pcr_diag_stamps[PCR_WG_LINEAR][14] = __builtin_amdgcn_s_memrealtime();
+#endif
 
   // 1. bound
   {
@@ -1128,7 +1132,10 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) tmax = max(tmax, __shfl_xor(tmax, off, kWave));
     tmax = __builtin_amdgcn_readfirstlane(tmax);
-    for (int i = total + wv; i < tmax; i += NW) buf_s[i * kBlk + lane] = PCR_KEY_PAD;
+    // rows [total, tpad) of every lane read as padding: the rank sweep reads
+    // eight rows per wait
+    const int tpad = (tmax + 7) & ~7;
+    for (int i = total + wv; i < tpad; i += NW) buf_s[i * kBlk + lane] = PCR_KEY_PAD;
     __syncthreads();
     PCR_STAMP(3);
 
@@ -1148,11 +1155,14 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     }
     auto sweep = [&](auto ne_c) {
       constexpr int NE = decltype(ne_c)::value;
-#pragma unroll 2
-      for (int j2 = 0; j2 < tmax; j2++) {
-        const kkey o = buf_s[j2 * kBlk + lane];
+      for (int j2 = 0; j2 < tpad; j2 += 8) {
+        kkey o[8];
 #pragma unroll
-        for (int e = 0; e < NE; e++) rank[e] += o < key[e] ? 1 : 0;
+        for (int u = 0; u < 8; u++) o[u] = buf_s[(j2 + u) * kBlk + lane];
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+#pragma unroll
+          for (int e = 0; e < NE; e++) rank[e] += o[u] < key[e] ? 1 : 0;
       }
     };
     if (ne <= 3)
@@ -1227,6 +1237,10 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
       }
     }
     PCR_STAMP(6);
+#ifdef PCR_DIAG
+    if (threadIdx.x == 0 && PCR_WG_LINEAR < 1024)
+      pcr_diag_stamps[PCR_WG_LINEAR][15] = __builtin_amdgcn_s_memrealtime();
+#endif
     return;
   }
 

@@ -35,7 +35,16 @@ __global__ __launch_bounds__(256) void match_sqnorm_cm_kernel(const float* __res
   if (i >= n) return;
   const float* col = f + (size_t)p * c * n + i;
   float s = 0.0f;
-  for (int k = 0; k < c; k++) s = __builtin_fmaf(col[(size_t)k * n], col[(size_t)k * n], s);
+  int k = 0;
+  // 16 loads in flight before the (ordered) chain consumes them
+  for (; k + 16 <= c; k += 16) {
+    float v[16];
+#pragma unroll
+    for (int e = 0; e < 16; e++) v[e] = col[(size_t)(k + e) * n];
+#pragma unroll
+    for (int e = 0; e < 16; e++) s = __builtin_fmaf(v[e], v[e], s);
+  }
+  for (; k < c; k++) s = __builtin_fmaf(col[(size_t)k * n], col[(size_t)k * n], s);
   const float r = __builtin_sqrtf(s);
   sq[(size_t)p * n + i] = r * r;  // pcr_match_sqnorm
 }

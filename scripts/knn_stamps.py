@@ -1,0 +1,50 @@
+"""Per-phase s_memtime stamps of the KNN selection at BASELINE c2 (diagnostic
+library lib/libpcr_amd_diag.so, `make -C <pkg>/csrc diag`).  Phases: 0->1
+bound, 1->2 count, 2->3 cut + collect, 3->4 rank, 4->5 scatter.  Not part of
+the product."""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "point-cloud-registration-based-on-rotation-invariant-feature_amd")
+os.environ["PCR_AMD_LIB"] = os.path.join(PKG, "lib", os.environ.get("DIAGLIB", "libpcr_amd_diag.so"))
+sys.path[:0] = [ROOT, PKG]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+from pcr_amd import _lib  # noqa: E402
+from pcr_amd.extractor import SphExtractor  # noqa: E402
+
+b, n, k = int(os.environ.get("B", 32)), int(os.environ.get("N", 1024)), 32
+dev = torch.device("cuda:0")
+g = torch.Generator(device=dev).manual_seed(0)
+xyz = torch.randn((b, 3, n), generator=g, device=dev)
+xyz = (xyz - xyz.mean(2, keepdim=True)).contiguous()
+nrm = torch.randn((b, 3, n), generator=g, device=dev)
+ex = SphExtractor(b, n, 8, k, 8, device=dev)
+s = torch.cuda.current_stream().cuda_stream
+ok = ex.knn_sort(xyz, s)
+for _ in range(3):
+    ex.knn_select(xyz, nrm, s, sorted_ok=ok, ppf=False)
+torch.cuda.synchronize()
+buf = (ctypes.c_ulonglong * (1024 * 16))()
+_lib.load().pcr_diag_read_knn(buf)
+a = np.frombuffer(buf, dtype=np.uint64).reshape(1024, 16).astype(np.int64)
+nwg = min(1024, b * ((n + 63) // 64))
+a = a[:nwg]
+for p in range(1, 7):
+    d = a[:, p] - a[:, p - 1]
+    okp = (a[:, p] > 0) & (a[:, p - 1] > 0)
+    if okp.any():
+        print("phase %d->%d: median %d max %d cycles" % (p - 1, p, np.median(d[okp]), d[okp].max()))
+t0, t5 = a[:, 0][a[:, 0] > 0], a[:, 6][a[:, 6] > 0]
+print("span %d cycles over %d workgroups" % (t5.max() - t0.min(), nwg))
+rt = (a[:, 15] - a[:, 14]).astype(np.float64)
+cy = (a[:, 6] - a[:, 0]).astype(np.float64)
+okr = (a[:, 15] > 0) & (a[:, 14] > 0) & (a[:, 6] > 0)
+if okr.any():
+    print("shader clock (s_memtime / s_memrealtime at 100 MHz): median %.0f MHz; "
+          "phase 0->6 median %.1f us" % (np.median(cy[okr] / rt[okr]) * 100,
+                                         np.median(rt[okr]) / 100.0))
+    t14, t15 = a[:, 14][okr], a[:, 15][okr]
+    print("realtime span of stamped phases over workgroups: %.1f us" % ((t15.max() - t14.min()) / 100.0))
