@@ -375,6 +375,101 @@ __global__ __launch_bounds__(256) void ball_query_kernel(const float* __restrict
     for (int v = cnt; v < u; v++) I[v] = first;
 }
 
+// The same query, one wave per 64 centres (lane = centre) and NW waves per
+// workgroup, each wave scanning a contiguous quarter of the points in index
+// order.  The cloud is staged in LDS once per workgroup and read as
+// broadcast float4s (four candidates per read), the squared distances run
+// two candidates per packed instruction in the reference's contraction
+// order (pcr_sumsq3f: y*y, then +x*x, then +z*z), and every accepted point
+// is appended to the lane's u16 list of its wave in LDS.  The lists of the
+// NW waves concatenate in index order, so the first u of them, padded with
+// the first hit (0 if none), are the reference's slots; they are written
+// out row by row with coalesced stores.  (double)d2 > 1e-5 is evaluated as
+// d2 > 1e-5f: float(1e-5) lies below 1e-5, so for every float d2 the two
+// agree.
+constexpr int kBqWaves = 4;
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void ball_query_wave_kernel(
+    const float* __restrict__ centers, const float* __restrict__ points, int m, int n, int npad,
+    float r2, int u, int* __restrict__ idx) {
+  extern __shared__ __align__(16) unsigned char bq_s[];
+  float* px = (float*)bq_s;
+  float* py = px + npad;
+  float* pz = py + npad;
+  unsigned short* lst = (unsigned short*)(pz + npad);  // [NW][u][64]
+  __shared__ int cnt_s[NW][kWave];
+  const int b = blockIdx.y;
+  const int c0 = blockIdx.x * kWave;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const float* P = points + (size_t)b * 3 * n;
+  for (int i = tid; i < npad; i += NW * kWave) {
+    const bool ok = i < n;
+    px[i] = ok ? P[i] : __builtin_nanf("");
+    py[i] = ok ? P[n + i] : __builtin_nanf("");
+    pz[i] = ok ? P[2 * n + i] : __builtin_nanf("");
+  }
+  const int j = c0 + lane;
+  const bool live = j < m;
+  const float* C = centers + (size_t)b * 3 * m;
+  const float cx = live ? C[j] : 0.0f, cy = live ? C[m + j] : 0.0f, cz = live ? C[2 * m + j] : 0.0f;
+  __syncthreads();
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const f2 cx2 = {cx, cx}, cy2 = {cy, cy}, cz2 = {cz, cz};
+  const int q = ((npad / 4 + NW - 1) / NW) * 4;
+  const int t0 = min(npad, wv * q), t1 = min(npad, t0 + q);
+  unsigned short* my = lst + (size_t)wv * u * kWave + lane;
+  int cnt = 0;
+  for (int t = t0; t < t1; t += 4) {
+    const float4 X = *(const float4*)(px + t);
+    const float4 Y = *(const float4*)(py + t);
+    const float4 Z = *(const float4*)(pz + t);
+    f2 d[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const f2 dx = cx2 - (h ? f2{X.z, X.w} : f2{X.x, X.y});
+      const f2 dy = cy2 - (h ? f2{Y.z, Y.w} : f2{Y.x, Y.y});
+      const f2 dz = cz2 - (h ? f2{Z.z, Z.w} : f2{Z.x, Z.y});
+      f2 a = dy * dy;
+      a = __builtin_elementwise_fma(dx, dx, a);
+      d[h] = __builtin_elementwise_fma(dz, dz, a);
+    }
+    const float dd[4] = {d[0][0], d[0][1], d[1][0], d[1][1]};
+#pragma unroll
+    for (int h = 0; h < 4; h++) {
+      if (dd[h] < r2 && dd[h] > 1e-5f && cnt < u) {
+        my[cnt * kWave] = (unsigned short)(t + h);
+        cnt++;
+      }
+    }
+  }
+  cnt_s[wv][lane] = cnt;
+  __syncthreads();
+  // output rows: slot s of centre `row` comes from the wave whose list
+  // covers it in the concatenation
+  for (int row = 0; row < kWave; row++) {
+    const int jj = c0 + row;
+    if (jj >= m) break;
+    int off[NW + 1];
+    off[0] = 0;
+#pragma unroll
+    for (int w = 0; w < NW; w++) off[w + 1] = off[w] + cnt_s[w][row];
+    int first = 0;
+#pragma unroll
+    for (int w = NW - 1; w >= 0; w--)
+      if (cnt_s[w][row] > 0) first = lst[(size_t)w * u * kWave + row];
+    int* I = idx + ((size_t)b * m + jj) * u;
+    for (int sl = tid; sl < u; sl += NW * kWave) {
+      int v = first;
+#pragma unroll
+      for (int w = 0; w < NW; w++)
+        if (sl >= off[w] && sl < off[w + 1])
+          v = lst[((size_t)w * u + (sl - off[w])) * kWave + row];
+      I[sl] = v;
+    }
+  }
+}
+
 // grouping.cu:29-35: one thread per output element, coalesced stores
 __global__ __launch_bounds__(256) void grouping_kernel(const float* __restrict__ feat,
                                                        const int* __restrict__ idx, int c, int n,
@@ -596,8 +691,17 @@ extern "C" pcr_status pcr_ball_query(const float* centers, const float* points, 
   PCR_REQUIRE(b >= 0 && m >= 0 && n >= 0 && u >= 1, "ball_query: invalid sizes");
   if (b == 0 || m == 0) return PCR_OK;
   const float r2 = radius * radius;  // ball_query.cpp:24 (float * float)
-  hipLaunchKernelGGL(ball_query_kernel, dim3(ceil_div(m, 256), b), dim3(256), 0,
-                     as_stream(stream), centers, points, m, n, r2, u, idx);
+  const int npad = (n + 3) / 4 * 4;
+  const size_t smem = (size_t)npad * 12 + (size_t)kBqWaves * u * kWave * 2;
+  if (n >= 1 && n <= 65535 && smem <= 96 * 1024) {
+    allow_big_lds(ball_query_wave_kernel<kBqWaves>, smem);
+    hipLaunchKernelGGL(ball_query_wave_kernel<kBqWaves>, dim3(ceil_div(m, kWave), b),
+                       dim3(kBqWaves * kWave), smem, as_stream(stream), centers, points, m, n,
+                       npad, r2, u, idx);
+  } else {
+    hipLaunchKernelGGL(ball_query_kernel, dim3(ceil_div(m, 256), b), dim3(256), 0,
+                       as_stream(stream), centers, points, m, n, r2, u, idx);
+  }
   return launch_status("ball_query");
 }
 

@@ -293,3 +293,24 @@ def test_sph_devox_backward_irregular_corners(dev):
     gy = rng.standard_normal((b, c, n)).astype(np.float32)
     gx = ops.spherical_trilinear_devoxelize_backward(T(gy, dev), T(inds, dev), T(wgts, dev), r)
     close(N(gx), oracle.devoxelize_backward(gy, inds, wgts, r, spherical=True), 1e-4)
+
+
+@pytest.mark.parametrize("b,m,n,radius,u,scale", [
+    (3, 1024, 1024, 0.3, 128, 0.35),   # the sph-dg model's BallQuery(0.3, 128) at c2
+    (2, 700, 1500, 0.3, 16, 0.35),     # centres != points, u reached early (index-order cut)
+    (2, 513, 2048, 0.2, 128, 0.35),    # c3 per-cloud size, ragged centre count
+    (1, 64, 77, 0.9, 200, 0.35),       # u > n: padding with the first hit
+    (1, 100, 300, 0.05, 8, 1.0),       # sparse: many centres with no hit (all-0 rows)
+    (2, 256, 9000, 0.3, 64, 0.35),     # beyond the u16 / LDS fast path: the scan kernel
+])
+def test_ball_query_paths(dev, b, m, n, radius, u, scale):
+    """pcr_ball_query's wave kernel (and the per-centre scan past its LDS
+    budget) against ball_query.cu:30-49 as the oracle restates it."""
+    from pcr_amd import ops
+    rng = np.random.default_rng(m + n + u)
+    pts = (rng.standard_normal((b, 3, n)) * scale).astype(np.float32)
+    ctr = (rng.standard_normal((b, 3, m)) * scale).astype(np.float32)
+    ctr[:, :, :min(m, n) // 4] = pts[:, :, :min(m, n) // 4]   # centres on points: d2 = 0 excluded
+    pts[:, :, 5:9] = pts[:, :, 1:2]                             # duplicates
+    idx = ops.ball_query(T(ctr, dev), T(pts, dev), radius, u)
+    assert np.array_equal(N(idx), oracle.ball_query(ctr, pts, radius, u))
