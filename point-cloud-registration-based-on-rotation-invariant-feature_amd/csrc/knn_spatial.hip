@@ -743,10 +743,6 @@ __device__ inline float cand_dist(float qx, float qy, float qz, float sx, float 
 // two candidates at once (v_pk_add / v_pk_mul / v_pk_fma_f32); per element
 // the same operations and roundings as cand_dist
 __device__ inline pf2 cand_dist2(pf2 qx, pf2 qy, pf2 qz, pf2 sx, pf2 sy, pf2 sz) {
-#if defined(KNN_EXP) && KNN_EXP == 6
-  return pf2{cand_dist(qx[0], qy[0], qz[0], sx[0], sy[0], sz[0]),
-             cand_dist(qx[1], qy[1], qz[1], sx[1], sy[1], sz[1])};
-#endif
   const pf2 a = qx - sx, bq = qy - sy, c = qz - sz;
   pf2 d = a * a;
   d = __builtin_elementwise_fma(bq, bq, d);
@@ -1029,44 +1025,41 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
   const float ftop = (qlive && !fallback) ? __uint_as_float((unsigned)(etop + 1) << 21) : 0.0f;
 
   PCR_STAMP(1);
-  // 2. count
-  if (!fallback) {
+  // 2. count + 3. cut.  Pass 1 counts quarter-octave bins (float bits >> 21)
+  // of the kNB below D_q's bin.  A block where some query has more than CAP
+  // keys at its cut (a bin of many near-equal distances: an outlier facing
+  // the bulk of the cloud) recounts inside each query's cut bin with
+  // 1/64-octave bins (bits >> 17) before it gives up to the insertion
+  // fallback.  Every wave computes the same cut for its 64 queries.
+  int total = 0, slot = 0, bstar = -1;
+  int shift = 21, base = ebase;
+  unsigned ucut = 0u;
+#ifdef PCR_DIAG
+  int diag_reason = fallback ? 1 : 0;
+#endif
+  auto count_cut = [&](float lim) {
     unsigned* hw = hist_s + (size_t)(wv / FPD) * (kNB + 1) * kBlk + lane;
     const unsigned inc = 1u << ((wv % FPD) * CB);
-#if defined(KNN_EXP) && KNN_EXP == 7
-    unsigned xacc = 0;
-#endif
-    // counter of bin e (clamped to [ebase, ebase + kNB]; the last = not
+    // counter of bin e (clamped to [base, base + kNB]; the last = not
     // counted, also NaN) at hwb + e * kBlk
-    unsigned* hwb = hw - ebase * kBlk;
-    const int etop1 = ebase + kNB;
-    visit(ftop, [&](int, const float (&d)[4]) {
+    unsigned* hwb = hw - base * kBlk;
+    const int top = base + kNB;
+    const int sh = shift;
+    visit(lim, [&](int, const float (&d)[4]) {
 #pragma unroll
       for (int h = 0; h < 4; h++) {
-        const int e = med3_i32((int)(__float_as_uint(d[h]) >> 21), ebase, etop1);
-#if defined(KNN_EXP) && KNN_EXP == 7
-        xacc += (unsigned)e << (h * 5);
-#else
+        const int e = med3_i32((int)(__float_as_uint(d[h]) >> sh), base, top);
         __hip_atomic_fetch_add(hwb + e * kBlk, inc, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_WORKGROUP);
-#endif
       }
     });
-#if defined(KNN_EXP) && KNN_EXP == 7
-    if (xacc == 0x9e3779b9u) hw[0] = xacc;
-#endif
-  }
-  __syncthreads();
-
-  PCR_STAMP(2);
-  // 3. cut (every wave computes the same values for its 64 queries)
-  int total = 0, slot = 0;
-  unsigned ucut = 0u;
-  if (!fallback) {
+    __syncthreads();
+    PCR_STAMP(2);
     unsigned cum[NG], cut[NG];
 #pragma unroll
     for (int g = 0; g < NG; g++) cum[g] = cut[g] = 0u;
-    int bstar = -1;
+    bstar = -1;
+    total = 0;
 #pragma unroll
     for (int bin = 0; bin < kNB; bin++) {
       int tb = 0;
@@ -1082,19 +1075,40 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
         for (int g = 0; g < NG; g++) cut[g] = cum[g];
       }
     }
-    fallback = __any(qlive && (bstar < 0 || total > CAP));
-    if (qlive && !fallback) ucut = (unsigned)(ebase + bstar + 1) << 21;
     // slots of the waves before this one
     const int mg = wv / FPD;
     const unsigned below = (1u << ((wv % FPD) * CB)) - 1u;
+    slot = 0;
 #pragma unroll
     for (int g = 0; g < NG; g++)
       slot += (int)field_sum<CB>(g < mg ? cut[g] : (g == mg ? (cut[g] & below) : 0u));
+  };
+  if (!fallback) {
+    count_cut(ftop);
+    const bool no_cut = __any(qlive && bstar < 0);
+#ifdef PCR_DIAG
+    diag_reason |= (no_cut ? 2 : 0) | (__any(qlive && total > CAP) ? 4 : 0);
+#endif
+    if (!no_cut && __any(qlive && total > CAP)) {
+      // refine: bin 0 = below the cut bin, bins 1..16 = its 16 sub-bins
+      const float lim = qlive ? __uint_as_float((unsigned)(base + bstar + 1) << 21) : 0.0f;
+      base = qlive ? ((base + bstar) << 4) - 1 : 0;
+      shift = 17;
+      __syncthreads();  // pass-1 histogram reads done
+      for (int i = threadIdx.x; i < NG * (kNB + 1) * kBlk; i += NW * kBlk) hist_s[i] = 0u;
+      __syncthreads();
+      count_cut(lim);
+#ifdef PCR_DIAG
+      diag_reason |= 8;
+#endif
+    }
+    fallback = __any(qlive && (bstar < 0 || total > CAP));
+    if (qlive && !fallback) ucut = (unsigned)(base + bstar + 1) << shift;
   }
   __syncthreads();  // histogram reads done: buf_s overwrites it
 #ifdef PCR_DIAG
   if (threadIdx.x == 0 && PCR_WG_LINEAR < 1024) {
-    pcr_diag_stamps[PCR_WG_LINEAR][8] = fallback ? 1 : 0;
+    pcr_diag_stamps[PCR_WG_LINEAR][8] = diag_reason;
     pcr_diag_stamps[PCR_WG_LINEAR][9] = (unsigned long long)total;
     pcr_diag_stamps[PCR_WG_LINEAR][10] = (unsigned long long)nvisit;
   }
@@ -1114,16 +1128,11 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
         const int j4[4] = {jj.x, jj.y, jj.z, jj.w};
 #pragma unroll
         for (int h = 0; h < 4; h++) {
-#if defined(KNN_EXP) && KNN_EXP == 9
-          buf_s[(take[h] ? slot : CAP) * kBlk + lane] = make_key(d[h], j4[h]);
-          slot += take[h] ? 1 : 0;
-#else
           // exec-masked: only the taking lanes store (few lanes of a wave)
           if (take[h]) {
             buf_s[slot * kBlk + lane] = make_key(d[h], j4[h]);
             slot++;
           }
-#endif
         }
       }
     });
@@ -1250,10 +1259,11 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
   for (int s2 = 0; s2 < k; s2++) buf_s[s2 * kBlk + lane] = undef;
   kkey kth = undef;
   for (int blk = 0; blk < nblk; blk++) {
-    const float* bx = cs.x + cbase + (size_t)blk * kBlk;
-    const float* by = cs.y + cbase + (size_t)blk * kBlk;
-    const float* bz = cs.z + cbase + (size_t)blk * kBlk;
-    const int* bj = cs.j + cbase + (size_t)blk * kBlk;
+    // cached clouds read the candidates from LDS (broadcast reads)
+    const float* bx = CL ? cand_s + blk * kBlk : cs.x + cbase + (size_t)blk * kBlk;
+    const float* by = CL ? cand_s + CACHE + blk * kBlk : cs.y + cbase + (size_t)blk * kBlk;
+    const float* bz = CL ? cand_s + 2 * CACHE + blk * kBlk : cs.z + cbase + (size_t)blk * kBlk;
+    const int* bj = CL ? cand_j + blk * kBlk : cs.j + cbase + (size_t)blk * kBlk;
     for (int t = 0; t < kBlk; t++) {
       const kkey x = make_key(cand_dist(qx, qy, qz, bx[t], by[t], bz[t]), bj[t]);
       if (x < kth) {
@@ -1305,6 +1315,13 @@ static void launch_select(const KnnSet& qs, const KnnSet& cs, int b, int k, floa
 #define PCR_SEL(CBV, CLV, CACHEV)                                                             \
   hipLaunchKernelGGL((knn_select_kernel<NW, CBV, CLV, PPF, CAP, KSEL, CACHEV>), grid, blk, 0, st, \
                      qs, cs, k, dist, idx, qxyz, qnrm, cxyz, cnrm, relative, ppf)
+  if constexpr (CAP == kCap) {
+    // c3 clouds (2048 points): 32 KB of candidates in LDS, two workgroups per CU
+    if (cs.npad > kSelCache && cs.npad <= 2 * kSelCache) {
+      PCR_SEL(16, true, 2 * kSelCache);
+      return;
+    }
+  }
   if (per_wave <= 255 && cs.npad <= kSelCache)
     PCR_SEL(8, true, kSelCache);
   else if (per_wave <= 255)

@@ -1,7 +1,7 @@
 """Times the KNN selection launch alone (the Morton sort done once before),
 HIP events on the launching stream, at BASELINE c2 (32 x 1024, k=32) and the
 c3 per-cloud shape (256 x 2048, k=32), and checks the result against the
-one-call path.  usage: python scripts/knn_select_time.py"""
+one-call path.  usage: [CFG=BxNxK,...] python scripts/knn_select_time.py"""
 import os
 import sys
 
@@ -14,7 +14,10 @@ from pcr_amd import ops  # noqa: E402
 from pcr_amd.extractor import SphExtractor  # noqa: E402
 
 dev = torch.device("cuda:0")
-for b, n, k in ((32, 1024, 32), (256, 2048, 32), (32, 1024, 16)):
+CFG = os.environ.get("CFG")
+cfgs = [tuple(int(v) for v in c.split("x")) for c in CFG.split(",")] if CFG else \
+    [(32, 1024, 32), (256, 2048, 32), (32, 1024, 16)]
+for b, n, k in cfgs:
     g = torch.Generator(device=dev).manual_seed(0)
     xyz = torch.randn((b, 3, n), generator=g, device=dev)
     xyz = (xyz - xyz.mean(2, keepdim=True)).contiguous()

@@ -38,6 +38,11 @@ for p in range(1, 7):
     if okp.any():
         print("phase %d->%d: median %d max %d cycles" % (p - 1, p, np.median(d[okp]), d[okp].max()))
 t0, t5 = a[:, 0][a[:, 0] > 0], a[:, 6][a[:, 6] > 0]
+fb = a[:, 8]
+for code in sorted(set(int(v) for v in fb if v)):
+    w = np.where(fb == code)[0]
+    print("cut flags %d (1 no bound, 2 cut below range, 4 over capacity, 8 refined): "
+          "%d workgroups, first %s" % (code, len(w), [int(v) for v in w[:6]]))
 print("span %d cycles over %d workgroups" % (t5.max() - t0.min(), nwg))
 rt = (a[:, 15] - a[:, 14]).astype(np.float64)
 cy = (a[:, 6] - a[:, 0]).astype(np.float64)

@@ -44,8 +44,9 @@ def test_select_k_values(dev, k):
 
 @pytest.mark.parametrize("n", [1000, 65, 129, 700, 1025, 2048, 3001, 4096])
 def test_select_ragged_sizes(dev, n):
-    """<= 1024 points: the LDS candidate cache; beyond (BASELINE c3: 2048):
-    the global-memory sweep with per-block box tests and 16-bit fields."""
+    """<= 1024 points: the LDS candidate cache with byte fields; <= 2048
+    (BASELINE c3): the 2048-candidate cache with 16-bit fields; beyond: the
+    global-memory sweep with per-block box tests."""
     xyz, _, _ = gaussian_clouds(2, n, seed=n)
     check_self(dev, xyz, 32)
 
@@ -53,6 +54,20 @@ def test_select_ragged_sizes(dev, n):
 def test_select_cached_2k_duplicates_and_k16(dev):
     xyz, _, _ = gaussian_clouds(2, 2048, seed=77)
     xyz[0, :, 500:700] = xyz[0, :, 500:501]  # fallback blocks past the LDS cache
+    check_self(dev, xyz, 32)
+    check_self(dev, xyz, 16)
+
+
+@pytest.mark.parametrize("n", [1024, 2048, 3001])
+def test_select_outlier_refined_cut(dev, n):
+    """Far outliers facing a compact cloud: their distances to the bulk fall
+    into one or two quarter-octave bins (far more than the 88-key capacity),
+    so their query blocks recount inside the cut bin with 1/64-octave bins
+    (the refinement pass) instead of taking the insertion fallback."""
+    xyz, _, _ = gaussian_clouds(2, n, seed=n + 5)
+    xyz[0, :, 7] = (30.0, 0.0, 0.0)
+    xyz[0, :, n // 2] = (0.0, -12.0, 5.0)
+    xyz[1, :, n - 1] = (8.0, 8.0, 8.0)
     check_self(dev, xyz, 32)
     check_self(dev, xyz, 16)
 
