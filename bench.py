@@ -62,6 +62,9 @@ def parse():
                     help="pcr_extractor_run schedule (include/pcr_amd.h): 1 = three streams "
                          "(sort+select+PPF / prep+means+devox / dense-grid stream), 2 = as 1 "
                          "with the Morton sort on the prep stream, 0 = two streams")
+    ap.add_argument("--no-kernel-timing", action="store_true",
+                    help="diagnostic: no timing events around the grid kernel (no in-step "
+                         "kernel duration; checks the events' own cost)")
     ap.add_argument("--steps-per-launch", type=int, default=40,
                     help="most pipelined steps per native runner call; --steps and --warmup "
                          "are split into calls of at most this many steps")
@@ -231,7 +234,7 @@ def main():
     for i, m in enumerate(timed_chunks):
         # the last call of the timed region also brackets every step's grid
         # kernel with timing events on its stream (in-step durations)
-        launch(i, m, timed=(i == len(timed_chunks) - 1))
+        launch(i, m, timed=(i == len(timed_chunks) - 1) and not args.no_kernel_timing)
     for w in pending:
         w.wait()
     pending.clear()

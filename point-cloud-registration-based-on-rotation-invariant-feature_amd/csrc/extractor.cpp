@@ -184,6 +184,41 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
       continue;
     }
     const int q = s & 1;
+    // diagnostic builds only: PCR_RUN_SKIP drops launches to price each
+    // kernel's share of the step (1 select, 2 PPF, 4 grid stream, 8 prep,
+    // 16 means, 32 sort; 8/16/32 after the first two steps)
+    static const int skip = PCR_KNOB("PCR_RUN_SKIP", 0);
+    if (skip && schedule == 1) {
+      const bool warm = s >= 2;
+      if (!(warm && (skip & 8))) {
+        if (s >= 2) PCR_HIP(hipStreamWaitEvent(sp, stream_done[q], 0), "slot wait");
+        PCR_TRY(pcr_extractor_voxel_prep(a->xyz, a->b, a->n, a->r, a->norm_coords, a->ind,
+                                           a->dinds[q], a->dwgts[q], a->vox_ws[q],
+                                           a->vox_ws_bytes, sp));
+      }
+      if (!(warm && (skip & 16)))
+        PCR_TRY(pcr_extractor_voxel_means_devox(a->features, a->b, a->c, a->n, a->r, a->devox,
+                                                a->dinds[q], a->dwgts[q], desc, a->vox_ws[q],
+                                                a->vox_ws_bytes, sp));
+      PCR_HIP(hipEventRecord(means_done[q], sp), "means record");
+      PCR_HIP(hipStreamWaitEvent(sv, means_done[q], 0), "means wait");
+      if (s < rn->timed_cap) PCR_HIP(hipEventRecord(rn->t0[s], sv), "timing record");
+      if (!(skip & 4))
+        PCR_TRY(pcr_extractor_voxel_stream(a->b, a->c, a->n, a->r, a->cnt, a->grid,
+                                           a->vox_ws[q], a->vox_ws_bytes, sv));
+      if (s < rn->timed_cap) PCR_HIP(hipEventRecord(rn->t1[s], sv), "timing record");
+      PCR_HIP(hipEventRecord(stream_done[q], sv), "stream record");
+      if (!(warm && (skip & 32))) PCR_TRY(knn_sort(a, 0, sn, &sorted));
+      else sorted = true;
+      if (!(skip & 1))
+        PCR_TRY(pcr_knn_local_ppf_prepared(a->xyz, a->normals, a->b, a->n, a->k, a->relative,
+                                           a->knn_idx, a->knn_dist, nullptr, a->knn_ws[0],
+                                           a->knn_ws_bytes, sn));
+      if (!(skip & 2))
+        PCR_TRY(pcr_local_ppf_forward(a->xyz, a->normals, a->xyz, a->normals, a->knn_idx, a->b,
+                                      a->n, a->n, a->k, 1, a->relative, a->local_ppf, sn));
+      continue;
+    }
     if (schedule == 2) {
       if (s >= 2) PCR_HIP(hipStreamWaitEvent(sp, sel_done[q], 0), "knn slot wait");
       PCR_TRY(knn_sort(a, q, sp, &sorted));
