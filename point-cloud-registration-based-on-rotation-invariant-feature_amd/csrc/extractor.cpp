@@ -186,12 +186,15 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
     const int q = s & 1;
     // diagnostic builds only: PCR_RUN_SKIP drops launches to price each
     // kernel's share of the step (1 select, 2 PPF, 4 grid stream, 8 prep,
-    // 16 means, 32 sort; 8/16/32 after the first two steps)
+    // 16 means, 32 sort; 8/16/32 after the first two steps; 64: the grid
+    // stream does not wait for the means event, 128: no stream_done record,
+    // 256: prep does not wait for the slot; 64-256 break the ordering)
     static const int skip = PCR_KNOB("PCR_RUN_SKIP", 0);
     if (skip && schedule == 1) {
       const bool warm = s >= 2;
       if (!(warm && (skip & 8))) {
-        if (s >= 2) PCR_HIP(hipStreamWaitEvent(sp, stream_done[q], 0), "slot wait");
+        if (s >= 2 && !(skip & 256))
+          PCR_HIP(hipStreamWaitEvent(sp, stream_done[q], 0), "slot wait");
         PCR_TRY(pcr_extractor_voxel_prep(a->xyz, a->b, a->n, a->r, a->norm_coords, a->ind,
                                            a->dinds[q], a->dwgts[q], a->vox_ws[q],
                                            a->vox_ws_bytes, sp));
@@ -201,13 +204,13 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
                                                 a->dinds[q], a->dwgts[q], desc, a->vox_ws[q],
                                                 a->vox_ws_bytes, sp));
       PCR_HIP(hipEventRecord(means_done[q], sp), "means record");
-      PCR_HIP(hipStreamWaitEvent(sv, means_done[q], 0), "means wait");
+      if (!(skip & 64)) PCR_HIP(hipStreamWaitEvent(sv, means_done[q], 0), "means wait");
       if (s < rn->timed_cap) PCR_HIP(hipEventRecord(rn->t0[s], sv), "timing record");
       if (!(skip & 4))
         PCR_TRY(pcr_extractor_voxel_stream(a->b, a->c, a->n, a->r, a->cnt, a->grid,
                                            a->vox_ws[q], a->vox_ws_bytes, sv));
       if (s < rn->timed_cap) PCR_HIP(hipEventRecord(rn->t1[s], sv), "timing record");
-      PCR_HIP(hipEventRecord(stream_done[q], sv), "stream record");
+      if (!(skip & 128)) PCR_HIP(hipEventRecord(stream_done[q], sv), "stream record");
       if (!(warm && (skip & 32))) PCR_TRY(knn_sort(a, 0, sn, &sorted));
       else sorted = true;
       if (!(skip & 1))

@@ -1786,6 +1786,12 @@ extern "C" pcr_status pcr_extractor_voxel_stream(int b, int c, int n, int r, int
   if (aux == 0 && uu == 4) PCR_LAUNCH_STREAM(4, 3, 4, 0);
   else if (aux == 0) PCR_LAUNCH_STREAM(4, 3, 2, 0);
   else if (aux == 2) PCR_LAUNCH_STREAM(4, 3, 2, 2);
+#ifdef PCR_DIAG
+  else if (aux == 17) PCR_LAUNCH_STREAM(4, 3, 2, 17);
+  else if (aux == 18) PCR_LAUNCH_STREAM(4, 3, 2, 18);
+  else if (aux == 19) PCR_LAUNCH_STREAM(4, 3, 2, 19);
+  else if (aux == 1) PCR_LAUNCH_STREAM(4, 3, 2, 1);
+#endif
   else if (uu == 4) PCR_LAUNCH_STREAM(4, 3, 4, 16);
   else PCR_LAUNCH_STREAM(4, 3, 2, 16);
 #undef PCR_LAUNCH_STREAM
