@@ -727,8 +727,13 @@ __global__ __launch_bounds__(kMeansNT) void vox_means_kernel(
   constexpr int NT = kMeansNT;
   constexpr int PB = kMeansMaxN / NT;  // points per thread
   extern __shared__ __align__(16) unsigned char smem_raw[];
-  const int b = blockIdx.x / ngrp;
-  const int grp = blockIdx.x % ngrp;
+  // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs, so with
+  // a batch of a multiple of 8 clouds XCD x runs every channel group of
+  // clouds x, x + 8, ...: a cloud's corner data and point order (read by all
+  // its channel groups) fill one XCD's L2 instead of all eight
+  const int nb = gridDim.x / ngrp;
+  const int b = (nb & 7) ? blockIdx.x / ngrp : (blockIdx.x & 7) + 8 * ((blockIdx.x >> 3) / ngrp);
+  const int grp = (nb & 7) ? blockIdx.x % ngrp : (blockIdx.x >> 3) % ngrp;
   const int c0 = grp * G;
   const int gcount = min(G, c - c0);
   const int tid = threadIdx.x;
