@@ -848,38 +848,41 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
       constexpr int S = kBlk / NW;
       constexpr int GPB = S / 4;
       static_assert(S % 4 == 0, "a wave owns whole groups of four");
-      const int ng = nblk * GPB;
-      auto off = [&](int g) { return (g / GPB) * kBlk + wv * S + (g % GPB) * 4; };
-      // two groups per iteration, the next two groups' reads in flight
-      auto rd = [&](int g, float4& X, float4& Y, float4& Z) {
-        const int o = off(g);
-        X = *(const float4*)(cand_s + o);
-        Y = *(const float4*)(cand_s + CACHE + o);
-        Z = *(const float4*)(cand_s + 2 * CACHE + o);
+      static_assert(GPB == 2, "two groups of four per wave and block");
+      // one block (two groups) per half iteration; positions advance by a
+      // constant, so every read is one base register plus an immediate.
+      // Reads past the last block land in the next LDS array (never used).
+      auto rd = [&](int o, float4 (&X)[2], float4 (&Y)[2], float4 (&Z)[2]) {
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+          X[h] = *(const float4*)(cand_s + o + 4 * h);
+          Y[h] = *(const float4*)(cand_s + CACHE + o + 4 * h);
+          Z[h] = *(const float4*)(cand_s + 2 * CACHE + o + 4 * h);
+        }
       };
-      auto eval = [&](int g, const float4& X, const float4& Y, const float4& Z) {
-        const pf2 d0 = cand_dist2(qx2, qy2, qz2, pf2{X.x, X.y}, pf2{Y.x, Y.y}, pf2{Z.x, Z.y});
-        const pf2 d1 = cand_dist2(qx2, qy2, qz2, pf2{X.z, X.w}, pf2{Y.z, Y.w}, pf2{Z.z, Z.w});
-        const float d[4] = {d0[0], d0[1], d1[0], d1[1]};
-        f(off(g), d);
+      auto eval = [&](int o, const float4 (&X)[2], const float4 (&Y)[2], const float4 (&Z)[2]) {
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+          const pf2 d0 = cand_dist2(qx2, qy2, qz2, pf2{X[h].x, X[h].y}, pf2{Y[h].x, Y[h].y},
+                                    pf2{Z[h].x, Z[h].y});
+          const pf2 d1 = cand_dist2(qx2, qy2, qz2, pf2{X[h].z, X[h].w}, pf2{Y[h].z, Y[h].w},
+                                    pf2{Z[h].z, Z[h].w});
+          const float d[4] = {d0[0], d0[1], d1[0], d1[1]};
+          f(o + 4 * h, d);
+        }
       };
       // ping-pong register sets A / B, no copies: B's reads are issued
       // before A's evaluation (and its LDS atomics / stores) and vice versa
-      auto cl = [&](int g) { return g < ng ? g : ng - 1; };
-      float4 AX0, AY0, AZ0, AX1, AY1, AZ1, BX0, BY0, BZ0, BX1, BY1, BZ1;
-      rd(cl(0), AX0, AY0, AZ0);
-      rd(cl(1), AX1, AY1, AZ1);
-      for (int g = 0; g < ng; g += 4) {
-        rd(cl(g + 2), BX0, BY0, BZ0);
-        rd(cl(g + 3), BX1, BY1, BZ1);
+      float4 AX[2], AY[2], AZ[2], BX[2], BY[2], BZ[2];
+      int o = wv * S;
+      rd(o, AX, AY, AZ);
+      for (int blk = 0; blk < nblk; blk += 2, o += 2 * kBlk) {
+        rd(o + kBlk, BX, BY, BZ);
         __builtin_amdgcn_sched_barrier(0);  // reads first, then A's (older) data is waited on
-        eval(g, AX0, AY0, AZ0);
-        if (g + 1 < ng) eval(g + 1, AX1, AY1, AZ1);
-        rd(cl(g + 4), AX0, AY0, AZ0);
-        rd(cl(g + 5), AX1, AY1, AZ1);
+        eval(o, AX, AY, AZ);
+        rd(o + 2 * kBlk, AX, AY, AZ);
         __builtin_amdgcn_sched_barrier(0);
-        if (g + 2 < ng) eval(g + 2, BX0, BY0, BZ0);
-        if (g + 3 < ng) eval(g + 3, BX1, BY1, BZ1);
+        if (blk + 1 < nblk) eval(o + kBlk, BX, BY, BZ);
       }
     } else if (breg) {
       // which of this wave's blocks does any query lane need?  Lane l tests
