@@ -188,7 +188,8 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
     // kernel's share of the step (1 select, 2 PPF, 4 grid stream, 8 prep,
     // 16 means, 32 sort; 8/16/32 after the first two steps; 64: the grid
     // stream does not wait for the means event, 128: no stream_done record,
-    // 256: prep does not wait for the slot; 64-256 break the ordering)
+    // 256: prep does not wait for the slot, 512: PPF on its own stream;
+    // 64-512 break the ordering)
     static const int skip = PCR_KNOB("PCR_RUN_SKIP", 0);
     if (skip && schedule == 1) {
       const bool warm = s >= 2;
@@ -217,9 +218,17 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
         PCR_TRY(pcr_knn_local_ppf_prepared(a->xyz, a->normals, a->b, a->n, a->k, a->relative,
                                            a->knn_idx, a->knn_dist, nullptr, a->knn_ws[0],
                                            a->knn_ws_bytes, sn));
+      // 512: the PPF on `origin` after the selection's event (timing only:
+      // the next selection may overwrite the indices it reads)
+      hipStream_t sppf = sn;
+      if (skip & 512) {
+        PCR_HIP(hipEventRecord(sel_done[q], sn), "select record");
+        PCR_HIP(hipStreamWaitEvent(org, sel_done[q], 0), "select wait");
+        sppf = org;
+      }
       if (!(skip & 2))
         PCR_TRY(pcr_local_ppf_forward(a->xyz, a->normals, a->xyz, a->normals, a->knn_idx, a->b,
-                                      a->n, a->n, a->k, 1, a->relative, a->local_ppf, sn));
+                                      a->n, a->n, a->k, 1, a->relative, a->local_ppf, sppf));
       continue;
     }
     if (schedule == 2) {

@@ -871,9 +871,9 @@ __global__ __launch_bounds__(kMeansNT) void vox_means_kernel(
 //    third buffer while the streamers store item t.  Under the write stream
 //    a load round trip takes microseconds; with two items of slack it never
 //    holds a barrier.  The barriers wait for LDS operations only.
-constexpr int kStreamG = 2;      // channels per item
-constexpr int kStreamNG = 9;     // 1 KB LDS-DMA pieces per item: two rows of ms <= 1152 floats
-constexpr int kStreamNB = 3;     // means buffers (item t streams, t+1 ready, t+2 landing)
+constexpr int kStreamG = 4;      // channels per item
+constexpr int kStreamNG = 17;    // 1 KB LDS-DMA pieces per item: four rows of ms <= 1088 floats
+constexpr int kStreamNB = 2;     // means buffers (item t streams, t+1 landing)
 constexpr int kStreamMaxN = 1024;
 constexpr int kStreamMaxW = 1024;  // occupancy words (r^3 <= 32768)
 
@@ -894,13 +894,12 @@ __device__ inline void lds_only_barrier() {
 }
 
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-template <int NS, int NB, int U, int AUX>
+template <int NS, int NB, int U, int AUX, int G = kStreamG, int NG = kStreamNG>
 __global__ __launch_bounds__((NS + 1) * 64) void vox_stream_kernel(int c, int n, int r3, VoxWs ws,
                                                                   float* __restrict__ out,
                                                                   int* __restrict__ cnt_out,
                                                                   int ngrp, int wpc, int per,
                                                                   int dbg) {
-  constexpr int G = kStreamG, NG = kStreamNG;
   constexpr int D = NB - 1;     // prefetch distance in items
   constexpr int NTS = NS * 64;  // streamer threads
   constexpr int BUFB = NG * 1024;
@@ -1764,10 +1763,17 @@ extern "C" pcr_status pcr_extractor_voxel_stream(int b, int c, int n, int r, int
   PCR_REQUIRE(n <= kStreamMaxN && r3 <= 32 * kStreamMaxW && r3 % 128 == 0,
               "%s: n=%d r=%d unsupported (n <= %d, r^3 <= %d, r^3 %% 128 == 0)", name, n, r,
               kStreamMaxN, 32 * kStreamMaxW);
-  PCR_REQUIRE(2 * ws.ms * 4 <= kStreamNG * 1024, "%s: means rows too long", name);
-  const int ngrp = ceil_div(c, kStreamG);
+  // channels per item G (one occupancy / segment-index computation per G
+  // stores) and means buffers NB; diagnostic builds can pick other shapes
+  static const int gk = PCR_KNOB("PCR_STREAM_G", 4);
+  static const int nbk = PCR_KNOB("PCR_STREAM_NB", 2);
+  const int G = gk == 8 ? 8 : gk == 2 ? 2 : 4;
+  const int NGP = G == 8 ? 33 : G == 4 ? 17 : 9;  // 1 KB pieces: G rows of ms <= 1024 G / ... floats
+  const int NB = (G == 4 && nbk == 3) ? 3 : G == 2 ? 3 : kStreamNB;
+  PCR_REQUIRE(G * ws.ms * 4 <= NGP * 1024, "%s: means rows too long", name);
+  const int ngrp = ceil_div(c, G);
   // a few workgroups per cloud (about one per CU in all), each a contiguous
-  // range of channel-pair items of that cloud
+  // range of channel-group items of that cloud
   static const int cap = PCR_KNOB("PCR_STREAM_WGS", 0);
   const int total = cap > 0 ? cap : device_cus();
   int wpc = total / (b > 0 ? b : 1);
@@ -1775,30 +1781,28 @@ extern "C" pcr_status pcr_extractor_voxel_stream(int b, int c, int n, int r, int
   if (wpc > ngrp) wpc = ngrp;
   const int per = ceil_div(ngrp, wpc);
   static const int dbg = PCR_KNOB("PCR_STREAM_DBG", 0);
-  static const int nb = PCR_KNOB("PCR_STREAM_NB", kStreamNB);
   PCR_REQUIRE(ws.W % 64 == 0, "%s: r^3 %% 2048 != 0 unsupported", name);
-  static const int uu = PCR_KNOB("PCR_STREAM_U", 2);
-  const size_t smem = (size_t)nb * kStreamNG * 1024 + (size_t)ws.W * 6 +
+  const size_t smem = (size_t)NB * NGP * 1024 + (size_t)ws.W * 6 +
                       ((size_t)ws.ms * 2 + 255) / 256 * 256;
-  static const int aux = PCR_KNOB("PCR_STREAM_AUX", 16);
-#define PCR_LAUNCH_STREAM(NSV, NBV, UV, AV)                                                    \
+#ifdef PCR_DIAG
+  static const int aux = PCR_KNOB("PCR_STREAM_AUX", 16);  // store cache policy experiments
+#endif
+#define PCR_LAUNCH_STREAM(NSV, NBV, UV, AV, GV, NGV)                                           \
   do {                                                                                        \
-    allow_big_lds(vox_stream_kernel<NSV, NBV, UV, AV>, smem);                                 \
-    hipLaunchKernelGGL((vox_stream_kernel<NSV, NBV, UV, AV>), dim3(b * wpc),                  \
+    allow_big_lds(vox_stream_kernel<NSV, NBV, UV, AV, GV, NGV>, smem);                        \
+    hipLaunchKernelGGL((vox_stream_kernel<NSV, NBV, UV, AV, GV, NGV>), dim3(b * wpc),         \
                        dim3((NSV + 1) * 64), smem, as_stream(stream), c, n, r3, ws, grid, cnt, \
                        ngrp, wpc, per, dbg);                                                  \
   } while (0)
-  if (aux == 0 && uu == 4) PCR_LAUNCH_STREAM(4, 3, 4, 0);
-  else if (aux == 0) PCR_LAUNCH_STREAM(4, 3, 2, 0);
-  else if (aux == 2) PCR_LAUNCH_STREAM(4, 3, 2, 2);
 #ifdef PCR_DIAG
-  else if (aux == 17) PCR_LAUNCH_STREAM(4, 3, 2, 17);
-  else if (aux == 18) PCR_LAUNCH_STREAM(4, 3, 2, 18);
-  else if (aux == 19) PCR_LAUNCH_STREAM(4, 3, 2, 19);
-  else if (aux == 1) PCR_LAUNCH_STREAM(4, 3, 2, 1);
+  if (G == 2) PCR_LAUNCH_STREAM(4, 3, 2, 16, 2, 9);
+  else if (G == 8) PCR_LAUNCH_STREAM(4, 2, 2, 16, 8, 33);
+  else if (NB == 3) PCR_LAUNCH_STREAM(4, 3, 2, 16, 4, 17);
+  else if (aux == 0) PCR_LAUNCH_STREAM(4, 2, 2, 0, 4, 17);
+  else if (aux == 2) PCR_LAUNCH_STREAM(4, 2, 2, 2, 4, 17);
+  else
 #endif
-  else if (uu == 4) PCR_LAUNCH_STREAM(4, 3, 4, 16);
-  else PCR_LAUNCH_STREAM(4, 3, 2, 16);
+    PCR_LAUNCH_STREAM(4, kStreamNB, 2, 16, kStreamG, kStreamNG);
 #undef PCR_LAUNCH_STREAM
   return launch_status(name);
 }
