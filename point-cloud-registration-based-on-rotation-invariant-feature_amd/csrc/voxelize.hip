@@ -1032,7 +1032,7 @@ __global__ __launch_bounds__((NS + 1) * 64) void vox_stream_kernel(int c, int n,
     // buffer stores with cache policy AUX (16 = sc1: write-through, the
     // line is not kept in the XCD's L2, so the grid stream does not evict
     // the other kernels' working sets)
-    const auto rs = __builtin_amdgcn_make_buffer_rsrc(ob, (short)0, 2 * r3 * 4, 0x00020000);
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(ob, (short)0, G * r3 * 4, 0x00020000);
 #pragma unroll
     for (int g = 0; g < G; g++) {
 #pragma unroll

@@ -61,6 +61,17 @@ def test_extractor_graph_replay(dev):
         assert torch.equal(out[key], v) or torch.allclose(out[key], v, equal_nan=True), key
 
 
+def poison(ex):
+    """Every output and workspace buffer of the extractor set to all-ones
+    bytes (NaN floats, -1 ints) before a run, so a checked result can only
+    come from that run's kernels, never from an earlier call's leftovers."""
+    import torch
+    bufs = list(ex.outputs(0).values()) + list(ex.outputs(1).values())
+    bufs += [ex.knn_ws, ex.ws] + list(ex._set(1))
+    for t in bufs:
+        t.view(-1).view(torch.uint8).fill_(0xFF)
+
+
 @pytest.mark.parametrize("schedule", [0, 1, 2])
 def test_extractor_native_runner(dev, schedule):
     """pcr_extractor_run (the bench's native multi-step enqueue): every
@@ -76,9 +87,12 @@ def test_extractor_native_runner(dev, schedule):
     for steps, timed in ((5, False), (3, True), (5, True), (1, False)):
         desc_steps = torch.empty((steps, b, c), device=dev)
         for _ in range(2):
+            poison(ex)
             out = ex.run_native(tx, tn, tf, steps, desc_steps, schedule=schedule, timed=timed)
         torch.cuda.synchronize()
         for key, v in ref.items():
+            if key == "desc":  # the runner writes each step's descriptor to desc_steps
+                continue
             assert torch.equal(out[key], v) or torch.allclose(out[key], v, equal_nan=True), \
                 (steps, key)
         for s in range(steps):

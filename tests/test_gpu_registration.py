@@ -56,10 +56,17 @@ def test_pair_step_matches_oracle(dev, p, n, c, k, r):
                           exp["match"], ("corr12", "corr21", "idx1", "idx2", "count")):
         assert np.array_equal(N(g), e), name
     # the native runner's per-step matching gives the same, every step
+    from test_gpu_extractor import poison
     for schedule in (0, 1, 2):
         desc_steps = torch.empty((4, 2 * p, c), device=dev)
+        poison(pe.ex)
+        for t in (pe.match.corr12, pe.match.corr21, pe.match.idx1, pe.match.idx2,
+                  pe.match.count):
+            t.view(-1).view(torch.uint8).fill_(0xFF)
         nat = pe.run_native(tx, tn, tf, 4, desc_steps, schedule=schedule)
         torch.cuda.synchronize()
+        for key in ("knn_idx", "ind", "cnt", "grid", "devox"):  # desc: desc_steps below
+            assert np.array_equal(N(nat[key]), exp[key]), (schedule, key)
         for g, e, name in zip((nat[x] for x in ("corr12", "corr21", "idx1", "idx2", "count")),
                               exp["match"], ("corr12", "corr21", "idx1", "idx2", "count")):
             assert np.array_equal(N(g), e), (schedule, name)
