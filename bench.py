@@ -160,6 +160,22 @@ def cpu_baseline(args):
                                                        cpu_model(), why)}
 
 
+def verify_runner(ex, xyz, nrm, feat, args, dev):
+    """Two native-runner steps with the bench's schedule vs one forward():
+    knn_idx, local_ppf, ind, cnt, grid and devox must be identical."""
+    sx = ex.ex if args.workload == "pairs" else ex
+    ref = {k: v.clone() for k, v in sx.forward(xyz, nrm, feat).items()}
+    for t in list(sx.outputs(0).values()) + list(sx.outputs(1).values()):
+        t.view(-1).view(torch.uint8).fill_(0xFF)
+    out = sx.run_native(xyz, nrm, feat, 2, None, schedule=args.schedule)
+    torch.cuda.synchronize(dev)
+    for key in ("knn_idx", "local_ppf", "ind", "cnt", "grid", "devox"):
+        if not torch.equal(out[key], ref[key]) and not torch.allclose(out[key], ref[key],
+                                                                      equal_nan=True):
+            raise SystemExit("bench: runner output %s differs from the single-step path" % key)
+    return True
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -257,6 +273,11 @@ def main():
     grid_gbs = grid_bytes / (grid_avg_ms * 1e-3) / 1e9
     kname = "vox_stream_kernel (sph-vox dense grid + cnt from the voxel means)"
 
+    # outside the timed region: the timed path's outputs are checked against
+    # the single-step (one call per stage) path on the same inputs, with every
+    # runner output poisoned first, so the number above is for complete work
+    verified = verify_runner(ex, xyz, nrm, feat, args, dev)
+
     total_clouds = b * world * args.steps
     value = total_clouds / elapsed
     step_bytes = algorithmic_bytes_per_cloud(n, k, r, c)["total"] * b
@@ -290,6 +311,7 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (seeded gaussian clouds, unit normals, U(-1,1) features)",
+        "outputs_verified": verified,
         "config": {"workload": ("sph-dg extractor forward: self-KNN k=%d + local PPF + "
                                 "sph-vox r=%d^3 + sph-devox + descriptor" % (k, r))
                    if args.workload == "extract" else
