@@ -672,12 +672,23 @@ extern "C" pcr_status pcr_local_ppf_forward(const float* points, const float* no
   PCR_REQUIRE(b >= 0 && n >= 1 && m >= 0 && u >= 0, "local_ppf_forward: invalid sizes");
   PCR_REQUIRE(u <= 65535, "local_ppf_forward: u too large");
   if (b == 0 || m == 0 || u == 0) return PCR_OK;
+  // diagnostic builds: PCR_PPF_SL = slots per thread of the LDS-staged kernel
+  // (0: the unstaged kernel)
+  static const int sl = PCR_KNOB("PCR_PPF_SL", 8);
   if (points == centers && normals == center_normals && n == m && idx_kmajor &&
-      n <= kPpfSelfMaxN) {
-    constexpr int SL = 8;
-    hipLaunchKernelGGL((local_ppf_self_kernel<SL>), dim3(ceil_div(n, 256), ceil_div(u, SL), b),
-                       dim3(256), (size_t)6 * n * 4, as_stream(stream), points, normals, idx, n,
-                       u, relative, out);
+      n <= kPpfSelfMaxN && sl != 0) {
+#define PCR_PPF_SELF(SLV)                                                                     \
+  hipLaunchKernelGGL((local_ppf_self_kernel<SLV>), dim3(ceil_div(n, 256), ceil_div(u, SLV), b), \
+                     dim3(256), (size_t)6 * n * 4, as_stream(stream), points, normals, idx, n,  \
+                     u, relative, out)
+#ifdef PCR_DIAG
+    if (sl == 16) PCR_PPF_SELF(16);
+    else if (sl == 32) PCR_PPF_SELF(32);
+    else if (sl == 4) PCR_PPF_SELF(4);
+    else
+#endif
+      PCR_PPF_SELF(8);
+#undef PCR_PPF_SELF
     return launch_status("local_ppf_forward");
   }
   hipLaunchKernelGGL(local_ppf_kernel, dim3(ceil_div(m, 256), u, b), dim3(256), 0,
