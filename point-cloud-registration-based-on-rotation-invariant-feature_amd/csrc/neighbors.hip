@@ -376,28 +376,28 @@ __global__ __launch_bounds__(256) void ball_query_kernel(const float* __restrict
 }
 
 // The same query, one wave per 64 centres (lane = centre) and NW waves per
-// workgroup, each wave scanning a contiguous quarter of the points in index
-// order.  The cloud is staged in LDS once per workgroup and read as
-// broadcast float4s (four candidates per read), the squared distances run
-// two candidates per packed instruction in the reference's contraction
-// order (pcr_sumsq3f: y*y, then +x*x, then +z*z), and every accepted point
-// is appended to the lane's u16 list of its wave in LDS.  The lists of the
-// NW waves concatenate in index order, so the first u of them, padded with
-// the first hit (0 if none), are the reference's slots; they are written
-// out row by row with coalesced stores.  (double)d2 > 1e-5 is evaluated as
-// d2 > 1e-5f: float(1e-5) lies below 1e-5, so for every float d2 the two
-// agree.
+// workgroup.  The cloud is staged in LDS once per workgroup and read as
+// broadcast float4s (four candidates per read); the squared distances run
+// two candidates per packed instruction in the reference's contraction order
+// (pcr_sumsq3f: y*y, then +x*x, then +z*z).  Each wave scans a contiguous
+// range of 32-point words and keeps, per centre, one hit bit per point: a
+// register word stored once per 32 candidates, no per-hit work.  The output
+// pass then turns every centre's bit row into its first u hit indices in
+// index order (a popcount prefix over the words, one wave per centre row),
+// padded with the first hit (0 if none): the reference's slots, whatever the
+// count of hits.  (double)d2 > 1e-5 is evaluated as d2 > 1e-5f: float(1e-5)
+// lies below 1e-5, so for every float d2 the two agree.
 constexpr int kBqWaves = 4;
 template <int NW>
-__global__ __launch_bounds__(NW * 64) void ball_query_wave_kernel(
-    const float* __restrict__ centers, const float* __restrict__ points, int m, int n, int npad,
+__global__ __launch_bounds__(NW * 64) void ball_query_mask_kernel(
+    const float* __restrict__ centers, const float* __restrict__ points, int m, int n, int nwords,
     float r2, int u, int* __restrict__ idx) {
   extern __shared__ __align__(16) unsigned char bq_s[];
+  const int npad = nwords * 32;
   float* px = (float*)bq_s;
   float* py = px + npad;
   float* pz = py + npad;
-  unsigned short* lst = (unsigned short*)(pz + npad);  // [NW][u][64]
-  __shared__ int cnt_s[NW][kWave];
+  unsigned* msk = (unsigned*)(pz + npad);  // [nwords][64]: bit i of word w = point 32 w + i
   const int b = blockIdx.y;
   const int c0 = blockIdx.x * kWave;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -416,57 +416,64 @@ __global__ __launch_bounds__(NW * 64) void ball_query_wave_kernel(
   __syncthreads();
   typedef float f2 __attribute__((ext_vector_type(2)));
   const f2 cx2 = {cx, cx}, cy2 = {cy, cy}, cz2 = {cz, cz};
-  const int q = ((npad / 4 + NW - 1) / NW) * 4;
-  const int t0 = min(npad, wv * q), t1 = min(npad, t0 + q);
-  unsigned short* my = lst + (size_t)wv * u * kWave + lane;
-  int cnt = 0;
-  for (int t = t0; t < t1; t += 4) {
-    const float4 X = *(const float4*)(px + t);
-    const float4 Y = *(const float4*)(py + t);
-    const float4 Z = *(const float4*)(pz + t);
-    f2 d[2];
+  const int wpw = (nwords + NW - 1) / NW;
+  const int w0 = min(nwords, wv * wpw), w1 = min(nwords, w0 + wpw);
+  for (int w = w0; w < w1; w++) {
+    unsigned bits = 0u;
 #pragma unroll
-    for (int h = 0; h < 2; h++) {
-      const f2 dx = cx2 - (h ? f2{X.z, X.w} : f2{X.x, X.y});
-      const f2 dy = cy2 - (h ? f2{Y.z, Y.w} : f2{Y.x, Y.y});
-      const f2 dz = cz2 - (h ? f2{Z.z, Z.w} : f2{Z.x, Z.y});
-      f2 a = dy * dy;
-      a = __builtin_elementwise_fma(dx, dx, a);
-      d[h] = __builtin_elementwise_fma(dz, dz, a);
-    }
-    const float dd[4] = {d[0][0], d[0][1], d[1][0], d[1][1]};
+    for (int t4 = 0; t4 < 32; t4 += 4) {
+      const int t = w * 32 + t4;
+      const float4 X = *(const float4*)(px + t);
+      const float4 Y = *(const float4*)(py + t);
+      const float4 Z = *(const float4*)(pz + t);
 #pragma unroll
-    for (int h = 0; h < 4; h++) {
-      if (dd[h] < r2 && dd[h] > 1e-5f && cnt < u) {
-        my[cnt * kWave] = (unsigned short)(t + h);
-        cnt++;
+      for (int h = 0; h < 2; h++) {
+        const f2 dx = cx2 - (h ? f2{X.z, X.w} : f2{X.x, X.y});
+        const f2 dy = cy2 - (h ? f2{Y.z, Y.w} : f2{Y.x, Y.y});
+        const f2 dz = cz2 - (h ? f2{Z.z, Z.w} : f2{Z.x, Z.y});
+        f2 a = dy * dy;
+        a = __builtin_elementwise_fma(dx, dx, a);
+        const f2 d = __builtin_elementwise_fma(dz, dz, a);
+        bits |= (d[0] < r2 && d[0] > 1e-5f ? 1u : 0u) << (t4 + 2 * h);
+        bits |= (d[1] < r2 && d[1] > 1e-5f ? 1u : 0u) << (t4 + 2 * h + 1);
       }
     }
+    msk[w * kWave + lane] = bits;
   }
-  cnt_s[wv][lane] = cnt;
   __syncthreads();
-  // output rows: slot s of centre `row` comes from the wave whose list
-  // covers it in the concatenation
-  for (int row = 0; row < kWave; row++) {
+  // output: one wave per centre row; lane l takes word 64 q + l of chunk q
+  for (int row = wv; row < kWave; row += NW) {
     const int jj = c0 + row;
     if (jj >= m) break;
-    int off[NW + 1];
-    off[0] = 0;
-#pragma unroll
-    for (int w = 0; w < NW; w++) off[w + 1] = off[w] + cnt_s[w][row];
-    int first = 0;
-#pragma unroll
-    for (int w = NW - 1; w >= 0; w--)
-      if (cnt_s[w][row] > 0) first = lst[(size_t)w * u * kWave + row];
     int* I = idx + ((size_t)b * m + jj) * u;
-    for (int sl = tid; sl < u; sl += NW * kWave) {
-      int v = first;
+    int base = 0, first = -1;
+    for (int q0 = 0; q0 < nwords && base < u; q0 += kWave) {
+      const int w = q0 + lane;
+      unsigned bits = w < nwords ? msk[w * kWave + row] : 0u;
+      const int pc = __popc(bits);
+      int incl = pc;
 #pragma unroll
-      for (int w = 0; w < NW; w++)
-        if (sl >= off[w] && sl < off[w + 1])
-          v = lst[((size_t)w * u + (sl - off[w])) * kWave + row];
-      I[sl] = v;
+      for (int off = 1; off < kWave; off <<= 1) {
+        const int o = __shfl_up(incl, off, kWave);
+        if (lane >= off) incl += o;
+      }
+      if (first < 0) {
+        const unsigned long long any = __ballot(bits != 0u);
+        if (any) {
+          const int l0 = __builtin_ctzll(any);
+          const unsigned b0 = __shfl(bits, l0, kWave);
+          first = (q0 + l0) * 32 + __builtin_ctz(b0);
+        }
+      }
+      int s = base + incl - pc;
+      while (bits && s < u) {
+        I[s++] = w * 32 + __builtin_ctz(bits);
+        bits &= bits - 1u;
+      }
+      base += __shfl(incl, kWave - 1, kWave);
     }
+    const int fill = first < 0 ? 0 : first;
+    for (int s = min(base, u) + lane; s < u; s += kWave) I[s] = fill;
   }
 }
 
@@ -702,13 +709,14 @@ extern "C" pcr_status pcr_ball_query(const float* centers, const float* points, 
   PCR_REQUIRE(b >= 0 && m >= 0 && n >= 0 && u >= 1, "ball_query: invalid sizes");
   if (b == 0 || m == 0) return PCR_OK;
   const float r2 = radius * radius;  // ball_query.cpp:24 (float * float)
-  const int npad = (n + 3) / 4 * 4;
-  const size_t smem = (size_t)npad * 12 + (size_t)kBqWaves * u * kWave * 2;
-  if (n >= 1 && n <= 65535 && smem <= 96 * 1024) {
-    allow_big_lds(ball_query_wave_kernel<kBqWaves>, smem);
-    hipLaunchKernelGGL(ball_query_wave_kernel<kBqWaves>, dim3(ceil_div(m, kWave), b),
+  const int nwords = (n + 31) / 32;
+  // staged cloud (12 B per point) + hit bits (64 centres x 1 bit per point)
+  const size_t smem = (size_t)nwords * 32 * 12 + (size_t)nwords * kWave * 4;
+  if (n >= 1 && smem <= 96 * 1024) {
+    allow_big_lds(ball_query_mask_kernel<kBqWaves>, smem);
+    hipLaunchKernelGGL(ball_query_mask_kernel<kBqWaves>, dim3(ceil_div(m, kWave), b),
                        dim3(kBqWaves * kWave), smem, as_stream(stream), centers, points, m, n,
-                       npad, r2, u, idx);
+                       nwords, r2, u, idx);
   } else {
     hipLaunchKernelGGL(ball_query_kernel, dim3(ceil_div(m, 256), b), dim3(256), 0,
                        as_stream(stream), centers, points, m, n, r2, u, idx);

@@ -301,10 +301,11 @@ def test_sph_devox_backward_irregular_corners(dev):
     (2, 513, 2048, 0.2, 128, 0.35),    # c3 per-cloud size, ragged centre count
     (1, 64, 77, 0.9, 200, 0.35),       # u > n: padding with the first hit
     (1, 100, 300, 0.05, 8, 1.0),       # sparse: many centres with no hit (all-0 rows)
-    (2, 256, 9000, 0.3, 64, 0.35),     # beyond the u16 / LDS fast path: the scan kernel
+    (2, 300, 4000, 0.3, 128, 0.35),    # near the hit-bit kernel's LDS limit (~4.9k points)
+    (2, 256, 9000, 0.3, 64, 0.35),     # beyond the hit-bit kernel's LDS budget: the scan kernel
 ])
 def test_ball_query_paths(dev, b, m, n, radius, u, scale):
-    """pcr_ball_query's wave kernel (and the per-centre scan past its LDS
+    """pcr_ball_query's hit-bit kernel (and the per-centre scan past its LDS
     budget) against ball_query.cu:30-49 as the oracle restates it."""
     from pcr_amd import ops
     rng = np.random.default_rng(m + n + u)
