@@ -775,6 +775,7 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
   unsigned* hist_s = (unsigned*)sel_u;
   kkey* buf_s = (kkey*)sel_u;
   __shared__ unsigned dest_s[kBlk];
+  __shared__ unsigned cut_s[2 + NG][kBlk];  // wave 0's cut: bin, count, wave fields
   __shared__ __align__(16) float cand_s[CL ? 3 * CACHE : 4];  // x | y | z
   __shared__ __align__(16) int cand_j[CL ? CACHE : 4];
   __shared__ __align__(16) float cand_w[CL ? 1 : NW][CL ? 4 : 3 * kBlk];  // a block per wave
@@ -1058,26 +1059,42 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     });
     __syncthreads();
     PCR_STAMP(2);
+    // wave 0 finds the cut of the 64 queries (the other waves would repeat
+    // the same sweep) and hands it over through LDS
     unsigned cum[NG], cut[NG];
 #pragma unroll
     for (int g = 0; g < NG; g++) cum[g] = cut[g] = 0u;
-    bstar = -1;
-    total = 0;
+    if (wv == 0) {
+      bstar = -1;
+      total = 0;
+      for (int b0 = 0; b0 < kNB; b0 += 4) {
 #pragma unroll
-    for (int bin = 0; bin < kNB; bin++) {
-      int tb = 0;
+        for (int bin = b0; bin < b0 + 4; bin++) {
+          int tb = 0;
 #pragma unroll
-      for (int g = 0; g < NG; g++) {
-        cum[g] += hist_s[(g * (kNB + 1) + bin) * kBlk + lane];
-        tb += (int)field_sum<CB>(cum[g]);
+          for (int g = 0; g < NG; g++) {
+            cum[g] += hist_s[(g * (kNB + 1) + bin) * kBlk + lane];
+            tb += (int)field_sum<CB>(cum[g]);
+          }
+          if (bstar < 0 && tb >= k) {
+            bstar = bin;
+            total = tb;
+#pragma unroll
+            for (int g = 0; g < NG; g++) cut[g] = cum[g];
+          }
+        }
+        if (__all(bstar >= 0)) break;
       }
-      if (bstar < 0 && tb >= k) {
-        bstar = bin;
-        total = tb;
+      cut_s[0][lane] = (unsigned)bstar;
+      cut_s[1][lane] = (unsigned)total;
 #pragma unroll
-        for (int g = 0; g < NG; g++) cut[g] = cum[g];
-      }
+      for (int g = 0; g < NG; g++) cut_s[2 + g][lane] = cut[g];
     }
+    __syncthreads();
+    bstar = (int)cut_s[0][lane];
+    total = (int)cut_s[1][lane];
+#pragma unroll
+    for (int g = 0; g < NG; g++) cut[g] = cut_s[2 + g][lane];
     // slots of the waves before this one
     const int mg = wv / FPD;
     const unsigned below = (1u << ((wv % FPD) * CB)) - 1u;
