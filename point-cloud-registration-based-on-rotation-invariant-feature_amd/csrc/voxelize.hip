@@ -871,9 +871,9 @@ __global__ __launch_bounds__(kMeansNT) void vox_means_kernel(
 //    third buffer while the streamers store item t.  Under the write stream
 //    a load round trip takes microseconds; with two items of slack it never
 //    holds a barrier.  The barriers wait for LDS operations only.
-constexpr int kStreamG = 4;      // channels per item
-constexpr int kStreamNG = 17;    // 1 KB LDS-DMA pieces per item: four rows of ms <= 1088 floats
-constexpr int kStreamNB = 2;     // means buffers (item t streams, t+1 landing)
+constexpr int kStreamG = 2;      // channels per item
+constexpr int kStreamNG = 9;     // 1 KB LDS-DMA pieces per item: two rows of ms <= 1152 floats
+constexpr int kStreamNB = 3;     // means buffers (item t streams, t+1 ready, t+2 landing)
 constexpr int kStreamMaxN = 1024;
 constexpr int kStreamMaxW = 1024;  // occupancy words (r^3 <= 32768)
 
@@ -1765,11 +1765,14 @@ extern "C" pcr_status pcr_extractor_voxel_stream(int b, int c, int n, int r, int
               kStreamMaxN, 32 * kStreamMaxW);
   // channels per item G (one occupancy / segment-index computation per G
   // stores) and means buffers NB; diagnostic builds can pick other shapes
-  static const int gk = PCR_KNOB("PCR_STREAM_G", 4);
-  static const int nbk = PCR_KNOB("PCR_STREAM_NB", 2);
-  const int G = gk == 8 ? 8 : gk == 2 ? 2 : 4;
-  const int NGP = G == 8 ? 33 : G == 4 ? 17 : 9;  // 1 KB pieces: G rows of ms <= 1024 G / ... floats
-  const int NB = (G == 4 && nbk == 3) ? 3 : G == 2 ? 3 : kStreamNB;
+  // (two channels and three buffers: 36 KB, so the grid kernel fits on a CU
+  // beside two selection workgroups; four channels per item measured ~3%
+  // slower in the step despite half the index work per store)
+  static const int gk = PCR_KNOB("PCR_STREAM_G", kStreamG);
+  static const int nbk = PCR_KNOB("PCR_STREAM_NB", 0);
+  const int G = gk == 8 ? 8 : gk == 4 ? 4 : 2;
+  const int NGP = G == 8 ? 33 : G == 4 ? 17 : 9;  // 1 KB pieces holding G rows of ms floats
+  const int NB = G == 2 ? kStreamNB : (G == 4 && nbk == 3) ? 3 : 2;
   PCR_REQUIRE(G * ws.ms * 4 <= NGP * 1024, "%s: means rows too long", name);
   const int ngrp = ceil_div(c, G);
   // a few workgroups per cloud (about one per CU in all), each a contiguous
@@ -1795,11 +1798,11 @@ extern "C" pcr_status pcr_extractor_voxel_stream(int b, int c, int n, int r, int
                        ngrp, wpc, per, dbg);                                                  \
   } while (0)
 #ifdef PCR_DIAG
-  if (G == 2) PCR_LAUNCH_STREAM(4, 3, 2, 16, 2, 9);
+  if (G == 4 && NB == 3) PCR_LAUNCH_STREAM(4, 3, 2, 16, 4, 17);
+  else if (G == 4) PCR_LAUNCH_STREAM(4, 2, 2, 16, 4, 17);
   else if (G == 8) PCR_LAUNCH_STREAM(4, 2, 2, 16, 8, 33);
-  else if (NB == 3) PCR_LAUNCH_STREAM(4, 3, 2, 16, 4, 17);
-  else if (aux == 0) PCR_LAUNCH_STREAM(4, 2, 2, 0, 4, 17);
-  else if (aux == 2) PCR_LAUNCH_STREAM(4, 2, 2, 2, 4, 17);
+  else if (aux == 0) PCR_LAUNCH_STREAM(4, 3, 2, 0, 2, 9);
+  else if (aux == 2) PCR_LAUNCH_STREAM(4, 3, 2, 2, 2, 9);
   else
 #endif
     PCR_LAUNCH_STREAM(4, kStreamNB, 2, 16, kStreamG, kStreamNG);
