@@ -709,7 +709,7 @@ constexpr int kNB = 24;
 constexpr int kCap = 88;
 constexpr int kSelCache = 1024;  // candidates staged in LDS per workgroup
 constexpr int kSelMaxK = 32;
-constexpr int kCap64 = 176;  // the same selection for 32 < k <= 64 (large clouds)
+constexpr int kCap64 = 112;  // the same selection for 32 < k <= 64 (large clouds): two workgroups per CU
 constexpr int kSelMaxK64 = 64;
 
 typedef float pf2 __attribute__((ext_vector_type(2)));
@@ -1006,7 +1006,19 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
   // 1. bound
   {
     float dq = __builtin_inff();
-    if (breg) {
+    // a self KNN over many blocks takes its bound from the blocks within
+    // kBoundWin of the query block in Morton order (any block of >= k points
+    // bounds kth, so fewer blocks only loosen the bound; the box nearest a
+    // query is almost always there): the boxes are read by scalar loads, not
+    // one readlane sweep over all of this wave's blocks
+    constexpr int kBoundWin = 64;
+    if (!CL && qs.x == cs.x && nblk > 2 * kBoundWin + NW) {
+      const int lo = max(0, qblk - kBoundWin), hi = min(nblk - 1, qblk + kBoundWin);
+      for (int blk = lo + wv; blk <= hi; blk += NW) {
+        const int real = min(kBlk, m - blk * kBlk);
+        if (real >= k) dq = fminf(dq, box_ub(qx, qy, qz, boxes + (size_t)blk * 8));
+      }
+    } else if (breg) {
       for_blocks([&](int blk, const float (&b6)[6]) {
         const int real = min(kBlk, m - blk * kBlk);
         if (real >= k) dq = fminf(dq, box_ub(qx, qy, qz, b6));
