@@ -96,6 +96,43 @@ __device__ inline void latency_kernel_priority() {
 #endif
 }
 
+// Diagnostic builds: per-kernel issue priorities from the environment
+// (PCR_PRIO_<slot>=0..3, slot 0 sort, 1 select, 2 PPF, 3 prep, 4 means,
+// 5 grid stream; -1 = the product's choice).  Each translation unit keeps its
+// own copy of the table and loads it before its first launch.
+#ifdef PCR_DIAG
+static __device__ int pcr_prio_tab[8];
+static inline void diag_prio_init() {
+  static bool done = false;
+  if (done) return;
+  done = true;
+  int t[8];
+  char name[32];
+  for (int i = 0; i < 8; i++) {
+    snprintf(name, sizeof(name), "PCR_PRIO_%d", i);
+    t[i] = getenv(name) ? atoi(getenv(name)) : -1;
+  }
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(pcr_prio_tab), t, sizeof(t));
+}
+// returns true when the environment overrides this slot's priority
+__device__ inline bool diag_prio(int slot) {
+  const int p = __builtin_amdgcn_readfirstlane(pcr_prio_tab[slot]);
+  if (p < 0) return false;
+  if (p == 0) __builtin_amdgcn_s_setprio(0);
+  else if (p == 1) __builtin_amdgcn_s_setprio(1);
+  else if (p == 2) __builtin_amdgcn_s_setprio(2);
+  else __builtin_amdgcn_s_setprio(3);
+  return true;
+}
+#define PCR_PRIO_INIT() diag_prio_init()
+#define PCR_PRIO(slot) diag_prio(slot)
+#else
+#define PCR_PRIO_INIT() \
+  do {                  \
+  } while (0)
+#define PCR_PRIO(slot) false
+#endif
+
 // Workgroup barrier that orders LDS only.  __syncthreads() also waits for the
 // thread's outstanding global stores (vmcnt(0)) before the barrier, so a
 // barrier after a burst of global writes stalls on their completion; this one

@@ -68,6 +68,11 @@ pcr_status knn_select_ppf(const pcr_extractor_args* a, int q, bool sorted, hipSt
   if (!sorted)  // no sorted path: the one-call selection + PPF
     return pcr_knn_local_ppf(a->xyz, a->normals, a->b, a->n, a->k, a->relative, a->knn_idx,
                              a->knn_dist, a->local_ppf, a->knn_ws[q], a->knn_ws_bytes, st);
+  static const int fuse = PCR_KNOB("PCR_RUN_FUSE", 0);
+  if (fuse)  // diagnostic: the PPF in the selection's epilogue
+    return pcr_knn_local_ppf_prepared(a->xyz, a->normals, a->b, a->n, a->k, a->relative,
+                                      a->knn_idx, a->knn_dist, a->local_ppf, a->knn_ws[q],
+                                      a->knn_ws_bytes, st);
   PCR_TRY(pcr_knn_local_ppf_prepared(a->xyz, a->normals, a->b, a->n, a->k, a->relative,
                                        a->knn_idx, a->knn_dist, nullptr, a->knn_ws[q],
                                        a->knn_ws_bytes, st));

@@ -102,7 +102,7 @@ __global__ __launch_bounds__(NT) void knn_sort_kernel(const float* __restrict__ 
   extern __shared__ __align__(16) unsigned long long keys[];  // [npad_sort]
   __shared__ float red[6][NT / kWave];
   __shared__ float frame[6];
-  latency_kernel_priority();
+  if (!PCR_PRIO(0)) latency_kernel_priority();
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
   const int E = npad_sort / NT;
@@ -779,6 +779,7 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
   __shared__ __align__(16) float cand_s[CL ? 3 * CACHE : 4];  // x | y | z
   __shared__ __align__(16) int cand_j[CL ? CACHE : 4];
   __shared__ __align__(16) float cand_w[CL ? 1 : NW][CL ? 4 : 3 * kBlk];  // a block per wave
+  (void)PCR_PRIO(1);
   const int b = blockIdx.y;
   const int qblk = blockIdx.x;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1342,6 +1343,7 @@ static void launch_select(const KnnSet& qs, const KnnSet& cs, int b, int k, floa
                           int* idx, const float* qxyz, const float* qnrm, const float* cxyz,
                           const float* cnrm, int relative, float* ppf, hipStream_t st) {
   // a wave sees ceil(nblk / NW) * 64 candidates: byte fields when that fits
+  PCR_PRIO_INIT();
   const int per_wave = ceil_div(cs.nblk, NW) * kBlk;
   const dim3 grid(qs.nblk, b), blk(NW * 64);
 #define PCR_SEL(CBV, CLV, CACHEV)                                                             \
@@ -1375,6 +1377,7 @@ static int next_pow2i(int v) {
 }
 
 static void launch_sort(const float* pts, int b, int n, const KnnSet& s, hipStream_t st) {
+  PCR_PRIO_INIT();
   if (n > kKnnMaxSortN) {
     hipLaunchKernelGGL(knn_big_frame_kernel, dim3(b), dim3(kSortBlock), 0, st, pts, n, s);
     hipLaunchKernelGGL(knn_big_count_kernel, dim3(ceil_div(n, 256), b), dim3(256), 0, st, pts, n,

@@ -277,6 +277,7 @@ __global__ __launch_bounds__(256) void local_ppf_self_kernel(const float* __rest
                                                              int k, int relative,
                                                              float* __restrict__ out) {
   extern __shared__ __align__(16) float cl_s[];  // [6][n]: x y z nx ny nz
+  (void)PCR_PRIO(2);
   const int tid = threadIdx.x;
   const int j = blockIdx.x * 256 + tid;
   const int q0 = blockIdx.y * SL;
@@ -682,6 +683,7 @@ extern "C" pcr_status pcr_local_ppf_forward(const float* points, const float* no
   // diagnostic builds: PCR_PPF_SL = slots per thread of the LDS-staged kernel
   // (0: the unstaged kernel)
   static const int sl = PCR_KNOB("PCR_PPF_SL", 8);
+  PCR_PRIO_INIT();
   if (points == centers && normals == center_normals && n == m && idx_kmajor &&
       n <= kPpfSelfMaxN && sl != 0) {
 #define PCR_PPF_SELF(SLV)                                                                     \

@@ -175,7 +175,7 @@ __global__ __launch_bounds__(NT) void vox_prep_kernel(
   __shared__ float s_stat[4];
   __shared__ int s_flag;  // a crowded voxel: the bitonic path
 
-  if (prio) latency_kernel_priority();
+  if (!PCR_PRIO(3) && prio) latency_kernel_priority();
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
   constexpr int nt = NT;
@@ -731,6 +731,7 @@ __global__ __launch_bounds__(kMeansNT) void vox_means_kernel(
   // a batch of a multiple of 8 clouds XCD x runs every channel group of
   // clouds x, x + 8, ...: a cloud's corner data and point order (read by all
   // its channel groups) fill one XCD's L2 instead of all eight
+  (void)PCR_PRIO(4);
   const int nb = gridDim.x / ngrp;
   const int b = (nb & 7) ? blockIdx.x / ngrp : (blockIdx.x & 7) + 8 * ((blockIdx.x >> 3) / ngrp);
   const int grp = (nb & 7) ? blockIdx.x % ngrp : (blockIdx.x >> 3) % ngrp;
@@ -910,6 +911,7 @@ __global__ __launch_bounds__((NS + 1) * 64) void vox_stream_kernel(int c, int n,
   unsigned* bm_s = (unsigned*)(smem_raw + NB * BUFB);              // [W]
   unsigned short* pre_s = (unsigned short*)(bm_s + W);             // [W]
   unsigned short* scnt_s = pre_s + W;                              // [ms -> 256 B], slot n = 0
+  (void)PCR_PRIO(5);
   const int b = blockIdx.x / wpc;
   const int j0 = (blockIdx.x % wpc) * per;
   const int nit = min(ngrp, j0 + per) - j0;
@@ -1528,6 +1530,7 @@ static pcr_status run_voxelize(const float* features, const float* coords_f, con
   size_t need = vox_ws_layout(b, n, r, &ws, workspace);
   PCR_REQUIRE(workspace != nullptr && ws_bytes >= need, "%s: workspace too small (%zu < %zu)",
               name, ws_bytes, need);
+  PCR_PRIO_INIT();
   if (what & 1) {
     // clouds of <= 1024 points: 256 threads (four points each), so a prep
     // workgroup fits on a CU beside the other stream's KNN selection instead
@@ -1691,6 +1694,7 @@ extern "C" pcr_status pcr_extractor_voxel_means_devox(const float* features, int
                                                       void* workspace, size_t workspace_bytes,
                                                       void* stream) {
   const char* name = "extractor_voxel_means_devox";
+  PCR_PRIO_INIT();
   VoxWs ws;
   pcr_status rc = extractor_ws(b, c, n, r, workspace, workspace_bytes, &ws, name);
   if (rc != PCR_OK) return rc;
@@ -1754,6 +1758,7 @@ extern "C" pcr_status pcr_extractor_voxel_stream(int b, int c, int n, int r, int
                                                  float* grid, void* workspace,
                                                  size_t workspace_bytes, void* stream) {
   const char* name = "extractor_voxel_stream";
+  PCR_PRIO_INIT();
   VoxWs ws;
   pcr_status rc = extractor_ws(b, c, n, r, workspace, workspace_bytes, &ws, name);
   if (rc != PCR_OK) return rc;

@@ -4,7 +4,7 @@
 # signal or timeout (anything else non-zero) stops the script: nothing more
 # touches the GPU after a fault.
 #   usage: scripts/gpu_steps.sh <step> [<step> ...]
-#   steps: smoke tests tests_all large c5 bench modes prof pmc
+#   steps: smoke tests tests_all large c5 bench bench_drv prof pmc
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
@@ -25,12 +25,7 @@ for step in "$@"; do
     tests) run pytest_gpu 1200 python -m pytest tests -x -q -m gpu -p no:cacheprovider ;;
     tests_all) run pytest_gpu 1200 python -m pytest tests -q -m gpu -p no:cacheprovider ;;
     bench) run bench 600 python bench.py ;;
-    modes) run bench_psv 300 python bench.py --mode pipelined_sv --no-cpu-baseline
-           run bench_p3 300 python bench.py --mode pipelined3 --no-cpu-baseline
-           run bench_p4 300 python bench.py --mode pipelined4 --no-cpu-baseline
-
-           run bench_graph 300 python bench.py --mode graph --no-cpu-baseline
-           run bench_eager 300 python bench.py --mode eager --no-cpu-baseline ;;
+    bench_drv) run bench_drv 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
     prof) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
           run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 80 --warmup 40 --no-cpu-baseline ;;
     pmc)  run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 5 --warmup 5 --steps-per-launch 5 --kernel-iters 5 --no-cpu-baseline
