@@ -217,7 +217,9 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
                                            a->vox_ws[q], a->vox_ws_bytes, sv));
       if (s < rn->timed_cap) PCR_HIP(hipEventRecord(rn->t1[s], sv), "timing record");
       if (!(skip & 128)) PCR_HIP(hipEventRecord(stream_done[q], sv), "stream record");
-      if (!(warm && (skip & 32))) PCR_TRY(knn_sort(a, 0, sn, &sorted));
+      // 1024: sort and PPF on `origin` with no waits (the selection alone on
+      // s_nbr; timing only, breaks the ordering)
+      if (!(warm && (skip & 32))) PCR_TRY(knn_sort(a, 0, (skip & 1024) && warm ? org : sn, &sorted));
       else sorted = true;
       if (!(skip & 1))
         PCR_TRY(pcr_knn_local_ppf_prepared(a->xyz, a->normals, a->b, a->n, a->k, a->relative,
@@ -225,7 +227,7 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
                                            a->knn_ws_bytes, sn));
       // 512: the PPF on `origin` after the selection's event (timing only:
       // the next selection may overwrite the indices it reads)
-      hipStream_t sppf = sn;
+      hipStream_t sppf = (skip & 1024) && warm ? org : sn;
       if (skip & 512) {
         PCR_HIP(hipEventRecord(sel_done[q], sn), "select record");
         PCR_HIP(hipStreamWaitEvent(org, sel_done[q], 0), "select wait");

@@ -776,8 +776,12 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
   kkey* buf_s = (kkey*)sel_u;
   __shared__ unsigned dest_s[kBlk];
   __shared__ unsigned cut_s[2 + NG][kBlk];  // wave 0's cut: bin, count, wave fields
+  // cached clouds: the Morton-sorted candidates (the near ones of a query
+  // block cluster in a few groups, so few groups are collected) and their
+  // point ids as u16, read with the coordinates: the collect pass never
+  // waits on an LDS read inside its sweep
   __shared__ __align__(16) float cand_s[CL ? 3 * CACHE : 4];  // x | y | z
-  __shared__ __align__(16) int cand_j[CL ? CACHE : 4];
+  __shared__ __align__(16) unsigned short cand_j[CL ? CACHE : 8];
   __shared__ __align__(16) float cand_w[CL ? 1 : NW][CL ? 4 : 3 * kBlk];  // a block per wave
   (void)PCR_PRIO(1);
   const int b = blockIdx.y;
@@ -800,7 +804,7 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     const int np = cs.npad;
     for (int i = threadIdx.x; i < np; i += NW * kBlk) {
       cand_s[i] = cs.x[cbase + i];
-      cand_j[i] = cs.j[cbase + i];
+      cand_j[i] = (unsigned short)cs.j[cbase + i];
       cand_s[CACHE + i] = cs.y[cbase + i];
       cand_s[2 * CACHE + i] = cs.z[cbase + i];
     }
@@ -845,7 +849,8 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     }
   };
   int cj_cur = 0;  // original index of candidate `lane` of the block in process
-  auto visit = [&](float lim, auto&& f) {
+  auto visit = [&](float lim, auto want_j, auto&& f) {
+    constexpr bool WANT_J = decltype(want_j)::value;
     if (CL) {
       constexpr int S = kBlk / NW;
       constexpr int GPB = S / 4;
@@ -854,15 +859,19 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
       // one block (two groups) per half iteration; positions advance by a
       // constant, so every read is one base register plus an immediate.
       // Reads past the last block land in the next LDS array (never used).
-      auto rd = [&](int o, float4 (&X)[2], float4 (&Y)[2], float4 (&Z)[2]) {
+      // the ids of the wave's 8 candidates (u16) are read with them only
+      // when the callback uses them (the collect pass)
+      auto rd = [&](int o, float4 (&X)[2], float4 (&Y)[2], float4 (&Z)[2], uint4& J) {
 #pragma unroll
         for (int h = 0; h < 2; h++) {
           X[h] = *(const float4*)(cand_s + o + 4 * h);
           Y[h] = *(const float4*)(cand_s + CACHE + o + 4 * h);
           Z[h] = *(const float4*)(cand_s + 2 * CACHE + o + 4 * h);
         }
+        if (WANT_J) J = *(const uint4*)(cand_j + o);
       };
-      auto eval = [&](int o, const float4 (&X)[2], const float4 (&Y)[2], const float4 (&Z)[2]) {
+      auto eval = [&](int o, const float4 (&X)[2], const float4 (&Y)[2], const float4 (&Z)[2],
+                      const uint4& J) {
 #pragma unroll
         for (int h = 0; h < 2; h++) {
           const pf2 d0 = cand_dist2(qx2, qy2, qz2, pf2{X[h].x, X[h].y}, pf2{Y[h].x, Y[h].y},
@@ -870,21 +879,22 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
           const pf2 d1 = cand_dist2(qx2, qy2, qz2, pf2{X[h].z, X[h].w}, pf2{Y[h].z, Y[h].w},
                                     pf2{Z[h].z, Z[h].w});
           const float d[4] = {d0[0], d0[1], d1[0], d1[1]};
-          f(o + 4 * h, d);
+          f(o + 4 * h, d, h == 0 ? uint2{J.x, J.y} : uint2{J.z, J.w});
         }
       };
       // ping-pong register sets A / B, no copies: B's reads are issued
       // before A's evaluation (and its LDS atomics / stores) and vice versa
       float4 AX[2], AY[2], AZ[2], BX[2], BY[2], BZ[2];
+      uint4 AJ = {0u, 0u, 0u, 0u}, BJ = {0u, 0u, 0u, 0u};
       int o = wv * S;
-      rd(o, AX, AY, AZ);
+      rd(o, AX, AY, AZ, AJ);
       for (int blk = 0; blk < nblk; blk += 2, o += 2 * kBlk) {
-        rd(o + kBlk, BX, BY, BZ);
+        rd(o + kBlk, BX, BY, BZ, BJ);
         __builtin_amdgcn_sched_barrier(0);  // reads first, then A's (older) data is waited on
-        eval(o, AX, AY, AZ);
-        rd(o + 2 * kBlk, AX, AY, AZ);
+        eval(o, AX, AY, AZ, AJ);
+        rd(o + 2 * kBlk, AX, AY, AZ, AJ);
         __builtin_amdgcn_sched_barrier(0);
-        if (blk + 1 < nblk) eval(o + kBlk, BX, BY, BZ);
+        if (blk + 1 < nblk) eval(o + kBlk, BX, BY, BZ, BJ);
       }
     } else if (breg) {
       // which of this wave's blocks does any query lane need?  Lane l tests
@@ -961,7 +971,7 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
           const pf2 d0 = cand_dist2(qx2, qy2, qz2, pf2{X.x, X.y}, pf2{Y.x, Y.y}, pf2{Z.x, Z.y});
           const pf2 d1 = cand_dist2(qx2, qy2, qz2, pf2{X.z, X.w}, pf2{Y.z, Y.w}, pf2{Z.z, Z.w});
           const float d[4] = {d0[0], d0[1], d1[0], d1[1]};
-          f(cur * kBlk + t, d);
+          f(cur * kBlk + t, d, uint2{0u, 0u});
         }
         cur = nxt;
       }
@@ -980,14 +990,14 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
           const pf2 d0 = cand_dist2(qx2, qy2, qz2, pf2{X.x, X.y}, pf2{Y.x, Y.y}, pf2{Z.x, Z.y});
           const pf2 d1 = cand_dist2(qx2, qy2, qz2, pf2{X.z, X.w}, pf2{Y.z, Y.w}, pf2{Z.z, Z.w});
           const float d[4] = {d0[0], d0[1], d1[0], d1[1]};
-          f(blk * kBlk + t, d);
+          f(blk * kBlk + t, d, uint2{0u, 0u});
         }
       }
     }
   };
   // original indices of the four candidates at sorted position pos
   auto cand_idx4 = [&](int pos) {
-    if (CL) return *(const int4*)(cand_j + pos);
+    if (CL) return int4{0, 0, 0, 0};  // unused: the cached path passes its ids to the callback
     if (breg) {
       const int t = pos & (kBlk - 1);
       return int4{__builtin_amdgcn_readlane(cj_cur, t), __builtin_amdgcn_readlane(cj_cur, t + 1),
@@ -1062,7 +1072,7 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     unsigned* hwb = hw - base * kBlk;
     const int top = base + kNB;
     const int sh = shift;
-    visit(lim, [&](int, const float (&d)[4]) {
+    visit(lim, std::false_type(), [&](int, const float (&d)[4], uint2) {
 #pragma unroll
       for (int h = 0; h < 4; h++) {
         const int e = med3_i32((int)(__float_as_uint(d[h]) >> sh), base, top);
@@ -1151,13 +1161,15 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
   if (!fallback) {
     // 4. collect
     const float fcut = __uint_as_float(ucut);
-    visit(fcut, [&](int pos, const float (&d)[4]) {
+    visit(fcut, std::true_type(), [&](int pos, const float (&d)[4], uint2 jp) {
       bool take[4];
 #pragma unroll
       for (int h = 0; h < 4; h++) take[h] = __float_as_uint(d[h]) < ucut;
       // most groups of four are taken by no lane: skip them uniformly
       if (__any(take[0] | take[1] | take[2] | take[3])) {
-        const int4 jj = cand_idx4(pos);
+        const int4 jj = CL ? int4{(int)(jp.x & 0xFFFFu), (int)(jp.x >> 16), (int)(jp.y & 0xFFFFu),
+                                  (int)(jp.y >> 16)}
+                           : cand_idx4(pos);
         const int j4[4] = {jj.x, jj.y, jj.z, jj.w};
 #pragma unroll
         for (int h = 0; h < 4; h++) {
@@ -1296,9 +1308,10 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     const float* bx = CL ? cand_s + blk * kBlk : cs.x + cbase + (size_t)blk * kBlk;
     const float* by = CL ? cand_s + CACHE + blk * kBlk : cs.y + cbase + (size_t)blk * kBlk;
     const float* bz = CL ? cand_s + 2 * CACHE + blk * kBlk : cs.z + cbase + (size_t)blk * kBlk;
-    const int* bj = CL ? cand_j + blk * kBlk : cs.j + cbase + (size_t)blk * kBlk;
+    const int* bj = cs.j + cbase + (size_t)blk * kBlk;
     for (int t = 0; t < kBlk; t++) {
-      const kkey x = make_key(cand_dist(qx, qy, qz, bx[t], by[t], bz[t]), bj[t]);
+      const kkey x = make_key(cand_dist(qx, qy, qz, bx[t], by[t], bz[t]),
+                              CL ? (int)cand_j[blk * kBlk + t] : bj[t]);
       if (x < kth) {
         int s2 = k - 1;
         while (s2 > 0) {
