@@ -273,6 +273,11 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
         PCR_HIP(hipEventRecord(sel_done[q], sn), "select record");
       }
     } else {
+      // the first step's neighbour stream starts after that step's voxel
+      // means: prep + means (the grid stream's chain) get the chip first, so
+      // the grid stream starts ~1/3 sooner (a 20-step call: 289k -> 298k
+      // clouds/s; long runs unchanged)
+      if (s == 0) PCR_HIP(hipStreamWaitEvent(sn, means_done[q], 0), "head wait");
       PCR_TRY(knn_sort(a, 0, sn, &sorted));
       PCR_TRY(knn_select_ppf(a, 0, sorted, sn));
     }

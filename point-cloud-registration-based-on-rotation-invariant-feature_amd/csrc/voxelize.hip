@@ -1794,6 +1794,7 @@ extern "C" pcr_status pcr_extractor_voxel_stream(int b, int c, int n, int r, int
                       ((size_t)ws.ms * 2 + 255) / 256 * 256;
 #ifdef PCR_DIAG
   static const int aux = PCR_KNOB("PCR_STREAM_AUX", 16);  // store cache policy experiments
+  static const int nsk = PCR_KNOB("PCR_STREAM_NS", 4);    // streamer waves per workgroup
 #endif
 #define PCR_LAUNCH_STREAM(NSV, NBV, UV, AV, GV, NGV)                                           \
   do {                                                                                        \
@@ -1808,6 +1809,8 @@ extern "C" pcr_status pcr_extractor_voxel_stream(int b, int c, int n, int r, int
   else if (G == 8) PCR_LAUNCH_STREAM(4, 2, 2, 16, 8, 33);
   else if (aux == 0) PCR_LAUNCH_STREAM(4, 3, 2, 0, 2, 9);
   else if (aux == 2) PCR_LAUNCH_STREAM(4, 3, 2, 2, 2, 9);
+  else if (nsk == 2) PCR_LAUNCH_STREAM(2, 3, 2, 16, 2, 9);
+  else if (nsk == 8) PCR_LAUNCH_STREAM(8, 3, 2, 16, 2, 9);
   else
 #endif
     PCR_LAUNCH_STREAM(4, kStreamNB, 2, 16, kStreamG, kStreamNG);

@@ -7,7 +7,7 @@ L=$PWD/point-cloud-registration-based-on-rotation-invariant-feature_amd/lib
 lib=$1; shift
 for rnd in 1 2; do
   for envs in "$@"; do
-    v=$(env $envs PCR_AMD_LIB=$L/$lib.so timeout -k 10 120 python bench.py --no-cpu-baseline --no-verify \
+    v=$(env $envs PCR_AMD_LIB=$L/$lib.so timeout -k 10 120 python bench.py --no-cpu-baseline --no-verify $BENCH_ARGS \
         2>/dev/null | grep -o '"value": [0-9.]*')
     rc=$?
     echo "$lib [$envs] $v"
