@@ -349,13 +349,17 @@ pcr_status pcr_read_xyzn_txt(const char *path, float *out, long long rows, int c
  * pcr_runner_create on the current device and reused by every call (NULL:
  * transient events for this call only).  With timed_steps > 0 the runner
  * also brackets the grid-stream kernel (pcr_extractor_voxel_stream) of the
- * first timed_steps steps of each run with timing events on its stream;
+ * last min(steps, timed_steps) steps of each run (pipeline full; fewer after
+ * pcr_runner_set_timed) with timing events on its stream;
  * pcr_runner_grid_times waits for them and returns the per-step durations
  * (ms) of the last run -- the dominant kernel's in-step duration. */
 typedef struct pcr_runner pcr_runner;
 pcr_status pcr_runner_create(int timed_steps, pcr_runner **out);
 void pcr_runner_destroy(pcr_runner *runner);
 pcr_status pcr_runner_grid_times(pcr_runner *runner, float *ms, int cap, int *count);
+/* steps timed by each later run (0..timed_steps of pcr_runner_create; the
+ * default is all of them) */
+pcr_status pcr_runner_set_timed(pcr_runner *runner, int timed_steps);
 typedef struct pcr_extractor_args {
   int b, n, c, k, r, relative;
   const float *xyz, *normals, *features;  /* [b,3,n], [b,3,n], [b,c,n] */

@@ -26,6 +26,7 @@ struct pcr_runner {
   hipEvent_t* t0 = nullptr;       // [timed_cap] before each grid launch
   hipEvent_t* t1 = nullptr;       // [timed_cap] after it
   int timed_last = 0;             // pairs recorded by the last run
+  int timed_want = 0;             // steps each run times (<= timed_cap)
   ~pcr_runner() {
     for (hipEvent_t e : sync)
       if (e) (void)hipEventDestroy(e);
@@ -113,6 +114,7 @@ extern "C" pcr_status pcr_runner_create(int timed_steps, pcr_runner** out) {
     rn->t0 = new hipEvent_t[timed_steps]();
     rn->t1 = new hipEvent_t[timed_steps]();
     rn->timed_cap = timed_steps;
+    rn->timed_want = timed_steps;
     for (int i = 0; i < timed_steps && ok; i++)
       ok = hipEventCreate(&rn->t0[i]) == hipSuccess && hipEventCreate(&rn->t1[i]) == hipSuccess;
   }
@@ -126,6 +128,13 @@ extern "C" pcr_status pcr_runner_create(int timed_steps, pcr_runner** out) {
 }
 
 extern "C" void pcr_runner_destroy(pcr_runner* rn) { delete rn; }
+
+extern "C" pcr_status pcr_runner_set_timed(pcr_runner* rn, int timed_steps) {
+  PCR_REQUIRE(rn != nullptr && timed_steps >= 0 && timed_steps <= rn->timed_cap,
+              "runner_set_timed: %d outside [0, %d]", timed_steps, rn ? rn->timed_cap : 0);
+  rn->timed_want = timed_steps;
+  return PCR_OK;
+}
 
 extern "C" pcr_status pcr_runner_grid_times(pcr_runner* rn, float* ms, int cap, int* count) {
   PCR_REQUIRE(rn != nullptr && ms != nullptr && count != nullptr, "runner_grid_times: NULL");
@@ -167,7 +176,9 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
     ~Owned() { delete p; }
   } owned{tmp};
   pcr_runner* const rn = runner;
-  rn->timed_last = schedule == 0 ? 0 : steps < rn->timed_cap ? steps : rn->timed_cap;
+  rn->timed_last = schedule == 0 ? 0 : steps < rn->timed_want ? steps : rn->timed_want;
+  // the LAST timed_last steps of the run are timed (the pipeline is full)
+  const int t_first = steps - rn->timed_last;
   hipEvent_t* e = rn->sync;
   hipEvent_t fork = e[0], means_done[2] = {e[1], e[2]}, stream_done[2] = {e[3], e[4]},
              join[3] = {e[5], e[6], e[7]}, sort_done[2] = {e[8], e[9]},
@@ -211,11 +222,11 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
                                                 a->vox_ws_bytes, sp));
       PCR_HIP(hipEventRecord(means_done[q], sp), "means record");
       if (!(skip & 64)) PCR_HIP(hipStreamWaitEvent(sv, means_done[q], 0), "means wait");
-      if (s < rn->timed_cap) PCR_HIP(hipEventRecord(rn->t0[s], sv), "timing record");
+      if (s >= t_first) PCR_HIP(hipEventRecord(rn->t0[s - t_first], sv), "timing record");
       if (!(skip & 4))
         PCR_TRY(pcr_extractor_voxel_stream(a->b, a->c, a->n, a->r, a->cnt, a->grid,
                                            a->vox_ws[q], a->vox_ws_bytes, sv));
-      if (s < rn->timed_cap) PCR_HIP(hipEventRecord(rn->t1[s], sv), "timing record");
+      if (s >= t_first) PCR_HIP(hipEventRecord(rn->t1[s - t_first], sv), "timing record");
       if (!(skip & 128)) PCR_HIP(hipEventRecord(stream_done[q], sv), "stream record");
       // 1024: sort and PPF on `origin` with no waits (the selection alone on
       // s_nbr; timing only, breaks the ordering)
@@ -253,11 +264,11 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
     PCR_HIP(hipEventRecord(means_done[q], sp), "means record");
     PCR_TRY(match_pairs(a, sp));
     PCR_HIP(hipStreamWaitEvent(sv, means_done[q], 0), "means wait");
-    const bool timed = s < rn->timed_cap;
-    if (timed) PCR_HIP(hipEventRecord(rn->t0[s], sv), "timing record");
+    const bool timed = s >= t_first;
+    if (timed) PCR_HIP(hipEventRecord(rn->t0[s - t_first], sv), "timing record");
     PCR_TRY(pcr_extractor_voxel_stream(a->b, a->c, a->n, a->r, a->cnt, a->grid, a->vox_ws[q],
                                        a->vox_ws_bytes, sv));
-    if (timed) PCR_HIP(hipEventRecord(rn->t1[s], sv), "timing record");
+    if (timed) PCR_HIP(hipEventRecord(rn->t1[s - t_first], sv), "timing record");
     PCR_HIP(hipEventRecord(stream_done[q], sv), "stream record");
     if (schedule == 2) {
       PCR_HIP(hipStreamWaitEvent(sn, sort_done[q], 0), "sort wait");

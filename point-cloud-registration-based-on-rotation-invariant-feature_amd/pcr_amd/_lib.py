@@ -54,6 +54,7 @@ SIGNATURES = {
     "pcr_runner_create": (ST, [I, ctypes.POINTER(P)]),
     "pcr_runner_destroy": (None, [P]),
     "pcr_runner_grid_times": (ST, [P, P, I, ctypes.POINTER(I)]),
+    "pcr_runner_set_timed": (ST, [P, I]),
     "pcr_extractor_run": (ST, [P, P, I, I, P, P, P, P, P]),
     "pcr_mutual_nn_workspace_size": (SZ, [I, I, I]),
     "pcr_mutual_nn_match": (ST, [P, P, I, I, I, I, P, P, P, P, P, P, SZ, P]),

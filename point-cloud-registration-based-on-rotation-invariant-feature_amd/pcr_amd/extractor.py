@@ -258,6 +258,13 @@ class SphExtractor:
         self._runner, self._runner_cap = h, int(timed_steps)
         return h
 
+    def reserve_timing(self, timed_steps):
+        """Create the runner with room for `timed_steps` grid-kernel timing
+        pairs now, so a later run_native(..., timed=True) of that many steps
+        does not synchronise the device and create events inside a timed
+        region."""
+        self._get_runner(int(timed_steps))
+
     def _free_runner(self):
         if getattr(self, "_runner", None) is not None:
             torch.cuda.synchronize(self.device)
@@ -288,12 +295,17 @@ class SphExtractor:
         on s_pre, the grid stream on s_vox, sort + select + PPF on s_nbr,
         voxel buffer sets alternating), 2 = as 1 with the Morton sort on
         s_pre, 0 = two streams with the fused grid kernel.  One ctypes call
-        for all steps.  timed: bracket each step's grid-stream kernel with
-        timing events (read back with grid_kernel_times()).  match: a
+        for all steps.  timed: bracket the grid-stream kernel of every step
+        (True) or of the last N steps (an int N) with timing events (read
+        back with grid_kernel_times()).  match: a
         registration.PairMatch whose buffers receive, every step, the
         mutual-NN matching of clouds [0, B/2) against [B/2, B)."""
         self._check_inputs(xyz, normals, features)
-        runner = self._get_runner(steps if timed else 0)
+        # timed: True = every step, an int N = the last N steps
+        ntimed = min(steps, (steps if timed is True else int(timed)) if timed else 0)
+        runner = self._get_runner(ntimed)
+        if self._runner_cap:
+            _lib.check(_lib.load().pcr_runner_set_timed(runner, ntimed), "runner_set_timed")
         s1 = self._set(1)
         a = _lib.ExtractorArgs()
         a.b, a.n, a.c, a.k, a.r, a.relative = self.b, self.n, self.c, self.k, self.r, \

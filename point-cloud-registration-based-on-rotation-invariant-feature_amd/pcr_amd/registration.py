@@ -82,3 +82,6 @@ class PairExtractor:
 
     def grid_kernel_times(self):
         return self.ex.grid_kernel_times()
+
+    def reserve_timing(self, timed_steps):
+        self.ex.reserve_timing(timed_steps)

@@ -83,8 +83,8 @@ def test_extractor_native_runner(dev, schedule):
     ex = SphExtractor(b, n, c, k, r, device=dev)
     ref = {kk: v.clone() for kk, v in ex.forward(tx, tn, tf).items()}
     # the runner's events are reused across calls of different lengths, with
-    # and without grid-kernel timing
-    for steps, timed in ((5, False), (3, True), (5, True), (1, False)):
+    # and without grid-kernel timing (True: every step; an int N: the last N)
+    for steps, timed in ((5, False), (3, True), (5, True), (6, 2), (1, False)):
         desc_steps = torch.empty((steps, b, c), device=dev)
         for _ in range(2):
             poison(ex)
@@ -99,7 +99,7 @@ def test_extractor_native_runner(dev, schedule):
             assert torch.equal(desc_steps[s], ref["desc"]), (steps, s)
         if timed:
             ms = ex.grid_kernel_times()
-            assert len(ms) == (0 if schedule == 0 else steps)
+            assert len(ms) == (0 if schedule == 0 else steps if timed is True else min(steps, timed))
             assert all(0 < t < 100 for t in ms)
 
 
