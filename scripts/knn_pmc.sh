@@ -7,9 +7,10 @@ LIB=${1:-libpcr_amd_diag}
 export PCR_AMD_LIB=$PWD/point-cloud-registration-based-on-rotation-invariant-feature_amd/lib/$LIB.so
 i=0
 for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY" \
-           "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_INSTS_VMEM GRBM_GUI_ACTIVE"; do
+           "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_INSTS_VMEM GRBM_GUI_ACTIVE" \
+           "SQ_LDS_BANK_CONFLICT SQ_LDS_ADDR_CONFLICT SQ_LDS_UNALIGNED_STALL"; do
   i=$((i+1))
-  timeout -k 10 200 rocprofv3 --pmc $set -d gpurun_out/kpmc$i -o run --output-format csv -- python3 scripts/knn_bench.py > gpurun_out/kpmc$i.log 2>&1 || { echo "pass $i failed"; tail -5 gpurun_out/kpmc$i.log; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc $set -d gpurun_out/kpmc$i -o run --output-format csv -- python3 scripts/knn_bench.py > gpurun_out/kpmc$i.log 2>&1 || { echo "pass $i failed"; tail -5 gpurun_out/kpmc$i.log; exit 1; }
 done
 python3 - <<'PY'
 import csv, glob, collections

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Turn the two rocprofv3 --pmc passes of scripts/gpu_steps.sh (FETCH_SIZE,
 WRITE_SIZE; separate passes, TCC slots) into profiles/pmc_traffic.json, the
-per-launch HBM bytes of the dominant kernel that bench.py reports as
-roofline.traffic.
+per-launch HBM bytes of the dominant kernel (bench.py roofline.kernel.traffic)
+and of the whole step, summed over the step's kernels (roofline.traffic).
 
 gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports half
 the bytes of a wide coalesced streaming read, so it is doubled; WRITE_SIZE is
@@ -20,20 +20,26 @@ from collections import defaultdict
 KERNEL = os.environ.get("PCR_PMC_KERNEL", "vox_stream_kernel")
 
 
-def per_dispatch(d, counter):
+# the kernels of one bench step (schedule 1): one launch each per step
+STEP_KERNELS = ("knn_sort_kernel", "knn_select_kernel", "local_ppf_self_kernel",
+                "vox_prep_kernel", "vox_means_kernel", "vox_stream_kernel")
+
+
+def per_dispatch(d, counter, kernel=None):
+    kernel = kernel or KERNEL
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     if not files:
         raise SystemExit(f"no counter_collection.csv under {d}")
     acc = defaultdict(float)
     for fn in files:
         for row in csv.DictReader(open(fn)):
-            if KERNEL not in row.get("Kernel_Name", ""):
+            if kernel not in row.get("Kernel_Name", ""):
                 continue
             if row.get("Counter_Name") != counter:
                 continue
             acc[row["Dispatch_Id"]] += float(row["Counter_Value"])
     if not acc:
-        raise SystemExit(f"no {counter} rows for {KERNEL} under {d}")
+        raise SystemExit(f"no {counter} rows for {kernel} under {d}")
     return list(acc.values())
 
 
@@ -48,7 +54,15 @@ def main():
            "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
            "grid_kernel_hbm_bytes_per_launch": fetch + write,
            "dispatches": [len(f), len(w)],
+           "step_kernels": {}, "step_hbm_bytes": 0.0,
            "note": "FETCH_SIZE x2 (gfx950 half-count on wide streaming reads), WRITE_SIZE as is; KiB -> bytes"}
+    # the whole step: every step kernel's average fetch + write per launch
+    for kname in STEP_KERNELS:
+        kf = per_dispatch(fd, "FETCH_SIZE", kname)
+        kw = per_dispatch(wd, "WRITE_SIZE", kname)
+        kb = 2.0 * sum(kf) / len(kf) * 1024.0 + sum(kw) / len(kw) * 1024.0
+        res["step_kernels"][kname] = kb
+        res["step_hbm_bytes"] += kb
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps(res))
