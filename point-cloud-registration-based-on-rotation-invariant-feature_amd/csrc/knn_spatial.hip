@@ -775,7 +775,7 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
   unsigned* hist_s = (unsigned*)sel_u;
   kkey* buf_s = (kkey*)sel_u;
   __shared__ unsigned dest_s[kBlk];
-  __shared__ unsigned cut_s[2 + NG][kBlk];  // wave 0's cut: bin, count, wave fields
+  __shared__ unsigned cut_s[2 + 2 * NG][kBlk];  // wave 0's cut: bin, count, wave fields (cut, below)
   // cached clouds: the Morton-sorted candidates (the near ones of a query
   // block cluster in a few groups, so few groups are collected) and their
   // point ids as u16, read with the coordinates: the collect pass never
@@ -1058,9 +1058,12 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
   // the bulk of the cloud) recounts inside each query's cut bin with
   // 1/64-octave bins (bits >> 17) before it gives up to the insertion
   // fallback.  Every wave computes the same cut for its 64 queries.
-  int total = 0, slot = 0, bstar = -1;
+  // total: keys at or below the cut bin; lo_total (S): keys below it (all of
+  // them are among the k nearest); slot / slot_lo: this wave's first slot
+  // among all / the below-cut keys of the lane
+  int total = 0, slot = 0, bstar = -1, lo_total = 0, slot_lo = 0;
   int shift = 21, base = ebase;
-  unsigned ucut = 0u;
+  unsigned ucut = 0u, ulo = 0u;
 #ifdef PCR_DIAG
   int diag_reason = fallback ? 1 : 0;
 #endif
@@ -1084,18 +1087,20 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     PCR_STAMP(2);
     // wave 0 finds the cut of the 64 queries (the other waves would repeat
     // the same sweep) and hands it over through LDS
-    unsigned cum[NG], cut[NG];
+    unsigned cum[NG], cut[NG], cutb[NG];
 #pragma unroll
-    for (int g = 0; g < NG; g++) cum[g] = cut[g] = 0u;
+    for (int g = 0; g < NG; g++) cum[g] = cut[g] = cutb[g] = 0u;
     if (wv == 0) {
       bstar = -1;
       total = 0;
       for (int b0 = 0; b0 < kNB; b0 += 4) {
 #pragma unroll
         for (int bin = b0; bin < b0 + 4; bin++) {
+          unsigned prev[NG];
           int tb = 0;
 #pragma unroll
           for (int g = 0; g < NG; g++) {
+            prev[g] = cum[g];
             cum[g] += hist_s[(g * (kNB + 1) + bin) * kBlk + lane];
             tb += (int)field_sum<CB>(cum[g]);
           }
@@ -1103,7 +1108,10 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
             bstar = bin;
             total = tb;
 #pragma unroll
-            for (int g = 0; g < NG; g++) cut[g] = cum[g];
+            for (int g = 0; g < NG; g++) {
+              cut[g] = cum[g];
+              cutb[g] = prev[g];
+            }
           }
         }
         if (__all(bstar >= 0)) break;
@@ -1111,28 +1119,45 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
       cut_s[0][lane] = (unsigned)bstar;
       cut_s[1][lane] = (unsigned)total;
 #pragma unroll
-      for (int g = 0; g < NG; g++) cut_s[2 + g][lane] = cut[g];
+      for (int g = 0; g < NG; g++) {
+        cut_s[2 + g][lane] = cut[g];
+        cut_s[2 + NG + g][lane] = cutb[g];
+      }
     }
     __syncthreads();
     bstar = (int)cut_s[0][lane];
     total = (int)cut_s[1][lane];
 #pragma unroll
-    for (int g = 0; g < NG; g++) cut[g] = cut_s[2 + g][lane];
-    // slots of the waves before this one
+    for (int g = 0; g < NG; g++) {
+      cut[g] = cut_s[2 + g][lane];
+      cutb[g] = cut_s[2 + NG + g][lane];
+    }
+    // slots of the waves before this one, among all and among the below-cut
+    // keys; the lane's below-cut total
     const int mg = wv / FPD;
     const unsigned below = (1u << ((wv % FPD) * CB)) - 1u;
-    slot = 0;
+    slot = slot_lo = lo_total = 0;
 #pragma unroll
-    for (int g = 0; g < NG; g++)
+    for (int g = 0; g < NG; g++) {
       slot += (int)field_sum<CB>(g < mg ? cut[g] : (g == mg ? (cut[g] & below) : 0u));
+      slot_lo += (int)field_sum<CB>(g < mg ? cutb[g] : (g == mg ? (cutb[g] & below) : 0u));
+      lo_total += (int)field_sum<CB>(cutb[g]);
+    }
   };
+  // the collected keys sit in two regions of the key buffer: rows [0, S) the
+  // keys below the cut bin (all among the k nearest, S < k), rows [cut0,
+  // cut0 + total - S) the cut bin's keys, so each is ranked within its own
+  // region (S^2 + C^2 compares instead of (S + C)^2).  A lane whose cut bin
+  // holds more than CAP - cut0 keys overflows.
+  const int cut0 = (k + 7) & ~7;
+  auto overflow = [&]() { return qlive && total - lo_total > CAP - cut0; };
   if (!fallback) {
     count_cut(ftop);
     const bool no_cut = __any(qlive && bstar < 0);
 #ifdef PCR_DIAG
-    diag_reason |= (no_cut ? 2 : 0) | (__any(qlive && total > CAP) ? 4 : 0);
+    diag_reason |= (no_cut ? 2 : 0) | (__any(overflow()) ? 4 : 0);
 #endif
-    if (!no_cut && __any(qlive && total > CAP)) {
+    if (!no_cut && __any(overflow())) {
       // refine: bin 0 = below the cut bin, bins 1..16 = its 16 sub-bins
       const float lim = qlive ? __uint_as_float((unsigned)(base + bstar + 1) << 21) : 0.0f;
       base = qlive ? ((base + bstar) << 4) - 1 : 0;
@@ -1145,8 +1170,11 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
       diag_reason |= 8;
 #endif
     }
-    fallback = __any(qlive && (bstar < 0 || total > CAP));
-    if (qlive && !fallback) ucut = (unsigned)(base + bstar + 1) << shift;
+    fallback = __any(qlive && bstar < 0) || __any(overflow());
+    if (qlive && !fallback) {
+      ucut = (unsigned)(base + bstar + 1) << shift;
+      ulo = bstar > 0 ? (unsigned)(base + bstar) << shift : 0u;
+    }
   }
   __syncthreads();  // histogram reads done: buf_s overwrites it
 #ifdef PCR_DIAG
@@ -1161,6 +1189,7 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
   if (!fallback) {
     // 4. collect
     const float fcut = __uint_as_float(ucut);
+    int slot_cut = cut0 + (slot - slot_lo);
     visit(fcut, std::true_type(), [&](int pos, const float (&d)[4], uint2 jp) {
       bool take[4];
 #pragma unroll
@@ -1175,41 +1204,50 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
         for (int h = 0; h < 4; h++) {
           // exec-masked: only the taking lanes store (few lanes of a wave)
           if (take[h]) {
-            buf_s[slot * kBlk + lane] = make_key(d[h], j4[h]);
-            slot++;
+            const bool lo = __float_as_uint(d[h]) < ulo;
+            buf_s[(lo ? slot_lo : slot_cut) * kBlk + lane] = make_key(d[h], j4[h]);
+            slot_lo += lo ? 1 : 0;
+            slot_cut += lo ? 0 : 1;
           }
         }
       }
     });
-    // rows [total, tmax) of every lane read as padding in the rank sweep
-    int tmax = total;
+    // region sizes: S = lo_total below the cut bin, C = total - S in it;
+    // rows past a lane's own count, up to the wave-wide maximum rounded to
+    // eight (the sweep reads eight rows per wait), read as padding
+    const int cnt_c = total - lo_total;
+    auto wave_max_i = [&](int v) {
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) tmax = max(tmax, __shfl_xor(tmax, off, kWave));
-    tmax = __builtin_amdgcn_readfirstlane(tmax);
-    // rows [total, tpad) of every lane read as padding: the rank sweep reads
-    // eight rows per wait
-    const int tpad = (tmax + 7) & ~7;
-    for (int i = total + wv; i < tpad; i += NW) buf_s[i * kBlk + lane] = PCR_KEY_PAD;
+      for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off, kWave));
+      return __builtin_amdgcn_readfirstlane(v);
+    };
+    const int smax = wave_max_i(lo_total), cmax = wave_max_i(cnt_c);
+    const int spad = (smax + 7) & ~7, cpad = (cmax + 7) & ~7;
+    for (int i = lo_total + wv; i < spad; i += NW) buf_s[i * kBlk + lane] = PCR_KEY_PAD;
+    for (int i = cnt_c + wv; i < cpad; i += NW) buf_s[(cut0 + i) * kBlk + lane] = PCR_KEY_PAD;
     __syncthreads();
     PCR_STAMP(3);
 
-    // 5. rank: wave wv holds keys wv, wv + NW, ... (ne of them, wave-uniform)
-    //    and counts, for each, the keys below it in one sweep of all tmax
+    // 5. rank: wave wv holds the keys wv, wv + NW, ... of each region and
+    //    counts, for each, the keys below it in one sweep of that region's
     //    rows; the sweep is compiled for a few key counts so that no compare
-    //    is wasted on empty key slots and none needs a guard
-    constexpr int kE = CAP / NW;  // collected keys ranked per wave (max)
+    //    is wasted on empty key slots and none needs a guard.  A below-cut
+    //    key's rank is its rank in its region; a cut-bin key's is S + its
+    //    rank in its region.
+    constexpr int kEL = (KSEL + NW - 1) / NW;  // below-cut keys per wave (S < k <= KSEL)
+    constexpr int kEC = CAP / NW;              // cut-bin keys per wave (C <= CAP - cut0)
+    constexpr int kE = kEC > kEL ? kEC : kEL;
+    // one register set for both regions (the below-cut keys are placed before
+    // the cut bin's are loaded): the selection's VGPRs bound how many other
+    // waves share its CUs
     kkey key[kE];
     int rank[kE];
-    const int ne = (tmax - wv + NW - 1) / NW;  // keys this wave holds: wv + e * NW < tmax
-#pragma unroll
-    for (int e = 0; e < kE; e++) {
-      const int i = wv + e * NW;
-      key[e] = i < total ? buf_s[i * kBlk + lane] : PCR_KEY_PAD;
-      rank[e] = 0;
-    }
-    auto sweep = [&](auto ne_c) {
+    const int nel = (smax - wv + NW - 1) / NW;
+    const int nec = (cmax - wv + NW - 1) / NW;
+    // rows [r0, r0 + rpad) against the first NE keys
+    auto sweep = [&](auto ne_c, int r0, int rpad) __attribute__((always_inline)) {
       constexpr int NE = decltype(ne_c)::value;
-      for (int j2 = 0; j2 < tpad; j2 += 8) {
+      for (int j2 = r0; j2 < r0 + rpad; j2 += 8) {
         kkey o[8];
 #pragma unroll
         for (int u = 0; u < 8; u++) o[u] = buf_s[(j2 + u) * kBlk + lane];
@@ -1219,26 +1257,51 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
           for (int e = 0; e < NE; e++) rank[e] += o[u] < key[e] ? 1 : 0;
       }
     };
-    if (ne <= 3)
-      sweep(std::integral_constant<int, 3>());
-    else if (ne <= 5)
-      sweep(std::integral_constant<int, 5>());
-    else if (ne <= 7)
-      sweep(std::integral_constant<int, 7>());
-    else if (ne <= 9)
-      sweep(std::integral_constant<int, 9>());
-    else if (ne <= 13 && kE > 13)
-      sweep(std::integral_constant<int, (kE > 13 ? 13 : kE)>());
-    else if (ne <= 17 && kE > 17)
-      sweep(std::integral_constant<int, (kE > 17 ? 17 : kE)>());
-    else
-      sweep(std::integral_constant<int, kE>());
-    PCR_STAMP(4);
-    __syncthreads();  // all ranking reads of buf_s are done
+    auto sweep_n = [&](int ne, int r0, int rpad, auto km_c) __attribute__((always_inline)) {
+      constexpr int KM = decltype(km_c)::value;
+      if (ne <= 0) return;
+      if (ne <= 1)
+        sweep(std::integral_constant<int, 1>(), r0, rpad);
+      else if (ne <= 2)
+        sweep(std::integral_constant<int, 2>(), r0, rpad);
+      else if (ne <= 3 || KM <= 3)
+        sweep(std::integral_constant<int, (KM < 3 ? KM : 3)>(), r0, rpad);
+      else if (ne <= 4 || KM <= 4)
+        sweep(std::integral_constant<int, (KM < 4 ? KM : 4)>(), r0, rpad);
+      else if (ne <= 6 || KM <= 6)
+        sweep(std::integral_constant<int, (KM < 6 ? KM : 6)>(), r0, rpad);
+      else if (ne <= 8 || KM <= 8)
+        sweep(std::integral_constant<int, (KM < 8 ? KM : 8)>(), r0, rpad);
+      else
+        sweep(std::integral_constant<int, KM>(), r0, rpad);
+    };
+    // below-cut region: ranks within it are final
 #pragma unroll
     for (int e = 0; e < kE; e++) {
       const int i = wv + e * NW;
-      if (e < ne && i < total && rank[e] < k) buf_s[rank[e] * kBlk + lane] = key[e];
+      key[e] = (e < kEL && i < lo_total) ? buf_s[i * kBlk + lane] : PCR_KEY_PAD;
+      rank[e] = 0;
+    }
+    sweep_n(nel, 0, spad, std::integral_constant<int, kEL>());
+    __syncthreads();  // the region's ranking reads are done
+    // placed in rows [0, S), which the cut-bin sweep does not read
+#pragma unroll
+    for (int e = 0; e < kEL; e++)
+      if (wv + e * NW < lo_total) buf_s[rank[e] * kBlk + lane] = key[e];
+    // cut-bin region: rank S + its rank within the region, kept when < k
+    // (rows [S, k) are below cut0, so no sweep reads them)
+#pragma unroll
+    for (int e = 0; e < kE; e++) {
+      const int i = wv + e * NW;
+      key[e] = (e < kEC && i < cnt_c) ? buf_s[(cut0 + i) * kBlk + lane] : PCR_KEY_PAD;
+      rank[e] = 0;
+    }
+    sweep_n(nec, cut0, cpad, std::integral_constant<int, kEC>());
+    PCR_STAMP(4);
+#pragma unroll
+    for (int e = 0; e < kEC; e++) {
+      const int r = lo_total + rank[e];
+      if (wv + e * NW < cnt_c && r < k) buf_s[r * kBlk + lane] = key[e];
     }
     __syncthreads();
     PCR_STAMP(5);
