@@ -1214,7 +1214,8 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     });
     // region sizes: S = lo_total below the cut bin, C = total - S in it;
     // rows past a lane's own count, up to the wave-wide maximum rounded to
-    // eight (the sweep reads eight rows per wait), read as padding
+    // four (the sweep reads four rows per wait: eight made this phase the
+    // kernel's VGPR peak, 94 instead of 72), read as padding
     const int cnt_c = total - lo_total;
     auto wave_max_i = [&](int v) {
 #pragma unroll
@@ -1222,7 +1223,7 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
       return __builtin_amdgcn_readfirstlane(v);
     };
     const int smax = wave_max_i(lo_total), cmax = wave_max_i(cnt_c);
-    const int spad = (smax + 7) & ~7, cpad = (cmax + 7) & ~7;
+    const int spad = (smax + 3) & ~3, cpad = (cmax + 3) & ~3;
     for (int i = lo_total + wv; i < spad; i += NW) buf_s[i * kBlk + lane] = PCR_KEY_PAD;
     for (int i = cnt_c + wv; i < cpad; i += NW) buf_s[(cut0 + i) * kBlk + lane] = PCR_KEY_PAD;
     __syncthreads();
@@ -1244,15 +1245,15 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     int rank[kE];
     const int nel = (smax - wv + NW - 1) / NW;
     const int nec = (cmax - wv + NW - 1) / NW;
-    // rows [r0, r0 + rpad) against the first NE keys
+    // rows [r0, r0 + rpad) against the first NE keys, four rows per wait
     auto sweep = [&](auto ne_c, int r0, int rpad) __attribute__((always_inline)) {
       constexpr int NE = decltype(ne_c)::value;
-      for (int j2 = r0; j2 < r0 + rpad; j2 += 8) {
-        kkey o[8];
+      for (int j2 = r0; j2 < r0 + rpad; j2 += 4) {
+        kkey o[4];
 #pragma unroll
-        for (int u = 0; u < 8; u++) o[u] = buf_s[(j2 + u) * kBlk + lane];
+        for (int u = 0; u < 4; u++) o[u] = buf_s[(j2 + u) * kBlk + lane];
 #pragma unroll
-        for (int u = 0; u < 8; u++)
+        for (int u = 0; u < 4; u++)
 #pragma unroll
           for (int e = 0; e < NE; e++) rank[e] += o[u] < key[e] ? 1 : 0;
       }
