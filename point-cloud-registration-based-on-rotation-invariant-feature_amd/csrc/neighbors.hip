@@ -270,8 +270,8 @@ __global__ __launch_bounds__(256) void local_ppf_kernel(
 // rows, so every neighbour gather is an LDS read: no dependent global loads,
 // which under the grid kernel's write stream take microseconds each.
 constexpr int kPpfSelfMaxN = 2048;
-template <int SL>
-__global__ __launch_bounds__(256) void local_ppf_self_kernel(const float* __restrict__ xyz,
+template <int SL, int NT = 256>
+__global__ __launch_bounds__(NT) void local_ppf_self_kernel(const float* __restrict__ xyz,
                                                              const float* __restrict__ nrm,
                                                              const int* __restrict__ idx, int n,
                                                              int k, int relative,
@@ -279,7 +279,7 @@ __global__ __launch_bounds__(256) void local_ppf_self_kernel(const float* __rest
   extern __shared__ __align__(16) float cl_s[];  // [6][n]: x y z nx ny nz
   (void)PCR_PRIO(2);
   const int tid = threadIdx.x;
-  const int j = blockIdx.x * 256 + tid;
+  const int j = blockIdx.x * NT + tid;
   const int q0 = blockIdx.y * SL;
   const int b = blockIdx.z;
   const float* P = xyz + (size_t)b * 3 * n;
@@ -288,11 +288,11 @@ __global__ __launch_bounds__(256) void local_ppf_self_kernel(const float* __rest
 #pragma unroll
   for (int s = 0; s < SL; s++)
     id[s] = (j < n && q0 + s < k) ? idx[((size_t)b * k + q0 + s) * n + j] : 0;
-  constexpr int E = kPpfSelfMaxN / 256;
+  constexpr int E = kPpfSelfMaxN / NT;
   float st[E][6];
 #pragma unroll
   for (int e = 0; e < E; e++) {
-    const int i = e * 256 + tid;
+    const int i = e * NT + tid;
     if (i < n) {
 #pragma unroll
       for (int a = 0; a < 3; a++) {
@@ -303,7 +303,7 @@ __global__ __launch_bounds__(256) void local_ppf_self_kernel(const float* __rest
   }
 #pragma unroll
   for (int e = 0; e < E; e++) {
-    const int i = e * 256 + tid;
+    const int i = e * NT + tid;
     if (i < n)
 #pragma unroll
       for (int a = 0; a < 6; a++) cl_s[(size_t)a * n + i] = st[e][a];
@@ -690,14 +690,23 @@ extern "C" pcr_status pcr_local_ppf_forward(const float* points, const float* no
   hipLaunchKernelGGL((local_ppf_self_kernel<SLV>), dim3(ceil_div(n, 256), ceil_div(u, SLV), b), \
                      dim3(256), (size_t)6 * n * 4, as_stream(stream), points, normals, idx, n,  \
                      u, relative, out)
+#define PCR_PPF_SELF_NT(SLV, NTV)                                                               \
+  hipLaunchKernelGGL((local_ppf_self_kernel<SLV, NTV>), dim3(ceil_div(n, NTV), ceil_div(u, SLV), b), \
+                     dim3(NTV), (size_t)6 * n * 4, as_stream(stream), points, normals, idx, n,  \
+                     u, relative, out)
 #ifdef PCR_DIAG
-    if (sl == 16) PCR_PPF_SELF(16);
+    static const int pnt = PCR_KNOB("PCR_PPF_NT", 256);
+    if (pnt == 512) PCR_PPF_SELF_NT(8, 512);
+    else if (pnt == 1024) PCR_PPF_SELF_NT(8, 1024);
+    else if (pnt == 1025) PCR_PPF_SELF_NT(16, 1024);
+    else if (sl == 16) PCR_PPF_SELF(16);
     else if (sl == 32) PCR_PPF_SELF(32);
     else if (sl == 4) PCR_PPF_SELF(4);
     else
 #endif
       PCR_PPF_SELF(8);
 #undef PCR_PPF_SELF
+#undef PCR_PPF_SELF_NT
     return launch_status("local_ppf_forward");
   }
   hipLaunchKernelGGL(local_ppf_kernel, dim3(ceil_div(m, 256), u, b), dim3(256), 0,
