@@ -298,7 +298,11 @@ __global__ __launch_bounds__(NT) void vox_prep_kernel(
   int* cnt_l = pre_l + W;                 // [n] points per occupied voxel
   int* perm_l = cnt_l + n;                // [n] points grouped by voxel
 
-  // 1. occupancy bitmap
+  // 1. occupancy bitmap.  The bitmap was zeroed at the top; the normalising
+  // mode's reductions put barriers in between, the others need one here, or
+  // a slow wave's zeroing can erase a fast wave's bit (seen on cube grids:
+  // a voxel lost its bit and its points joined the next segment)
+  if (MODE != kSphNormalize) lds_barrier();
   for (int i = tid; i < n; i += nt) cnt_l[i] = 0;
 #pragma unroll
   for (int e = 0; e < kMaxE; e++) {

@@ -141,3 +141,25 @@ def test_cube_avg_vox_backward_c3_shape(dev):
     gy = rng.standard_normal((b, c, r ** 3)).astype(np.float32)
     gx = ops.avg_voxelize_backward(T(gy, dev), ind, cnt)
     assert np.array_equal(N(gx), oracle.avg_voxelize_backward(gy, ei, ec))
+
+
+def test_cube_vox_forward_repeated(dev):
+    """The prep kernel zeroes its occupancy bitmap and then sets bits with LDS
+    atomics; on the cube path nothing else separated the two, so a slow
+    wave's zeroing could erase a fast wave's bit (a voxel then lost its bit
+    and its points joined the next segment: ~13% of runs at this shape).
+    Repeated runs must all match the oracle."""
+    from pcr_amd import ops
+    b, n, c, r = 4, 2048, 16, 32
+    rng = np.random.default_rng(36)
+    vc = rng.integers(0, r, (b, 3, n)).astype(np.int32)
+    feat = rng.uniform(-1, 1, (b, c, n)).astype(np.float32)
+    eo, ei, ec = oracle.avg_voxelize_forward(feat, vc, r)
+    tf, tv = T(feat, dev), T(vc, dev)
+    ecnt = torch.from_numpy(ec).to(dev)
+    bad = 0
+    for _ in range(60):
+        out, ind, cnt = ops.avg_voxelize_forward(tf, tv, r)
+        bad += int(not torch.equal(cnt, ecnt))
+    assert bad == 0, "%d of 60 runs gave wrong voxel counts" % bad
+    assert np.array_equal(N(out), eo) and np.array_equal(N(ind), ei)
