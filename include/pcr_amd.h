@@ -184,6 +184,15 @@ pcr_status pcr_trilinear_devoxelize_forward(int r, int is_training, const float 
 pcr_status pcr_devoxelize_backward(const float *grad_y, const int *inds, const float *wgts, int b,
                                    int c, int n, int r, int skip_neg, float *grad_x,
                                    void *stream);
+/* The same with a workspace of pcr_devoxelize_backward_workspace_size(b, n)
+ * bytes: spherical grads of clouds of <= 4096 points first sort each cloud's
+ * points by corner set once (instead of every channel-group workgroup
+ * sorting every 64 points), so the backward only sums runs.  Same results
+ * up to the fp32 summation order of the atomics (as the reference's). */
+size_t pcr_devoxelize_backward_workspace_size(int b, int n);
+pcr_status pcr_devoxelize_backward_ws(const float *grad_y, const int *inds, const float *wgts,
+                                      int b, int c, int n, int r, int skip_neg, float *grad_x,
+                                      void *workspace, size_t workspace_bytes, void *stream);
 
 /* PVConv dgcnn centre term (modules/pvconv.py:68-89): related[b,c,i] =
  * features[b,c,i] - avg_grid[b,c,ind[b,i]], 0 where ind == -1. */

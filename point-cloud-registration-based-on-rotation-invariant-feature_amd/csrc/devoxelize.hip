@@ -97,7 +97,8 @@ constexpr int kBwdMaxG = 4;
 
 __global__ __launch_bounds__(kBwdThreads) void devox_bwd_kernel(
     const float* __restrict__ grad_y, const int* __restrict__ inds, const float* __restrict__ wgts,
-    int c, int n, int r3, int G, int hw, int skip_neg, float* __restrict__ grad_x, int dbg) {
+    int c, int n, int r3, int G, int hw, int skip_neg, float* __restrict__ grad_x, int dbg,
+    const int* __restrict__ order) {
   extern __shared__ __align__(16) float acc_s[];  // [G][hw]
   const int grp = blockIdx.x;
   const int b = blockIdx.y;
@@ -124,8 +125,12 @@ __global__ __launch_bounds__(kBwdThreads) void devox_bwd_kernel(
     // corners do not follow that pattern take the per-point atomics.
     const int lane = tid & 63, wv = tid >> 6;
     constexpr long long kNoKey = (1ll << 57) - 1;  // above every key (ci0 < 2^22)
+    // `order` (devox_bwd_order_kernel): the cloud's points sorted by corner
+    // set, so a wave's 64 consecutive entries are already sorted and the
+    // per-wave sort is skipped (segments are also longer: fewer tails)
+    const int* ord = order ? order + (size_t)b * n : nullptr;
     for (int base = wv * kWave; base < n; base += kBwdThreads) {
-      const int i = base + lane;
+      const int i = ord ? (base + lane < n ? ord[base + lane] : n) : base + lane;
       const bool live = i < n && I[i] != -1;
       int ci[8];
       float cw[8];
@@ -156,6 +161,7 @@ __global__ __launch_bounds__(kBwdThreads) void devox_bwd_kernel(
           reg ? (((long long)ci[0] << 35) | ((long long)d4 << 13) | ((long long)d2 << 1) | d1)
               : kNoKey;
       long long k2 = (key0 << 6) | lane;
+      if (!ord)
 #pragma unroll
       for (int k = 2; k <= kWave; k <<= 1) {
 #pragma unroll
@@ -328,9 +334,86 @@ extern "C" pcr_status pcr_trilinear_devoxelize_forward(int r, int is_training, c
                        "trilinear_devoxelize_forward");
 }
 
+// The points of each cloud sorted by spherical corner set (the key the
+// backward's wave sort uses, compressed to 52 bits: cell 20, gamma step 20,
+// alpha step 11, beta step 1) with the point id below it; irregular and
+// dropped points last.  One workgroup per cloud.
+constexpr int kOrderMaxN = kSortBlock * kMaxE;
+__global__ __launch_bounds__(kSortBlock) void devox_bwd_order_kernel(const int* __restrict__ inds,
+                                                                     int n, int npad,
+                                                                     int* __restrict__ order) {
+  extern __shared__ __align__(16) unsigned long long okeys[];  // [npad]
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int E = npad / kSortBlock;
+  const int* I = inds + (size_t)b * 8 * n;
+  unsigned long long kv[kMaxE];
+#pragma unroll
+  for (int e = 0; e < kMaxE; e++) {
+    const int i = e * kSortBlock + tid;
+    kv[e] = ~0ull;
+    if (e < E && i < n) {
+      int ci[8];
+#pragma unroll
+      for (int q = 0; q < 8; q++) ci[q] = I[i + (size_t)q * n];
+      const int d1 = ci[1] - ci[0], d2 = ci[2] - ci[0], d4 = ci[4] - ci[0];
+      const bool reg = ci[0] != -1 && (d1 == 0 || d1 == 1) && d2 >= 0 && d4 >= 0 &&
+                       ci[3] == ci[2] + d1 && ci[5] == ci[4] + d1 && ci[6] == ci[4] + d2 &&
+                       ci[7] == ci[6] + d1 && ci[0] >= 0 && ci[0] < (1 << 20) &&
+                       d2 < (1 << 11) && d4 < (1 << 20);
+      const unsigned long long key =
+          reg ? (((unsigned long long)ci[0] << 32) | ((unsigned long long)d4 << 12) |
+                 ((unsigned long long)d2 << 1) | (unsigned long long)d1)
+              : (1ull << 52) - 1;
+      kv[e] = (key << 12) | (unsigned long long)i;
+    }
+  }
+  block_bitonic<kSortBlock>(kv, E, okeys);
+  int* o = order + (size_t)b * n;
+#pragma unroll
+  for (int e = 0; e < kMaxE; e++) {
+    const int i = e * kSortBlock + tid;
+    if (e < E && i < n) o[i] = (int)(kv[e] & 0xFFFull);
+  }
+}
+
+static pcr_status devox_backward(const float* grad_y, const int* inds, const float* wgts, int b,
+                                 int c, int n, int r, int skip_neg, float* grad_x,
+                                 const int* order, void* stream);
+
+extern "C" size_t pcr_devoxelize_backward_workspace_size(int b, int n) {
+  if (b <= 0 || n <= 0) return 256;
+  return ((size_t)b * n * 4 + 255) / 256 * 256;
+}
+
+extern "C" pcr_status pcr_devoxelize_backward_ws(const float* grad_y, const int* inds,
+                                                 const float* wgts, int b, int c, int n, int r,
+                                                 int skip_neg, float* grad_x, void* workspace,
+                                                 size_t workspace_bytes, void* stream) {
+  PCR_REQUIRE(b >= 0 && c >= 0 && n >= 0 && r >= 1, "devoxelize_backward: invalid sizes");
+  const int* order = nullptr;
+  // spherical grads of clouds the order kernel sorts in one workgroup (ids
+  // in 12 bits); otherwise the per-wave sort
+  if (skip_neg && n >= 1 && n <= kOrderMaxN && n <= 4096 && b > 0 && c > 0 && workspace &&
+      workspace_bytes >= pcr_devoxelize_backward_workspace_size(b, n)) {
+    int npad = kSortBlock;
+    while (npad < n) npad <<= 1;
+    hipLaunchKernelGGL(devox_bwd_order_kernel, dim3(b), dim3(kSortBlock), (size_t)npad * 8,
+                       as_stream(stream), inds, n, npad, (int*)workspace);
+    order = (const int*)workspace;
+  }
+  return devox_backward(grad_y, inds, wgts, b, c, n, r, skip_neg, grad_x, order, stream);
+}
+
 extern "C" pcr_status pcr_devoxelize_backward(const float* grad_y, const int* inds,
                                               const float* wgts, int b, int c, int n, int r,
                                               int skip_neg, float* grad_x, void* stream) {
+  return devox_backward(grad_y, inds, wgts, b, c, n, r, skip_neg, grad_x, nullptr, stream);
+}
+
+static pcr_status devox_backward(const float* grad_y, const int* inds, const float* wgts, int b,
+                                 int c, int n, int r, int skip_neg, float* grad_x,
+                                 const int* order, void* stream) {
   PCR_REQUIRE(b >= 0 && c >= 0 && n >= 0 && r >= 1, "devoxelize_backward: invalid sizes");
   const int64_t r3l = (int64_t)r * r * r;
   PCR_REQUIRE(r3l < (1ll << 31) / 64, "devoxelize_backward: resolution too large");
@@ -353,7 +436,7 @@ extern "C" pcr_status pcr_devoxelize_backward(const float* grad_y, const int* in
   allow_big_lds(devox_bwd_kernel, (size_t)G * hw * 4);
   hipLaunchKernelGGL(devox_bwd_kernel, dim3(ceil_div(c, G), b), dim3(kBwdThreads),
                      (size_t)G * hw * 4, as_stream(stream), grad_y, inds, wgts, c, n, r3, G, hw,
-                     skip_neg, grad_x, PCR_KNOB("PCR_DEVOX_BWD_DBG", 0));
+                     skip_neg, grad_x, PCR_KNOB("PCR_DEVOX_BWD_DBG", 0), order);
   return launch_status("devoxelize_backward");
 }
 

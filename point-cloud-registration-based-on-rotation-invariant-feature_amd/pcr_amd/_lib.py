@@ -42,6 +42,8 @@ SIGNATURES = {
     "pcr_spherical_trilinear_devoxelize_forward": (ST, [I, I, P, P, P, I, I, I, P, P, P, P]),
     "pcr_trilinear_devoxelize_forward": (ST, [I, I, P, P, I, I, I, P, P, P, P]),
     "pcr_devoxelize_backward": (ST, [P, P, P, I, I, I, I, I, P, P]),
+    "pcr_devoxelize_backward_workspace_size": (SZ, [I, I]),
+    "pcr_devoxelize_backward_ws": (ST, [P, P, P, I, I, I, I, I, P, P, SZ, P]),
     "pcr_dgcnn_center_gather": (ST, [P, P, P, I, I, I, I, P, P]),
     "pcr_extractor_workspace_size": (SZ, [I, I, I, I]),
     "pcr_extractor_voxel_stage": (ST, [P, P, I, I, I, I, P, P, P, P, P, P, P, P, P, SZ, P]),

@@ -300,9 +300,11 @@ def _devox_backward(grad_y, indices, weights, r, spherical, what):
     b, c, n = grad_y.shape
     r = int(r)
     gx = torch.empty((b, c, r * r * r), dtype=torch.float32, device=grad_y.device)
-    _lib.check(_lib.load().pcr_devoxelize_backward(
+    lib = _lib.load()
+    ws = _workspace(lib.pcr_devoxelize_backward_workspace_size(b, n), grad_y.device)
+    _lib.check(lib.pcr_devoxelize_backward_ws(
         _ptr(grad_y), _ptr(indices), _ptr(weights), b, c, n, r, int(spherical), _ptr(gx),
-        _stream()), what)
+        _ptr(ws), ws.numel(), _stream()), what)
     return gx
 
 
