@@ -128,9 +128,12 @@ __global__ __launch_bounds__(kBwdThreads) void devox_bwd_kernel(
     // `order` (devox_bwd_order_kernel): the cloud's points sorted by corner
     // set, so a wave's 64 consecutive entries are already sorted and the
     // per-wave sort is skipped (segments are also longer: fewer tails)
+    // (I and Wt are then the sorted copies, indexed by position; only the
+    // gradients are gathered by point)
     const int* ord = order ? order + (size_t)b * n : nullptr;
     for (int base = wv * kWave; base < n; base += kBwdThreads) {
-      const int i = ord ? (base + lane < n ? ord[base + lane] : n) : base + lane;
+      const int i = base + lane;
+      const int pt = ord ? (i < n ? ord[i] : 0) : i;
       const bool live = i < n && I[i] != -1;
       int ci[8];
       float cw[8];
@@ -147,7 +150,7 @@ __global__ __launch_bounds__(kBwdThreads) void devox_bwd_kernel(
             ci[7] < hw && hw < (1 << 22) && d2 < 4096 && d4 < (1 << 22);
       float gv[kBwdMaxG];
 #pragma unroll
-      for (int g = 0; g < kBwdMaxG; g++) gv[g] = (live && g < gcount) ? gy[(size_t)g * n + i] : 0.0f;
+      for (int g = 0; g < kBwdMaxG; g++) gv[g] = (live && g < gcount) ? gy[(size_t)g * n + pt] : 0.0f;
       if (live && !reg) {  // irregular: per-point atomics (as below)
 #pragma unroll
         for (int q = 0; q < 8; q++) {
@@ -265,7 +268,8 @@ __global__ __launch_bounds__(kBwdThreads) void devox_bwd_kernel(
         const int v = I[i + (size_t)q * n];
         if (v < hw || v >= r3) continue;
         const float w = Wt[i + (size_t)q * n];
-        for (int g = 0; g < gcount; g++) atomicAdd(gx + (size_t)g * r3 + v, w * gy[(size_t)g * n + i]);
+        const int pt = order ? order[(size_t)b * n + i] : i;  // I / Wt by position, gy by point
+        for (int g = 0; g < gcount; g++) atomicAdd(gx + (size_t)g * r3 + v, w * gy[(size_t)g * n + pt]);
       }
     }
   }
@@ -340,8 +344,11 @@ extern "C" pcr_status pcr_trilinear_devoxelize_forward(int r, int is_training, c
 // dropped points last.  One workgroup per cloud.
 constexpr int kOrderMaxN = kSortBlock * kMaxE;
 __global__ __launch_bounds__(kSortBlock) void devox_bwd_order_kernel(const int* __restrict__ inds,
+                                                                     const float* __restrict__ wgts,
                                                                      int n, int npad,
-                                                                     int* __restrict__ order) {
+                                                                     int* __restrict__ order,
+                                                                     int* __restrict__ sinds,
+                                                                     float* __restrict__ swgts) {
   extern __shared__ __align__(16) unsigned long long okeys[];  // [npad]
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
@@ -369,11 +376,24 @@ __global__ __launch_bounds__(kSortBlock) void devox_bwd_order_kernel(const int* 
     }
   }
   block_bitonic<kSortBlock>(kv, E, okeys);
+  // the point order, and the corner data in that order (the backward then
+  // reads it coalesced; only the gradients are gathered)
   int* o = order + (size_t)b * n;
+  int* si = sinds + (size_t)b * 8 * n;
+  float* sw = swgts + (size_t)b * 8 * n;
+  const float* W = wgts + (size_t)b * 8 * n;
 #pragma unroll
   for (int e = 0; e < kMaxE; e++) {
-    const int i = e * kSortBlock + tid;
-    if (e < E && i < n) o[i] = (int)(kv[e] & 0xFFFull);
+    const int pos = e * kSortBlock + tid;
+    if (e < E && pos < n) {
+      const int p = (int)(kv[e] & 0xFFFull);
+      o[pos] = p;
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        si[pos + (size_t)q * n] = I[p + (size_t)q * n];
+        sw[pos + (size_t)q * n] = W[p + (size_t)q * n];
+      }
+    }
   }
 }
 
@@ -381,9 +401,10 @@ static pcr_status devox_backward(const float* grad_y, const int* inds, const flo
                                  int c, int n, int r, int skip_neg, float* grad_x,
                                  const int* order, void* stream);
 
+// order [b][n] | sorted inds [b][8][n] | sorted wgts [b][8][n]
 extern "C" size_t pcr_devoxelize_backward_workspace_size(int b, int n) {
   if (b <= 0 || n <= 0) return 256;
-  return ((size_t)b * n * 4 + 255) / 256 * 256;
+  return ((size_t)b * n * 4 * 17 + 255) / 256 * 256;
 }
 
 extern "C" pcr_status pcr_devoxelize_backward_ws(const float* grad_y, const int* inds,
@@ -398,9 +419,13 @@ extern "C" pcr_status pcr_devoxelize_backward_ws(const float* grad_y, const int*
       workspace_bytes >= pcr_devoxelize_backward_workspace_size(b, n)) {
     int npad = kSortBlock;
     while (npad < n) npad <<= 1;
+    int* ord = (int*)workspace;
+    int* sinds = ord + (size_t)b * n;
+    float* swgts = (float*)(sinds + (size_t)b * 8 * n);
     hipLaunchKernelGGL(devox_bwd_order_kernel, dim3(b), dim3(kSortBlock), (size_t)npad * 8,
-                       as_stream(stream), inds, n, npad, (int*)workspace);
-    order = (const int*)workspace;
+                       as_stream(stream), inds, wgts, n, npad, ord, sinds, swgts);
+    // the backward reads the sorted corner data by position
+    return devox_backward(grad_y, sinds, swgts, b, c, n, r, skip_neg, grad_x, ord, stream);
   }
   return devox_backward(grad_y, inds, wgts, b, c, n, r, skip_neg, grad_x, order, stream);
 }
