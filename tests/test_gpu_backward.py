@@ -115,6 +115,34 @@ def test_sph_devox_backward_sum_order(dev, b, n, c, r):
     assert_within_sum_order(N(gx), exp, devox_backward_bound(gy, ei, ew, r ** 3, skip_neg=True))
 
 
+@pytest.mark.parametrize("with_ws", [False, True])
+def test_sph_devox_backward_entry_points(dev, with_ws):
+    """Both C entry points at the c3 per-cloud shape: pcr_devoxelize_backward
+    (each workgroup sorts every 64 points by corner set) and
+    pcr_devoxelize_backward_ws (each cloud's points sorted once, the corner
+    data read in that order), against the oracle at the sum-order bound."""
+    from pcr_amd import _lib
+    from pcr_amd.ops import _ptr, _stream
+    b, n, c, r = 3, 2048, 24, 32
+    nc, _, grid, gind, _ = _sph_setup(b, n, c, r, seed=41)
+    _, ei, ew = oracle.spherical_trilinear_devoxelize_forward(r, nc, grid, gind)
+    gy = np.random.default_rng(42).standard_normal((b, c, n)).astype(np.float32)
+    tg, ti, tw = T(gy, dev), T(ei, dev), T(ew, dev)
+    gx = torch.full((b, c, r ** 3), float("nan"), device=dev)
+    lib = _lib.load()
+    if with_ws:
+        ws = torch.empty(lib.pcr_devoxelize_backward_workspace_size(b, n), dtype=torch.uint8,
+                         device=dev)
+        rc = lib.pcr_devoxelize_backward_ws(_ptr(tg), _ptr(ti), _ptr(tw), b, c, n, r, 1,
+                                            _ptr(gx), _ptr(ws), ws.numel(), _stream())
+    else:
+        rc = lib.pcr_devoxelize_backward(_ptr(tg), _ptr(ti), _ptr(tw), b, c, n, r, 1, _ptr(gx),
+                                         _stream())
+    _lib.check(rc, "devoxelize_backward")
+    exp = oracle.devoxelize_backward(gy, ei, ew, r, spherical=True)
+    assert_within_sum_order(N(gx), exp, devox_backward_bound(gy, ei, ew, r ** 3, skip_neg=True))
+
+
 def test_sph_avg_vox_backward_c3_shape(dev):
     """spherical_avg_voxelize backward (spherical_vox.cu:139-163) at the c3
     per-cloud shape: a gather, bit-exact (dropped points get 0)."""
