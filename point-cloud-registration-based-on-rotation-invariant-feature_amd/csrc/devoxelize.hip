@@ -91,6 +91,53 @@ __global__ __launch_bounds__(256) void devox_fwd_kernel(const float* __restrict_
   }
 }
 
+// Cube forward for grids whose channel row fits in LDS (r <= 32): one
+// workgroup per (cloud, channel) stages the whole row with coalesced 16-byte
+// loads, so the 8 corner gathers of every point are LDS reads instead of
+// scattered 4-byte global gathers (a cloud's 8 point blocks used to fetch
+// each row's lines again).  Corners are recomputed per channel (a few VALU);
+// channel 0 writes inds / wgts.  Same corners and wsum8 order as
+// devox_fwd_kernel<false>, so the same bits.
+constexpr int kFwdRowThreads = 1024;
+__global__ __launch_bounds__(kFwdRowThreads) void devox_fwd_cube_row_kernel(
+    const float* __restrict__ coords, const float* __restrict__ feat, int c, int n, int r,
+    float* __restrict__ outs, int* __restrict__ inds, float* __restrict__ wgts) {
+  extern __shared__ __align__(16) float row_s[];  // [r^3]
+  const int j = blockIdx.x;
+  const int b = blockIdx.y;
+  const int tid = threadIdx.x;
+  const int r3 = r * r * r;
+  const float* f = feat + ((size_t)b * c + j) * r3;
+  if ((r3 & 3) == 0) {
+    const float4* f4 = (const float4*)f;
+    float4* s4 = (float4*)row_s;
+    for (int t = tid; t < (r3 >> 2); t += kFwdRowThreads) s4[t] = f4[t];
+  } else {
+    for (int t = tid; t < r3; t += kFwdRowThreads) row_s[t] = f[t];
+  }
+  __syncthreads();
+  const float* x = coords + (size_t)b * 3 * n;
+  float* o = outs + ((size_t)b * c + j) * n;
+  for (int i = tid; i < n; i += kFwdRowThreads) {
+    int idx[8];
+    float w[8];
+    pcr_cube_corners(x[i], x[i + n], x[i + 2 * n], r, idx, w);
+    if (j == 0) {
+      int* I = inds + (size_t)b * 8 * n;
+      float* Wt = wgts + (size_t)b * 8 * n;
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        I[i + (size_t)q * n] = idx[q];
+        Wt[i + (size_t)q * n] = w[q];
+      }
+    }
+    float fv[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) fv[q] = (idx[q] >= 0 && idx[q] < r3) ? row_s[idx[q]] : 0.0f;
+    o[i] = pcr_wsum8(w, fv);
+  }
+}
+
 // Backward with the dense grad written once (see header comment).
 constexpr int kBwdThreads = 256;
 constexpr int kBwdMaxG = 4;
@@ -307,6 +354,13 @@ static pcr_status devox_forward(bool sph, int r, const float* coords, const floa
   PCR_REQUIRE(b >= 0 && c >= 0 && n >= 0 && r >= 1, "%s: invalid sizes", name);
   PCR_REQUIRE((int64_t)r * r * r < (1ll << 31) / 64, "%s: resolution too large", name);
   if (b == 0 || n == 0) return PCR_OK;
+  const size_t row_bytes = (size_t)r * r * r * 4;
+  if (!sph && c > 0 && row_bytes <= 128 * 1024) {
+    allow_big_lds(devox_fwd_cube_row_kernel, row_bytes);
+    hipLaunchKernelGGL(devox_fwd_cube_row_kernel, dim3(c, b), dim3(kFwdRowThreads), row_bytes,
+                       as_stream(stream), coords, features, c, n, r, outs, inds, wgts);
+    return launch_status(name);
+  }
   const int cg = 8;
   dim3 grid(ceil_div(n, 256), c > 0 ? ceil_div(c, cg) : 1, b);
   if (sph)
