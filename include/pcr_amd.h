@@ -190,6 +190,15 @@ pcr_status pcr_devoxelize_backward(const float *grad_y, const int *inds, const f
  * sorting every 64 points), so the backward only sums runs.  Same results
  * up to the fp32 summation order of the atomics (as the reference's). */
 size_t pcr_devoxelize_backward_workspace_size(int b, int n);
+/* Workspace for pcr_devoxelize_backward_ws that also covers the cube
+ * gather path (spherical=0, r <= 32): each cloud's 8n (point, corner) pairs
+ * are counting-sorted by voxel once and every voxel sums its own segment, so
+ * grad_x is written once with no atomics (trilinear_devox.cu:120-163 does one
+ * global float atomic per pair and channel).  Same results up to the fp32
+ * summation order within a voxel.  With only
+ * pcr_devoxelize_backward_workspace_size(b, n) bytes the cube grads take
+ * the LDS-atomic kernel. */
+size_t pcr_devoxelize_backward_workspace_size_r(int b, int n, int r, int spherical);
 pcr_status pcr_devoxelize_backward_ws(const float *grad_y, const int *inds, const float *wgts,
                                       int b, int c, int n, int r, int skip_neg, float *grad_x,
                                       void *workspace, size_t workspace_bytes, void *stream);

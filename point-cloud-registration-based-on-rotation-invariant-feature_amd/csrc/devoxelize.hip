@@ -18,7 +18,9 @@
 // accumulates the hot window [0, hw) in LDS, streams zeros over the rest of
 // its slab with 16-byte stores, then (after its own stores are complete)
 // adds the rare out-of-window corners with global atomics and finally stores
-// the window.  The dense gradient is written exactly once.
+// the window.  The dense gradient is written exactly once.  Cube grads up
+// to r = 32 with a workspace are a gather instead (devox_cube_order_kernel /
+// devox_cube_gather_kernel): no float atomics at all.
 #include "common.hpp"
 
 namespace pcr {
@@ -451,6 +453,187 @@ __global__ __launch_bounds__(kSortBlock) void devox_bwd_order_kernel(const int* 
   }
 }
 
+// Cube grads as a gather (trilinear_devox.cu:120-163 scatters w * g into
+// grad_x with one float atomic per (point, corner, channel)).  The 8n
+// (point, corner) pairs of a cloud are counting-sorted by voxel once, here,
+// one workgroup per cloud with the r^3 counters in LDS; the gather kernel
+// then gives every voxel one thread that sums its segment for a group of
+// channels and writes grad_x exactly once, coalesced, with no atomics.
+// seg [b][r3 + 1]: first pair of each voxel (seg[r3] = pairs kept);
+// pairs [b][8n]: (point id, weight bits) in voxel order.  Pairs whose
+// voxel is outside [0, r3) are dropped, as the window kernel drops them.
+constexpr int kCubeOrderThreads = 1024;
+// counters padded by one word per 32 so the scan's per-thread runs of 32
+// contiguous voxels start in distinct banks
+__device__ inline int cube_pad(int v) { return v + (v >> 5); }
+__global__ __launch_bounds__(kCubeOrderThreads) void devox_cube_order_kernel(
+    const int* __restrict__ inds, const float* __restrict__ wgts, int n, int r3,
+    int* __restrict__ seg, int2* __restrict__ pairs) {
+  extern __shared__ __align__(16) int cnt_s[];  // [cube_pad(r3)] counters | [17] scan
+  int* scan_s = cnt_s + cube_pad(r3);
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int m = 8 * n;
+  const int* I = inds + (size_t)b * m;
+  const float* W = wgts + (size_t)b * m;
+  for (int v = tid; v < cube_pad(r3); v += kCubeOrderThreads) cnt_s[v] = 0;
+  lds_barrier();
+  for (int p = tid; p < m; p += kCubeOrderThreads) {
+    const int v = I[p];
+    if (v >= 0 && v < r3) atomicAdd(&cnt_s[cube_pad(v)], 1);
+  }
+  lds_barrier();
+  // exclusive scan: thread t owns the contiguous voxels [t * per, t * per + per)
+  const int per = (r3 + kCubeOrderThreads - 1) / kCubeOrderThreads;
+  const int v0 = min(tid * per, r3), v1 = min(v0 + per, r3);
+  int local = 0;
+  for (int v = v0; v < v1; v++) local += cnt_s[cube_pad(v)];
+  const int incl = block_inclusive_scan(local, scan_s);
+  int run = incl - local;
+  for (int v = v0; v < v1; v++) {
+    const int k = cnt_s[cube_pad(v)];
+    cnt_s[cube_pad(v)] = run;
+    run += k;
+  }
+  int* S = seg + (size_t)b * (r3 + 1);
+  if (tid == kCubeOrderThreads - 1) S[r3] = incl;
+  lds_barrier();
+  for (int v = tid; v < r3; v += kCubeOrderThreads) S[v] = cnt_s[cube_pad(v)];
+  lds_barrier();
+  int2* P = pairs + (size_t)b * m;
+  for (int p = tid; p < m; p += kCubeOrderThreads) {
+    const int v = I[p];
+    if (v >= 0 && v < r3) {
+      const int pos = atomicAdd(&cnt_s[cube_pad(v)], 1);
+      P[pos] = make_int2(p % n, __float_as_int(W[p]));
+    }
+  }
+}
+
+// One thread per voxel and G channels.  A voxel's pairs form a dependent
+// chain (pair load -> gradient gathers), so the kernel is bound by chain
+// latency times waves, not by bytes: G = 64 channels per thread quarters the
+// waves of G = 16, and the next pair is loaded while the current pair's G
+// gathers are in flight.
+constexpr int kCubeGatherThreads = 256;
+template <int G>
+__global__ __launch_bounds__(kCubeGatherThreads) void devox_cube_gather_kernel(
+    const float* __restrict__ grad_y, const int* __restrict__ seg, const int2* __restrict__ pairs,
+    int c, int n, int r3, float* __restrict__ grad_x) {
+  const int v = blockIdx.x * kCubeGatherThreads + threadIdx.x;
+  const int c0 = blockIdx.y * G;
+  const int b = blockIdx.z;
+  if (v >= r3) return;
+  const int gcount = min(G, c - c0);
+  const int* S = seg + (size_t)b * (r3 + 1);
+  const int s = S[v], e = S[v + 1];
+  const int2* P = pairs + (size_t)b * 8 * n;
+  const float* gy = grad_y + ((size_t)b * c + c0) * n;
+  float acc[G];
+#pragma unroll
+  for (int g = 0; g < G; g++) acc[g] = 0.0f;
+  int2 nxt = s < e ? P[s] : make_int2(0, 0);
+  for (int j = s; j < e; j++) {
+    const int2 pw = nxt;
+    if (j + 1 < e) nxt = P[j + 1];
+    const float w = __int_as_float(pw.y);
+    float gv[G];
+#pragma unroll
+    for (int g = 0; g < G; g++) gv[g] = g < gcount ? gy[(size_t)g * n + pw.x] : 0.0f;
+#pragma unroll
+    for (int g = 0; g < G; g++) acc[g] += w * gv[g];
+  }
+  float* gx = grad_x + ((size_t)b * c + c0) * r3 + v;
+#pragma unroll
+  for (int g = 0; g < G; g++)
+    if (g < gcount) gx[(size_t)g * r3] = acc[g];
+}
+
+// The same gather with everything it reads in LDS: one workgroup per
+// (cloud, group of kCubeLdsG channels) keeps those gradient rows in LDS and
+// walks the cloud's voxels in chunks of one voxel per thread.  A chunk's seg
+// entries and its contiguous pair range (up to kCubePairCap pairs; a larger
+// range is read from global memory) are loaded into registers one chunk
+// ahead, and the chunk boundaries two chunks ahead, so the global loads of
+// chunk i + 1 are in flight while chunk i sums from LDS and streams its
+// grad_x rows out.  Same pair order, so the same bits as
+// devox_cube_gather_kernel.
+constexpr int kCubeLdsThreads = 1024;
+constexpr int kCubeLdsG = 4;
+constexpr int kCubePairRegs = 4;
+constexpr int kCubePairCap = kCubePairRegs * kCubeLdsThreads;
+__global__ __launch_bounds__(kCubeLdsThreads) void devox_cube_gather_lds_kernel(
+    const float* __restrict__ grad_y, const int* __restrict__ seg, const int2* __restrict__ pairs,
+    int c, int n, int r3, float* __restrict__ grad_x) {
+  extern __shared__ __align__(16) float gy_s[];  // [G][n] | seg [T + 1] | pairs [cap]
+  int* seg_s = (int*)(gy_s + kCubeLdsG * n);
+  int2* pair_s = (int2*)(seg_s + ((kCubeLdsThreads + 2) & ~1));
+  constexpr int T = kCubeLdsThreads;
+  const int c0 = blockIdx.x * kCubeLdsG;
+  const int b = blockIdx.y;
+  const int tid = threadIdx.x;
+  const int gcount = min(kCubeLdsG, c - c0);
+  const float* gy = grad_y + ((size_t)b * c + c0) * n;
+  const int* S = seg + (size_t)b * (r3 + 1);
+  const int2* P = pairs + (size_t)b * 8 * n;
+  float* gx = grad_x + ((size_t)b * c + c0) * r3;
+  // chunk 0 in registers, chunk 1's boundaries
+  int sreg = S[min(tid, r3)];
+  int cur0 = S[0], cur1 = S[min(T, r3)];
+  int nxt0 = cur1, nxt1 = S[min(2 * T, r3)];
+  int2 preg[kCubePairRegs];
+#pragma unroll
+  for (int k = 0; k < kCubePairRegs; k++) {
+    const int t = k * T + tid;
+    preg[k] = (cur1 - cur0 <= kCubePairCap && t < cur1 - cur0) ? P[cur0 + t] : make_int2(0, 0);
+  }
+  for (int t = tid; t < kCubeLdsG * n; t += T) gy_s[t] = t < gcount * n ? gy[t] : 0.0f;
+  for (int v0 = 0; v0 < r3; v0 += T) {
+    __syncthreads();  // the previous chunk's LDS reads are done
+    const int p0 = cur0, np = cur1 - cur0;
+    const bool staged = np <= kCubePairCap;
+    seg_s[tid] = sreg;
+    if (tid == 0) seg_s[T] = cur1;
+#pragma unroll
+    for (int k = 0; k < kCubePairRegs; k++)
+      if (staged && k * T + tid < np) pair_s[k * T + tid] = preg[k];
+    const int vn = v0 + T;
+    if (vn < r3) {  // chunk i + 1 into registers, chunk i + 2's boundaries
+      sreg = S[min(vn + tid, r3)];
+      const int m = nxt1 - nxt0;
+#pragma unroll
+      for (int k = 0; k < kCubePairRegs; k++) {
+        const int t = k * T + tid;
+        if (m <= kCubePairCap && t < m) preg[k] = P[nxt0 + t];
+      }
+      cur0 = nxt0;
+      cur1 = nxt1;
+      nxt0 = nxt1;
+      nxt1 = S[min(vn + 2 * T, r3)];
+    }
+    __syncthreads();
+    const int v = v0 + tid;
+    if (v < r3) {
+      const int s = seg_s[tid], e = seg_s[tid + 1];
+      float acc[kCubeLdsG];
+#pragma unroll
+      for (int g = 0; g < kCubeLdsG; g++) acc[g] = 0.0f;
+      for (int j = s; j < e; j++) {
+        const int2 pw = staged ? pair_s[j - p0] : P[j];
+        const float w = __int_as_float(pw.y);
+#pragma unroll
+        for (int g = 0; g < kCubeLdsG; g++) acc[g] += w * gy_s[g * n + pw.x];
+      }
+#pragma unroll
+      for (int g = 0; g < kCubeLdsG; g++)
+        if (g < gcount) gx[(size_t)g * r3 + v] = acc[g];
+    }
+  }
+}
+static size_t cube_gather_lds_bytes(int n) {
+  return (size_t)kCubeLdsG * n * 4 + ((kCubeLdsThreads + 2) & ~1) * 4 + (size_t)kCubePairCap * 8;
+}
+
 static pcr_status devox_backward(const float* grad_y, const int* inds, const float* wgts, int b,
                                  int c, int n, int r, int skip_neg, float* grad_x,
                                  const int* order, void* stream);
@@ -459,6 +642,18 @@ static pcr_status devox_backward(const float* grad_y, const int* inds, const flo
 extern "C" size_t pcr_devoxelize_backward_workspace_size(int b, int n) {
   if (b <= 0 || n <= 0) return 256;
   return ((size_t)b * n * 4 * 17 + 255) / 256 * 256;
+}
+
+// cube grids up to 32^3 additionally: seg [b][r3 + 1] | pairs [b][8n]
+static size_t cube_seg_bytes(int b, int r3) { return ((size_t)b * (r3 + 1) * 4 + 255) / 256 * 256; }
+static bool cube_gather_ok(int n, int r) {
+  return r >= 1 && r <= 32 && n >= 1 && (int64_t)n * 8 < (1ll << 28);
+}
+extern "C" size_t pcr_devoxelize_backward_workspace_size_r(int b, int n, int r, int spherical) {
+  const size_t base = pcr_devoxelize_backward_workspace_size(b, n);
+  if (spherical || b <= 0 || !cube_gather_ok(n, r)) return base;
+  const size_t cube = cube_seg_bytes(b, r * r * r) + (size_t)b * 8 * n * 8;
+  return cube > base ? cube : base;
 }
 
 extern "C" pcr_status pcr_devoxelize_backward_ws(const float* grad_y, const int* inds,
@@ -480,6 +675,32 @@ extern "C" pcr_status pcr_devoxelize_backward_ws(const float* grad_y, const int*
                        as_stream(stream), inds, wgts, n, npad, ord, sinds, swgts);
     // the backward reads the sorted corner data by position
     return devox_backward(grad_y, sinds, swgts, b, c, n, r, skip_neg, grad_x, ord, stream);
+  }
+  if (!skip_neg && b > 0 && c > 0 && cube_gather_ok(n, r) && workspace &&
+      workspace_bytes >= pcr_devoxelize_backward_workspace_size_r(b, n, r, 0)) {
+    const int r3 = r * r * r;
+    int* seg = (int*)workspace;
+    int2* pairs = (int2*)((char*)workspace + cube_seg_bytes(b, r3));
+    const size_t lds = ((size_t)r3 + (r3 >> 5) + kCubeOrderThreads / kWave + 1) * 4;
+    allow_big_lds(devox_cube_order_kernel, lds);
+    hipLaunchKernelGGL(devox_cube_order_kernel, dim3(b), dim3(kCubeOrderThreads), lds,
+                       as_stream(stream), inds, wgts, n, r3, seg, pairs);
+    const dim3 vb(ceil_div(r3, kCubeGatherThreads));
+    const size_t lds_g = cube_gather_lds_bytes(n);
+    if (lds_g <= 80 * 1024) {
+      allow_big_lds(devox_cube_gather_lds_kernel, lds_g);
+      hipLaunchKernelGGL(devox_cube_gather_lds_kernel, dim3(ceil_div(c, kCubeLdsG), b),
+                         dim3(kCubeLdsThreads), lds_g, as_stream(stream), grad_y, seg, pairs, c,
+                         n, r3, grad_x);
+    } else if (c >= 48)
+      hipLaunchKernelGGL(devox_cube_gather_kernel<64>, dim3(vb.x, ceil_div(c, 64), b),
+                         dim3(kCubeGatherThreads), 0, as_stream(stream), grad_y, seg, pairs, c, n,
+                         r3, grad_x);
+    else
+      hipLaunchKernelGGL(devox_cube_gather_kernel<16>, dim3(vb.x, ceil_div(c, 16), b),
+                         dim3(kCubeGatherThreads), 0, as_stream(stream), grad_y, seg, pairs, c, n,
+                         r3, grad_x);
+    return launch_status("trilinear_devoxelize_backward");
   }
   return devox_backward(grad_y, inds, wgts, b, c, n, r, skip_neg, grad_x, order, stream);
 }

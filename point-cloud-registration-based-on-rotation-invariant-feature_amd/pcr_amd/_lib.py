@@ -43,6 +43,7 @@ SIGNATURES = {
     "pcr_trilinear_devoxelize_forward": (ST, [I, I, P, P, I, I, I, P, P, P, P]),
     "pcr_devoxelize_backward": (ST, [P, P, P, I, I, I, I, I, P, P]),
     "pcr_devoxelize_backward_workspace_size": (SZ, [I, I]),
+    "pcr_devoxelize_backward_workspace_size_r": (SZ, [I, I, I, I]),
     "pcr_devoxelize_backward_ws": (ST, [P, P, P, I, I, I, I, I, P, P, SZ, P]),
     "pcr_dgcnn_center_gather": (ST, [P, P, P, I, I, I, I, P, P]),
     "pcr_extractor_workspace_size": (SZ, [I, I, I, I]),

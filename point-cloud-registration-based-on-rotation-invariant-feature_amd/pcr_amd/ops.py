@@ -301,7 +301,8 @@ def _devox_backward(grad_y, indices, weights, r, spherical, what):
     r = int(r)
     gx = torch.empty((b, c, r * r * r), dtype=torch.float32, device=grad_y.device)
     lib = _lib.load()
-    ws = _workspace(lib.pcr_devoxelize_backward_workspace_size(b, n), grad_y.device)
+    ws = _workspace(lib.pcr_devoxelize_backward_workspace_size_r(b, n, r, int(spherical)),
+                    grad_y.device)
     _lib.check(lib.pcr_devoxelize_backward_ws(
         _ptr(grad_y), _ptr(indices), _ptr(weights), b, c, n, r, int(spherical), _ptr(gx),
         _ptr(ws), ws.numel(), _stream()), what)

@@ -35,6 +35,10 @@ for step in "$@"; do
     knnb) run knn_bench 300 python scripts/knn_bench.py ;;
     overlap) run overlap 300 python scripts/overlap_probe.py ;;
     c5) run c5_time 300 python scripts/c5_time.py ;;
+    cube) run cube_time 300 python scripts/cube_time.py ;;
+    cubebwd) run cube_bwd 300 python scripts/cube_bwd_time.py
+             cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+             run cube_bwd_prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/cubeprof -o run --output-format csv -- python3 scripts/cube_bwd_time.py ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

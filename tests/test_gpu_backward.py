@@ -9,6 +9,11 @@ launch shapes in pcr_devoxelize_backward (csrc/devoxelize.hip):
     channel per workgroup ("lds_whole_grid");
   * r^3 > 32768 (r = 64): a 20k-voxel LDS window plus global atomics for the
     corners past it ("window_atomics").
+With the pcr_devoxelize_backward_workspace_size_r workspace (what ops.py
+passes), r <= 32 instead takes the atomics-free gather: the (point, corner)
+pairs counting-sorted by voxel once per cloud, one thread per voxel
+summing its segment ("voxel_gather"; test_cube_devox_backward_entry_points
+covers both it and the LDS kernel at r = 16 / 32).
 Scatter results are compared against the oracle with the fp32 sum-order
 bound of tests/sumorder.py; the gather backward (avg voxelize) is bit-exact.
 """
@@ -43,7 +48,7 @@ def cube_coords(b, n, r, seed):
     return np.ascontiguousarray(cc)
 
 
-@pytest.mark.parametrize("r,branch", [(16, "lds_whole_grid"), (32, "lds_whole_grid"),
+@pytest.mark.parametrize("r,branch", [(16, "voxel_gather"), (32, "voxel_gather"),
                                       (64, "window_atomics")])
 def test_cube_devox_backward_branches(dev, r, branch):
     from pcr_amd import ops
@@ -209,3 +214,44 @@ def test_cube_devox_forward_row_kernel(dev, r):
     assert np.array_equal(N(inds), ei)
     assert np.array_equal(N(wgts), ew)
     assert np.array_equal(N(outs), eo)
+
+
+@pytest.mark.parametrize("r,n", [(5, 1500), (16, 1500), (32, 1500), (16, 3000)])
+@pytest.mark.parametrize("path", ["lds_atomics", "voxel_gather", "small_ws"])
+def test_cube_devox_backward_entry_points(dev, r, n, path):
+    """Cube grads through the C entry points: pcr_devoxelize_backward (LDS
+    float atomics), pcr_devoxelize_backward_ws with the _size_r workspace
+    (voxel-sorted gather) and with only the (b, n) workspace (falls back to
+    the LDS kernel).  Includes corners outside [0, r^3) (dropped by every
+    path) and a cloud with all points in one cell (one long segment).
+    The gather stages the gradient rows in LDS up to ~2.7k points
+    (devox_cube_gather_lds_kernel, n = 1500) and reads them from global
+    memory beyond (devox_cube_gather_kernel, n = 3000)."""
+    from pcr_amd import _lib
+    from pcr_amd.ops import _ptr, _stream
+    b, c = 3, 19
+    cc = cube_coords(b, n, r, seed=60 + r)
+    cc[2] = (r // 2 + 0.25 + 0.5 * np.random.default_rng(61).uniform(0, 1, (3, n))).astype(
+        np.float32)
+    _, ei, ew = oracle.trilinear_devoxelize_forward(r, cc, np.zeros((b, c, r ** 3), np.float32))
+    ei = ei.copy()
+    ei[0, 3, :7] = r ** 3 + 5
+    ei[1, 6, 10:13] = -4
+    gy = np.random.default_rng(62 + r).standard_normal((b, c, n)).astype(np.float32)
+    tg, ti, tw = T(gy, dev), T(ei, dev), T(ew, dev)
+    gx = torch.full((b, c, r ** 3), float("nan"), device=dev)
+    lib = _lib.load()
+    if path == "lds_atomics":
+        rc = lib.pcr_devoxelize_backward(_ptr(tg), _ptr(ti), _ptr(tw), b, c, n, r, 0, _ptr(gx),
+                                         _stream())
+    else:
+        size = (lib.pcr_devoxelize_backward_workspace_size_r(b, n, r, 0) if path == "voxel_gather"
+                else lib.pcr_devoxelize_backward_workspace_size(b, n))
+        ws = torch.empty(size, dtype=torch.uint8, device=dev)
+        rc = lib.pcr_devoxelize_backward_ws(_ptr(tg), _ptr(ti), _ptr(tw), b, c, n, r, 0,
+                                            _ptr(gx), _ptr(ws), ws.numel(), _stream())
+    _lib.check(rc, "devoxelize_backward")
+    keep = (ei >= 0) & (ei < r ** 3)
+    exp = oracle.devoxelize_backward(gy, np.where(keep, ei, 0), np.where(keep, ew, 0), r,
+                                     spherical=False)
+    assert_within_sum_order(N(gx), exp, devox_backward_bound(gy, ei, ew, r ** 3))
