@@ -551,7 +551,8 @@ __global__ __launch_bounds__(kCubeGatherThreads) void devox_cube_gather_kernel(
 
 // The same gather with everything it reads in LDS: one workgroup per
 // (cloud, group of kCubeLdsG channels) keeps those gradient rows in LDS and
-// walks the cloud's voxels in chunks of one voxel per thread.  A chunk's seg
+// walks the cloud's voxels in chunks of four consecutive voxels per thread
+// (float4 grad_x stores).  A chunk's seg
 // entries and its contiguous pair range (up to kCubePairCap pairs; a larger
 // range is read from global memory) are loaded into registers one chunk
 // ahead, and the chunk boundaries two chunks ahead, so the global loads of
@@ -560,15 +561,20 @@ __global__ __launch_bounds__(kCubeGatherThreads) void devox_cube_gather_kernel(
 // devox_cube_gather_kernel.
 constexpr int kCubeLdsThreads = 1024;
 constexpr int kCubeLdsG = 4;
+constexpr int kCubeVpt = 4;  // voxels per thread: a chunk is 4096 voxels
+constexpr int kCubeChunk = kCubeVpt * kCubeLdsThreads;
 constexpr int kCubePairRegs = 4;
 constexpr int kCubePairCap = kCubePairRegs * kCubeLdsThreads;
 __global__ __launch_bounds__(kCubeLdsThreads) void devox_cube_gather_lds_kernel(
     const float* __restrict__ grad_y, const int* __restrict__ seg, const int2* __restrict__ pairs,
     int c, int n, int r3, float* __restrict__ grad_x) {
-  extern __shared__ __align__(16) float gy_s[];  // [G][n] | seg [T + 1] | pairs [cap]
+  // [G][n] | seg [chunk] (the chunk's end stays in a register) | pairs [cap]:
+  // 80 KB at n = 2048, two workgroups per CU
+  extern __shared__ __align__(16) float gy_s[];
   int* seg_s = (int*)(gy_s + kCubeLdsG * n);
-  int2* pair_s = (int2*)(seg_s + ((kCubeLdsThreads + 2) & ~1));
+  int2* pair_s = (int2*)(seg_s + kCubeChunk);
   constexpr int T = kCubeLdsThreads;
+  constexpr int CH = kCubeChunk;
   const int c0 = blockIdx.x * kCubeLdsG;
   const int b = blockIdx.y;
   const int tid = threadIdx.x;
@@ -577,10 +583,13 @@ __global__ __launch_bounds__(kCubeLdsThreads) void devox_cube_gather_lds_kernel(
   const int* S = seg + (size_t)b * (r3 + 1);
   const int2* P = pairs + (size_t)b * 8 * n;
   float* gx = grad_x + ((size_t)b * c + c0) * r3;
+  const bool vec = (r3 & 3) == 0;
   // chunk 0 in registers, chunk 1's boundaries
-  int sreg = S[min(tid, r3)];
-  int cur0 = S[0], cur1 = S[min(T, r3)];
-  int nxt0 = cur1, nxt1 = S[min(2 * T, r3)];
+  int sreg[kCubeVpt];
+#pragma unroll
+  for (int k = 0; k < kCubeVpt; k++) sreg[k] = S[min(k * T + tid, r3)];
+  int cur0 = S[0], cur1 = S[min(CH, r3)];
+  int nxt0 = cur1, nxt1 = S[min(2 * CH, r3)];
   int2 preg[kCubePairRegs];
 #pragma unroll
   for (int k = 0; k < kCubePairRegs; k++) {
@@ -588,18 +597,19 @@ __global__ __launch_bounds__(kCubeLdsThreads) void devox_cube_gather_lds_kernel(
     preg[k] = (cur1 - cur0 <= kCubePairCap && t < cur1 - cur0) ? P[cur0 + t] : make_int2(0, 0);
   }
   for (int t = tid; t < kCubeLdsG * n; t += T) gy_s[t] = t < gcount * n ? gy[t] : 0.0f;
-  for (int v0 = 0; v0 < r3; v0 += T) {
+  for (int v0 = 0; v0 < r3; v0 += CH) {
     __syncthreads();  // the previous chunk's LDS reads are done
     const int p0 = cur0, np = cur1 - cur0;
     const bool staged = np <= kCubePairCap;
-    seg_s[tid] = sreg;
-    if (tid == 0) seg_s[T] = cur1;
+#pragma unroll
+    for (int k = 0; k < kCubeVpt; k++) seg_s[k * T + tid] = sreg[k];
 #pragma unroll
     for (int k = 0; k < kCubePairRegs; k++)
       if (staged && k * T + tid < np) pair_s[k * T + tid] = preg[k];
-    const int vn = v0 + T;
+    const int vn = v0 + CH;
     if (vn < r3) {  // chunk i + 1 into registers, chunk i + 2's boundaries
-      sreg = S[min(vn + tid, r3)];
+#pragma unroll
+      for (int k = 0; k < kCubeVpt; k++) sreg[k] = S[min(vn + k * T + tid, r3)];
       const int m = nxt1 - nxt0;
 #pragma unroll
       for (int k = 0; k < kCubePairRegs; k++) {
@@ -609,29 +619,43 @@ __global__ __launch_bounds__(kCubeLdsThreads) void devox_cube_gather_lds_kernel(
       cur0 = nxt0;
       cur1 = nxt1;
       nxt0 = nxt1;
-      nxt1 = S[min(vn + 2 * T, r3)];
+      nxt1 = S[min(vn + 2 * CH, r3)];
     }
     __syncthreads();
-    const int v = v0 + tid;
-    if (v < r3) {
-      const int s = seg_s[tid], e = seg_s[tid + 1];
-      float acc[kCubeLdsG];
+    const int vb = v0 + kCubeVpt * tid;  // this thread's 4 consecutive voxels
+    if (vb < r3) {
+      float acc[kCubeVpt][kCubeLdsG];
 #pragma unroll
-      for (int g = 0; g < kCubeLdsG; g++) acc[g] = 0.0f;
-      for (int j = s; j < e; j++) {
-        const int2 pw = staged ? pair_s[j - p0] : P[j];
-        const float w = __int_as_float(pw.y);
+      for (int q = 0; q < kCubeVpt; q++) {
 #pragma unroll
-        for (int g = 0; g < kCubeLdsG; g++) acc[g] += w * gy_s[g * n + pw.x];
+        for (int g = 0; g < kCubeLdsG; g++) acc[q][g] = 0.0f;
+        const int sq = kCubeVpt * tid + q;
+        const int s = seg_s[sq], e = sq + 1 < CH ? seg_s[sq + 1] : p0 + np;
+        for (int j = s; j < e; j++) {
+          const int2 pw = staged ? pair_s[j - p0] : P[j];
+          const float w = __int_as_float(pw.y);
+#pragma unroll
+          for (int g = 0; g < kCubeLdsG; g++) acc[q][g] += w * gy_s[g * n + pw.x];
+        }
       }
+      if (vec) {
 #pragma unroll
-      for (int g = 0; g < kCubeLdsG; g++)
-        if (g < gcount) gx[(size_t)g * r3 + v] = acc[g];
+        for (int g = 0; g < kCubeLdsG; g++)
+          if (g < gcount)
+            *(float4*)(gx + (size_t)g * r3 + vb) =
+                make_float4(acc[0][g], acc[1][g], acc[2][g], acc[3][g]);
+      } else {
+#pragma unroll
+        for (int q = 0; q < kCubeVpt; q++)
+#pragma unroll
+          for (int g = 0; g < kCubeLdsG; g++)
+            if (g < gcount && vb + q < r3) gx[(size_t)g * r3 + vb + q] = acc[q][g];
+      }
     }
   }
 }
 static size_t cube_gather_lds_bytes(int n) {
-  return (size_t)kCubeLdsG * n * 4 + ((kCubeLdsThreads + 2) & ~1) * 4 + (size_t)kCubePairCap * 8;
+  return (size_t)kCubeLdsG * n * 4 + kCubeChunk * 4 + (size_t)kCubePairCap * 8;
 }
 
 static pcr_status devox_backward(const float* grad_y, const int* inds, const float* wgts, int b,
