@@ -559,6 +559,13 @@ __global__ __launch_bounds__(kCubeGatherThreads) void devox_cube_gather_kernel(
 // chunk i + 1 are in flight while chunk i sums from LDS and streams its
 // grad_x rows out.  Same pair order, so the same bits as
 // devox_cube_gather_kernel.
+// Workgroup barrier that waits only for this wave's LDS operations: the
+// compiler's fenced barriers (__syncthreads, and lds_barrier on this
+// toolchain) wait for vmcnt(0), i.e. for every outstanding global load and
+// store, so a prefetch issued before them would be waited for at once.
+__device__ inline void lds_only_barrier() {
+  __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
 constexpr int kCubeLdsThreads = 1024;
 constexpr int kCubeLdsG = 4;
 constexpr int kCubeVpt = 4;  // voxels per thread: a chunk is 4096 voxels
@@ -598,7 +605,7 @@ __global__ __launch_bounds__(kCubeLdsThreads) void devox_cube_gather_lds_kernel(
   }
   for (int t = tid; t < kCubeLdsG * n; t += T) gy_s[t] = t < gcount * n ? gy[t] : 0.0f;
   for (int v0 = 0; v0 < r3; v0 += CH) {
-    __syncthreads();  // the previous chunk's LDS reads are done
+    lds_only_barrier();  // the previous chunk's LDS reads are done
     const int p0 = cur0, np = cur1 - cur0;
     const bool staged = np <= kCubePairCap;
 #pragma unroll
@@ -621,7 +628,7 @@ __global__ __launch_bounds__(kCubeLdsThreads) void devox_cube_gather_lds_kernel(
       nxt0 = nxt1;
       nxt1 = S[min(vn + 2 * CH, r3)];
     }
-    __syncthreads();
+    lds_only_barrier();
     const int vb = v0 + kCubeVpt * tid;  // this thread's 4 consecutive voxels
     if (vb < r3) {
       float acc[kCubeVpt][kCubeLdsG];
@@ -631,11 +638,22 @@ __global__ __launch_bounds__(kCubeLdsThreads) void devox_cube_gather_lds_kernel(
         for (int g = 0; g < kCubeLdsG; g++) acc[q][g] = 0.0f;
         const int sq = kCubeVpt * tid + q;
         const int s = seg_s[sq], e = sq + 1 < CH ? seg_s[sq + 1] : p0 + np;
-        for (int j = s; j < e; j++) {
-          const int2 pw = staged ? pair_s[j - p0] : P[j];
-          const float w = __int_as_float(pw.y);
+        // separate loops: a global pair load in the staged loop would make
+        // every iteration wait for the whole vmcnt (the prefetch included)
+        if (staged) {
+          for (int j = s; j < e; j++) {
+            const int2 pw = pair_s[j - p0];
+            const float w = __int_as_float(pw.y);
 #pragma unroll
-          for (int g = 0; g < kCubeLdsG; g++) acc[q][g] += w * gy_s[g * n + pw.x];
+            for (int g = 0; g < kCubeLdsG; g++) acc[q][g] += w * gy_s[g * n + pw.x];
+          }
+        } else {
+          for (int j = s; j < e; j++) {
+            const int2 pw = P[j];
+            const float w = __int_as_float(pw.y);
+#pragma unroll
+            for (int g = 0; g < kCubeLdsG; g++) acc[q][g] += w * gy_s[g * n + pw.x];
+          }
         }
       }
       if (vec) {
