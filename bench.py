@@ -2,28 +2,42 @@
 """bench.py -- north-star metric of BASELINE.json:
 point-clouds/sec (1024 pts, k=32) PPF + sph-vox forward at 1/2/4/8 MI355X.
 
-One step = one sph-dg extractor forward pass (pcr_amd.extractor.SphExtractor)
-over one batch of synthetic clouds already resident in HBM: self-KNN (k) +
-local PPF, spherical normalisation + voxelisation (dense [B,C,r^3] grid, ind,
-cnt), spherical devoxelisation of that grid and the per-cloud descriptor.
-Workload = BASELINE config 2: batch 32 x 1024 points, k=32, 32^3 spherical
-grid, C=64 channels (PVConv-1 width), per GPU.  Multi-GPU: one process per
-GPU (torch.distributed, RCCL), the batch is sharded by cloud (weak scaling:
-32 clouds per rank) and the per-cloud descriptors are all-gathered every step
-(registration matching), overlapped on a side stream.
+Workloads (one "step" = one pass of the hot path over one batch of synthetic
+clouds already resident in HBM):
 
-Prints ONE JSON line (rank 0).  `roofline` is step level: SURVEY 8d's
-algorithmic bytes of the whole step over ms_per_step against the 8 TB/s HBM
-peak; its `kernel` entry prices the dominant kernel (vox_stream_kernel, the
-dense [B,C,r^3] grid + cnt) from its in-step duration, HIP events on its own
-stream around its launches in the last 10 steps of the timed region.
-`cpu_baseline` times the CPU restatement (oracle/, the "port") on a bounded
-sample of the same workload on this box's host cores, single-thread and on
-every usable core.
+  extract (default, BASELINE c2) -- the sph-dg extractor forward
+      (pcr_amd.extractor.SphExtractor): self-KNN k=32 + local PPF, spherical
+      normalisation + voxelisation (dense [B,C,r^3] grid, ind, cnt),
+      spherical devoxelisation of that grid and the per-cloud descriptor;
+      32 clouds x 1024 points, r=32, C=64 per GPU.
+  pairs (BASELINE c4) -- registration pairs: the same forward over 128
+      source + 128 target clouds per GPU, on-rank mutual-NN matching of each
+      pair's devox features, descriptor all-gather across ranks.
+  c3 (BASELINE c3) -- the path's share of the classify train step: 256 x
+      2048 points, extractor forward + spherical devox backward + spherical
+      vox backward (the gradient chain the reference runs with atomics).
+  c5 (BASELINE c5) -- dense-scan stress: 8 x 65,536 points, k=64, r=64:
+      KNN + local PPF, normalisation, sph voxelize, sph devoxelize.
+
+Multi-GPU: one process per GPU (torch.distributed, RCCL), weak scaling:
+every rank runs its own batch; the only collective is the per-call
+descriptor all-gather (pcr_amd.distributed.DescriptorPipeline, side
+stream), for extract / pairs.  `--gpus N` without torchrun's environment
+starts N ranks itself (torch.distributed.run as a child process; this
+parent never touches the GPU) and fails when fewer than N GPUs are visible.
+
+Prints ONE JSON line (rank 0).  `roofline` is step level: the workload's
+algorithmic bytes (DESIGN.md 4 for the backward terms) over
+ms_per_step against the 8 TB/s HBM peak; its `kernel` entry prices the
+dominant kernel from its in-step duration, HIP events on the stream it runs
+on.  `cpu_baseline` times the CPU restatement (oracle/, the "port") on a
+bounded sample of the same workload on this box's host cores.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -36,26 +50,32 @@ for _p in (ROOT, PKG):
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
+VALU_PEAK_TFLOPS = 157.3   # MI355X fp32 vector peak (packed FMA), SURVEY.md 8d
+METRIC = "point-clouds/sec (1024 pts, k=32) PPF+sph-vox forward"
+
+DEFAULTS = {  # workload: (clouds per GPU, points, k, r, channels)
+    "extract": (32, 1024, 32, 32, 64),
+    "pairs": (256, 1024, 32, 32, 64),
+    "c3": (256, 2048, 32, 32, 64),
+    "c5": (8, 65536, 64, 64, 64),
+}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=40)
-    ap.add_argument("--workload", choices=("extract", "pairs"), default="extract",
-                    help="extract: BASELINE c2, the sph-dg extractor forward over 32 clouds "
-                         "per GPU; pairs: BASELINE c4, 256 clouds (128 registration pairs) "
-                         "per GPU, extractor forward over sources + targets, on-rank mutual-NN "
-                         "matching of their devoxelised features, descriptor all-gather")
-    ap.add_argument("--batch", type=int, default=None,
-                    help="clouds per GPU (default 32 for extract, 256 for pairs)")
-    ap.add_argument("--points", type=int, default=1024)
-    ap.add_argument("--k", type=int, default=32)
-    ap.add_argument("--res", type=int, default=32)
-    ap.add_argument("--channels", type=int, default=64)
-    ap.add_argument("--kernel-iters", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default 200 extract / pairs, 20 c3, 10 c5)")
+    ap.add_argument("--warmup", type=int, default=None,
+                    help="untimed warm-up steps (default 40 extract / pairs, 3 c3 / c5)")
+    ap.add_argument("--workload", choices=tuple(DEFAULTS), default="extract")
+    ap.add_argument("--batch", type=int, default=None, help="clouds per GPU")
+    ap.add_argument("--points", type=int, default=None)
+    ap.add_argument("--k", type=int, default=None)
+    ap.add_argument("--res", type=int, default=None)
+    ap.add_argument("--channels", type=int, default=None)
+    ap.add_argument("--kernel-iters", type=int, default=50, help="(kept for old command lines)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--schedule", type=int, choices=(0, 1, 2), default=1,
@@ -63,21 +83,59 @@ def parse():
                          "(sort+select+PPF / prep+means+devox / dense-grid stream), 2 = as 1 "
                          "with the Morton sort on the prep stream, 0 = two streams")
     ap.add_argument("--no-kernel-timing", action="store_true",
-                    help="diagnostic: no timing events around the grid kernel (no in-step "
-                         "kernel duration; checks the events' own cost)")
+                    help="diagnostic: no timing events around the dominant kernel")
     ap.add_argument("--no-verify", action="store_true",
-                    help="diagnostic: skip the after-run output check (runs that drop launches)")
+                    help="diagnostic: skip the output check before the warm-up")
     ap.add_argument("--steps-per-launch", type=int, default=40,
-                    help="most pipelined steps per native runner call; --steps and --warmup "
-                         "are split into calls of at most this many steps")
-    args = ap.parse_args()
-    if args.batch is None:
-        args.batch = 256 if args.workload == "pairs" else 32
+                    help="most pipelined steps per native runner call (extract / pairs); "
+                         "--steps and --warmup are split into calls of at most this many")
+    args = ap.parse_args(argv)
+    b, n, k, r, c = DEFAULTS[args.workload]
+    args.batch = b if args.batch is None else args.batch
+    args.points = n if args.points is None else args.points
+    args.k = k if args.k is None else args.k
+    args.res = r if args.res is None else args.res
+    args.channels = c if args.channels is None else args.channels
+    heavy = args.workload in ("c3", "c5")
+    if args.steps is None:
+        args.steps = {"c3": 20, "c5": 10}.get(args.workload, 200)
+    if args.warmup is None:
+        args.warmup = 3 if heavy else 40
     if args.workload == "pairs" and args.batch % 2:
         ap.error("--workload pairs needs an even --batch (source + target clouds)")
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
     return args
 
 
+# ------------------------------------------------------------ rank launch
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args, argv):
+    """--gpus N outside torchrun: start N ranks with torch.distributed.run as
+    a child process and return its exit code.  Only torch.cuda.device_count()
+    is called here (it does not initialise the GPU on this image)."""
+    visible = torch.cuda.device_count()
+    if visible < args.gpus:
+        print("bench: --gpus %d needs %d GPUs, but %d %s visible to this process"
+              % (args.gpus, args.gpus, visible, "is" if visible == 1 else "are"),
+              file=sys.stderr, flush=True)
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node=%d" % args.gpus, "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+# ------------------------------------------------------------ inputs
 def synthetic_inputs(b, n, c, device, seed):
     g = torch.Generator(device=device).manual_seed(seed)
     xyz = torch.randn((b, 3, n), generator=g, device=device)
@@ -115,161 +173,396 @@ def usable_cores():
     return aff, "affinity %d CPUs" % aff
 
 
+def _rate(one_batch, clouds_per_batch, seconds, threads):
+    """Clouds per second of one_batch() repeated for about `seconds`."""
+    import oracle
+    oracle.set_num_threads(threads)
+    one_batch()  # warm (page-in, thread pool)
+    done, t0 = 0, time.perf_counter()
+    while True:
+        one_batch()
+        done += clouds_per_batch
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            return done / el, done, el
+
+
 def cpu_baseline(args):
-    """Time the CPU restatement (oracle/pcr_oracle.c, OpenMP across clouds)
-    on repeated batches of the same workload: once on one thread and once on
-    every core this process may run on (len(os.sched_getaffinity(0))), each
-    for about args.cpu_seconds.  The all-core figure is `value`."""
+    """The CPU restatement (oracle/pcr_oracle.c, OpenMP across clouds) on a
+    bounded sample of the workload, once on one thread and once on every
+    core this process may run on; the all-core figure is `value`."""
     import numpy as np
     import oracle
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from clouds import gaussian_clouds
-    # the same workload on a sample batch of at most 32 clouds (16 pairs)
-    b, n, c, k, r = min(args.batch, 32), args.points, args.channels, args.k, args.res
+    n, c, k, r, wl = args.points, args.channels, args.k, args.res, args.workload
+    cores, why = usable_cores()
+    if wl == "c5":
+        # the oracle's reference KNN is O(N^2) per cloud (~50 s for one
+        # 65,536-point cloud on one core): the sample is every stage of the
+        # step for the whole batch, except that the KNN runs for a fixed
+        # subset of Q query points per cloud against the whole cloud; its
+        # time is scaled by N / Q (every query scans all N candidates)
+        b, q = args.batch, 1024
+        xyz, nrm, feat = gaussian_clouds(b, n, seed=0, c=c)
+        sub = np.ascontiguousarray(xyz[:, :, :q])
+
+        def timed(threads):
+            oracle.set_num_threads(threads)
+            t0 = time.perf_counter()
+            _, ki = oracle.knn_dir(sub, xyz, k)
+            t_knn = (time.perf_counter() - t0) * (n / q)
+            t0 = time.perf_counter()
+            oracle.local_ppf(xyz, nrm, sub, np.ascontiguousarray(nrm[:, :, :q]), ki,
+                             kmajor=True, relative=True)
+            t_ppf = (time.perf_counter() - t0) * (n / q)
+            t0 = time.perf_counter()
+            nc = oracle.normalize_sph(xyz)
+            grid, ind, _ = oracle.spherical_avg_voxelize_forward(feat, nc, r)
+            oracle.spherical_trilinear_devoxelize_forward(r, nc, grid, ind)
+            return t_knn + t_ppf + (time.perf_counter() - t0)
+
+        t1 = timed(1)  # one thread runs the clouds one after another
+        tn = timed(cores)
+        return {"value": b / tn, "unit": "point-clouds/sec", "cores": cores, "kind": "port",
+                "single_thread": {"value": b / t1, "cores": 1},
+                "sample": "the whole c5 step for %d clouds (N=%d, k=%d, r=%d, C=%d) except "
+                          "that KNN + local PPF ran for %d of the %d query points per cloud "
+                          "(each query scans all N candidates) and were scaled by N/%d; "
+                          "oracle/pcr_oracle.c, OpenMP over clouds, %s; %s"
+                          % (b, n, k, r, c, q, n, q, cpu_model(), why)}
+    b = min(args.batch, 32 if wl != "c3" else 8)
     xyz, nrm, feat = gaussian_clouds(b, n, seed=0, c=c)
-    pairs = args.workload == "pairs"
+    gy = np.random.default_rng(1).standard_normal((b, c, n)).astype(np.float32)
 
     def one_batch():
         _, ki = oracle.knn_dir(xyz, xyz, k)
         oracle.local_ppf(xyz, nrm, xyz, nrm, ki, kmajor=True, relative=True)
         nc = oracle.normalize_sph(xyz)
-        grid, ind, _ = oracle.spherical_avg_voxelize_forward(feat, nc, r)
-        dv, _, _ = oracle.spherical_trilinear_devoxelize_forward(r, nc, grid, ind)
+        grid, ind, cnt = oracle.spherical_avg_voxelize_forward(feat, nc, r)
+        dv, di, dw = oracle.spherical_trilinear_devoxelize_forward(r, nc, grid, ind)
         dv.max(axis=2)
-        if pairs:
+        if wl == "pairs":
             f = dv.transpose(0, 2, 1)
             oracle.mutual_nn(np.ascontiguousarray(f[:b // 2]), np.ascontiguousarray(f[b // 2:]))
+        if wl == "c3":
+            gg = oracle.devoxelize_backward(gy, di, dw, r, spherical=True)
+            oracle.avg_voxelize_backward(gg, ind, cnt)
 
-    def rate(threads, seconds):
-        oracle.set_num_threads(threads)
-        one_batch()  # warm (page-in, thread pool)
-        done, t0 = 0, time.perf_counter()
-        while True:
-            one_batch()
-            done += b
-            el = time.perf_counter() - t0
-            if el >= seconds:
-                return done / el, done, el
-
-    cores, why = usable_cores()
-    r1, d1, e1 = rate(1, args.cpu_seconds / 2)
-    rn, dn, en = rate(cores, args.cpu_seconds)
+    r1, d1, e1 = _rate(one_batch, b, args.cpu_seconds / 2, 1)
+    rn, dn, en = _rate(one_batch, b, args.cpu_seconds, cores)
     return {"value": rn, "unit": "point-clouds/sec", "cores": cores, "kind": "port",
             "single_thread": {"value": r1, "cores": 1},
-            "sample": "batches of %d clouds (N=%d, k=%d, r=%d, C=%d): %d clouds in %.1f s on "
+            "sample": "batches of %d clouds (N=%d, k=%d, r=%d, C=%d%s): %d clouds in %.1f s on "
                       "1 thread, %d clouds in %.1f s on %d threads; oracle/pcr_oracle.c, "
-                      "OpenMP over clouds, %s; %s" % (b, n, k, r, c, d1, e1, dn, en, cores,
-                                                       cpu_model(), why)}
+                      "OpenMP over clouds, %s; %s"
+                      % (b, n, k, r, c, ", forward + devox / vox backward" if wl == "c3" else "",
+                         d1, e1, dn, en, cores, cpu_model(), why)}
 
 
-def verify_runner(ex, xyz, nrm, feat, args, dev):
-    """Two native-runner steps with the bench's schedule vs one forward():
-    knn_idx, local_ppf, ind, cnt, grid and devox must be identical."""
-    sx = ex.ex if args.workload == "pairs" else ex
-    ref = {k: v.clone() for k, v in sx.forward(xyz, nrm, feat).items()}
-    for t in list(sx.outputs(0).values()) + list(sx.outputs(1).values()):
-        t.view(-1).view(torch.uint8).fill_(0xFF)
-    out = sx.run_native(xyz, nrm, feat, 2, None, schedule=args.schedule)
-    torch.cuda.synchronize(dev)
-    for key in ("knn_idx", "local_ppf", "ind", "cnt", "grid", "devox"):
-        if not torch.equal(out[key], ref[key]) and not torch.allclose(out[key], ref[key],
-                                                                      equal_nan=True):
-            raise SystemExit("bench: runner output %s differs from the single-step path" % key)
-    return True
+# ------------------------------------------------------------ workloads
+class ExtractWorkload:
+    """BASELINE c2 (extract) / c4 (pairs): the native runner enqueues up to
+    S pipelined steps per call; each call's descriptors are all-gathered
+    across ranks by the product pipeline (pcr_amd.distributed)."""
+
+    def __init__(self, args, dev, rank, world):
+        from pcr_amd.extractor import SphExtractor, algorithmic_bytes_per_cloud, \
+            stream_kernel_bytes_per_cloud
+        self.args, self.dev, self.world = args, dev, world
+        b, n, c, k, r = args.batch, args.points, args.channels, args.k, args.res
+        self.b, self.c = b, c
+        xyz, nrm, feat = synthetic_inputs(b, n, c, dev, seed=1234 + rank)
+        if args.workload == "pairs":
+            # targets = sources rotated by a fixed rotation and permuted
+            rot = torch.linalg.qr(torch.randn(3, 3, generator=torch.Generator().manual_seed(7)))[0]
+            rot = rot.to(dev)
+            perm = torch.randperm(n, generator=torch.Generator().manual_seed(8)).to(dev)
+            p = b // 2
+            xyz[p:] = torch.einsum("ij,bjn->bin", rot, xyz[:p])[:, :, perm]
+            nrm[p:] = torch.einsum("ij,bjn->bin", rot, nrm[:p])[:, :, perm]
+            feat[p:] = feat[:p][:, :, perm]
+            from pcr_amd.registration import PairExtractor
+            self.ex = PairExtractor(b // 2, n, c, k, r, device=dev)
+        else:
+            self.ex = SphExtractor(b, n, c, k, r, device=dev)
+        self.inputs = (xyz, nrm, feat)
+        self.S = max(1, args.steps_per_launch)
+        self.desc_steps = {}
+        self.pipe = None
+        if world > 1:
+            from pcr_amd.distributed import DescriptorPipeline
+            self.pipe = DescriptorPipeline([b] * world, c, self.S, dev)
+        self.step_bytes = algorithmic_bytes_per_cloud(n, k, r, c)["total"] * b
+        if args.workload == "pairs":
+            # matching: both clouds' [C, N] features read, corr12 / corr21 /
+            # idx1 / idx2 written (4 x 4N), per pair
+            self.step_bytes += (2 * 4 * c * n + 16 * n) * (b // 2)
+        self.kernel_bytes = stream_kernel_bytes_per_cloud(r, c) * b
+        self.KTIMED = 10
+
+    def chunks(self, total):
+        from pcr_amd.distributed import step_chunks
+        return step_chunks(total, self.S)
+
+    def verify(self):
+        """Two native-runner steps with the bench's schedule vs one forward():
+        knn_idx, local_ppf, ind, cnt, grid and devox must be identical (every
+        runner output poisoned first)."""
+        args = self.args
+        sx = self.ex.ex if args.workload == "pairs" else self.ex
+        xyz, nrm, feat = self.inputs
+        ref = {kk: v.clone() for kk, v in sx.forward(xyz, nrm, feat).items()}
+        for t in list(sx.outputs(0).values()) + list(sx.outputs(1).values()):
+            t.view(-1).view(torch.uint8).fill_(0xFF)
+        out = sx.run_native(xyz, nrm, feat, 2, None, schedule=args.schedule)
+        torch.cuda.synchronize(self.dev)
+        for key in ("knn_idx", "local_ppf", "ind", "cnt", "grid", "devox"):
+            if not torch.equal(out[key], ref[key]) and not torch.allclose(
+                    out[key], ref[key], equal_nan=True):
+                raise SystemExit("bench: runner output %s differs from the single-step path"
+                                 % key)
+        return True
+
+    def prepare_timing(self):
+        if not self.args.no_kernel_timing:
+            # the runner's timing events exist before the timed region
+            # (creating them synchronises the device)
+            self.ex.reserve_timing(self.KTIMED)
+
+    def run(self, steps, timed):
+        """`steps` steps; timed: the last call brackets the grid kernel of its
+        last KTIMED steps with HIP events on its stream (in-step durations)."""
+        from pcr_amd.distributed import run_pipelined
+        xyz, nrm, feat = self.inputs
+        ncalls = len(self.chunks(steps))
+
+        def launch(i, m):
+            if m not in self.desc_steps:
+                self.desc_steps[m] = torch.empty((m, self.b, self.c), device=self.dev)
+            tk = self.KTIMED if (timed and i == ncalls - 1 and
+                                 not self.args.no_kernel_timing) else False
+            self.ex.run_native(xyz, nrm, feat, m, self.desc_steps[m],
+                               schedule=self.args.schedule, timed=tk)
+            return self.desc_steps[m]
+
+        return run_pipelined(steps, self.S, launch, self.pipe)
+
+    def kernel_report(self):
+        ms = self.ex.grid_kernel_times()
+        avg = sum(ms) / len(ms) if ms else float("nan")
+        gbs = self.kernel_bytes / (avg * 1e-3) / 1e9
+        traffic = step_traffic = None
+        a = self.args
+        pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc_path):
+            try:
+                with open(pmc_path) as f:
+                    pm = json.load(f)
+                if pm.get("config") == [a.batch, a.points, a.k, a.res, a.channels]:
+                    traffic = pm.get("grid_kernel_hbm_bytes_per_launch")
+                    step_traffic = pm.get("step_hbm_bytes")
+            except (OSError, ValueError):
+                pass
+        return step_traffic, {
+            "name": "vox_stream_kernel (sph-vox dense grid + cnt from the voxel means)",
+            "bound": "hbm", "avg_ms_in_step": round(avg, 5), "launches_timed": len(ms),
+            "bytes_per_launch": self.kernel_bytes, "achieved": round(gbs, 1),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+            "traffic": traffic}
+
+    def config(self):
+        a = self.args
+        b, n, k, r, c = a.batch, a.points, a.k, a.res, a.channels
+        wl = ("sph-dg extractor forward: self-KNN k=%d + local PPF + sph-vox r=%d^3 + "
+              "sph-devox + descriptor" % (k, r)) if a.workload == "extract" else \
+            ("registration pairs (BASELINE c4): extractor forward over %d source + %d "
+             "target clouds (self-KNN k=%d + local PPF + sph-vox r=%d^3 + sph-devox + "
+             "descriptor), mutual-NN matching of each pair's devox features on-rank, "
+             "descriptor all-gather" % (b // 2, b // 2, k, r))
+        return {"workload": wl, "clouds_per_gpu": b,
+                "pairs_per_gpu": b // 2 if a.workload == "pairs" else None,
+                "points": n, "k": k, "resolution": r, "channels": c,
+                "global_batch": b * self.world,
+                "parallelism": "dp%d (clouds sharded, descriptor all-gather)" % self.world,
+                "schedule": a.schedule,
+                "runner_calls": [len(self.chunks(a.warmup)), len(self.chunks(a.steps))],
+                "steps_per_launch": self.S}
 
 
-def main():
-    args = parse()
+class C3Workload:
+    """BASELINE c3: the path's share of the classify train step at 256 x
+    2048 points.  One step = the extractor forward (one native runner step)
+    + the backward of the spherical devoxelisation (a synthetic upstream
+    gradient [B, C, N] -> gradient grid [B, C, r^3]) + the backward of the
+    spherical voxelisation of that gradient grid (-> [B, C, N]).  Conv3d /
+    MLP layers between them are outside the path."""
+
+    def __init__(self, args, dev, rank, world):
+        from pcr_amd import ops
+        from pcr_amd.extractor import SphExtractor, algorithmic_bytes_per_cloud
+        self.ops = ops
+        self.args, self.dev, self.world = args, dev, world
+        b, n, c, k, r = args.batch, args.points, args.channels, args.k, args.res
+        self.inputs = synthetic_inputs(b, n, c, dev, seed=1234 + rank)
+        g = torch.Generator(device=dev).manual_seed(99 + rank)
+        self.gy = torch.randn((b, c, n), generator=g, device=dev)
+        self.ex = SphExtractor(b, n, c, k, r, device=dev)
+        fwd = algorithmic_bytes_per_cloud(n, k, r, c)["total"]
+        # devox backward: upstream gradient 4CN + corner inds / wgts 64N in,
+        # the dense gradient grid 4C r^3 out (written once); vox backward:
+        # ind 4N + the counts of the points' voxels 4N + the gradient rows of
+        # the occupied voxels (<= 4CN) in, grad_x 4CN out
+        self.devox_bwd_bytes = (4 * c * n + 64 * n + 4 * c * r ** 3) * b
+        vox_bwd = 8 * n + 8 * c * n
+        self.step_bytes = fwd * b + self.devox_bwd_bytes + vox_bwd * b
+        self.t = []
+
+    def verify(self):
+        return None
+
+    def prepare_timing(self):
+        self.ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                   for _ in range(self.args.steps)]
+
+    def run(self, steps, timed):
+        ops, r = self.ops, self.args.res
+        xyz, nrm, feat = self.inputs
+        for s in range(steps):
+            out = self.ex.run_native(xyz, nrm, feat, 1, None, schedule=self.args.schedule)
+            if timed and not self.args.no_kernel_timing:
+                self.ev[s][0].record()
+            gg = ops.spherical_trilinear_devoxelize_backward(self.gy, out["dinds"], out["dwgts"], r)
+            if timed and not self.args.no_kernel_timing:
+                self.ev[s][1].record()
+            ops.spherical_avg_voxelize_backward(gg, out["ind"], out["cnt"])
+        self.timed_steps = steps if timed else 0
+        return steps
+
+    def kernel_report(self):
+        ms = [a.elapsed_time(b) for a, b in self.ev[:self.timed_steps]] \
+            if not self.args.no_kernel_timing else []
+        avg = sum(ms) / len(ms) if ms else float("nan")
+        gbs = self.devox_bwd_bytes / (avg * 1e-3) / 1e9
+        return None, {
+            "name": "spherical devoxelize backward (pcr_devoxelize_backward_ws: corner-set "
+                    "order + gather, dense gradient grid written once)",
+            "bound": "hbm", "avg_ms_in_step": round(avg, 5), "launches_timed": len(ms),
+            "bytes_per_launch": self.devox_bwd_bytes, "achieved": round(gbs, 1),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+            "traffic": None}
+
+    def config(self):
+        a = self.args
+        return {"workload": "BASELINE c3 train step, hot-path share: extractor forward "
+                            "(self-KNN k=%d + local PPF + sph-vox r=%d^3 + sph-devox + "
+                            "descriptor) + sph devox backward + sph vox backward"
+                            % (a.k, a.res),
+                "clouds_per_gpu": a.batch, "points": a.points, "k": a.k,
+                "resolution": a.res, "channels": a.channels,
+                "global_batch": a.batch * self.world,
+                "parallelism": "dp%d (clouds sharded, no collective)" % self.world}
+
+
+class C5Workload:
+    """BASELINE c5: 8 x 65,536 points, k=64, r=64 -- self-KNN + local PPF,
+    spherical normalisation, voxelisation and devoxelisation, each through
+    the torch-level op (ops.*) on the current stream."""
+
+    def __init__(self, args, dev, rank, world):
+        from pcr_amd import ops
+        from pcr_amd.extractor import algorithmic_bytes_per_cloud
+        self.ops = ops
+        self.args, self.dev, self.world = args, dev, world
+        b, n, c, k, r = args.batch, args.points, args.channels, args.k, args.res
+        self.inputs = synthetic_inputs(b, n, c, dev, seed=1234 + rank)
+        self.step_bytes = algorithmic_bytes_per_cloud(n, k, r, c)["total"] * b
+        # brute-force KNN: 9 N^2 fp32 ops per cloud (SURVEY.md 8d)
+        self.knn_ops = 9.0 * n * n * b
+
+    def verify(self):
+        return None
+
+    def prepare_timing(self):
+        self.ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                   for _ in range(self.args.steps)]
+
+    def run(self, steps, timed):
+        ops, a = self.ops, self.args
+        xyz, nrm, feat = self.inputs
+        for s in range(steps):
+            if timed and not a.no_kernel_timing:
+                self.ev[s][0].record()
+            ops.knn_local_ppf(xyz, nrm, a.k)
+            if timed and not a.no_kernel_timing:
+                self.ev[s][1].record()
+            nc = ops.spherical_normalize(xyz)
+            grid, ind, _ = ops.spherical_avg_voxelize_forward(feat, nc, a.res)
+            ops.spherical_trilinear_devoxelize_forward(a.res, True, nc, grid, ind)
+        self.timed_steps = steps if timed else 0
+        return steps
+
+    def kernel_report(self):
+        ms = [x.elapsed_time(y) for x, y in self.ev[:self.timed_steps]] \
+            if not self.args.no_kernel_timing else []
+        avg = sum(ms) / len(ms) if ms else float("nan")
+        tf = self.knn_ops / (avg * 1e-3) / 1e12
+        return None, {
+            "name": "self-KNN k=%d + local PPF (Morton sort + threshold selection + PPF; "
+                    "brute-force-equivalent fp32 ops 9N^2 per cloud)" % self.args.k,
+            "bound": "valu", "avg_ms_in_step": round(avg, 4), "launches_timed": len(ms),
+            "flops_per_launch": self.knn_ops, "achieved": round(tf, 2),
+            "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(tf / VALU_PEAK_TFLOPS, 4),
+            "traffic": None}
+
+    def config(self):
+        a = self.args
+        return {"workload": "BASELINE c5 dense-scan stress: self-KNN k=%d + local PPF + "
+                            "sph normalise + sph-vox r=%d^3 + sph-devox" % (a.k, a.res),
+                "clouds_per_gpu": a.batch, "points": a.points, "k": a.k,
+                "resolution": a.res, "channels": a.channels,
+                "global_batch": a.batch * self.world,
+                "parallelism": "dp%d (clouds sharded, no collective)" % self.world}
+
+
+WORKLOADS = {"extract": ExtractWorkload, "pairs": ExtractWorkload, "c3": C3Workload,
+             "c5": C5Workload}
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args, argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print("bench: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world), file=sys.stderr)
+        return 2
+    if local_rank >= torch.cuda.device_count():
+        print("bench: local rank %d has no GPU (%d visible)" % (local_rank,
+                                                                 torch.cuda.device_count()),
+              file=sys.stderr)
+        return 2
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    from pcr_amd.extractor import (SphExtractor, algorithmic_bytes_per_cloud,
-                                   stream_kernel_bytes_per_cloud)
-    b, n, c, k, r = args.batch, args.points, args.channels, args.k, args.res
-    xyz, nrm, feat = synthetic_inputs(b, n, c, dev, seed=1234 + rank)
-    if args.workload == "pairs":
-        # targets = sources rotated by a fixed rotation and permuted
-        rot = torch.linalg.qr(torch.randn(3, 3, generator=torch.Generator().manual_seed(7)))[0]
-        rot = rot.to(dev)
-        perm = torch.randperm(n, generator=torch.Generator().manual_seed(8)).to(dev)
-        p = b // 2
-        xyz[p:] = torch.einsum("ij,bjn->bin", rot, xyz[:p])[:, :, perm]
-        nrm[p:] = torch.einsum("ij,bjn->bin", rot, nrm[:p])[:, :, perm]
-        feat[p:] = feat[:p][:, :, perm]
-    if args.workload == "pairs":
-        from pcr_amd.registration import PairExtractor
-        ex = PairExtractor(b // 2, n, c, k, r, device=dev)
-    else:
-        ex = SphExtractor(b, n, c, k, r, device=dev)
-
-    # the native runner enqueues up to S pipelined steps per call; the step
-    # counts are split into calls of at most S steps (the last call shorter)
-    S = max(1, args.steps_per_launch)
-
-    def chunks(total):
-        return [min(S, total - i) for i in range(0, total, S)]
-
-    comm = torch.cuda.Stream(device=dev) if world > 1 else None
-    desc_out = [torch.empty((world * S * b, c), device=dev) for _ in range(2)]
-    desc_in = [torch.empty((S * b, c), device=dev) for _ in range(2)]
-    pending = []
-    desc_steps = {m: torch.empty((m, b, c), device=dev) for m in set(chunks(args.steps)) |
-                  set(chunks(args.warmup))}
-
-    def launch(i, m, timed=False):
-        """One native runner call of m steps (call i of a sequence)."""
-        ex.run_native(xyz, nrm, feat, m, desc_steps[m], schedule=args.schedule, timed=timed)
-        src = desc_steps[m].view(m * b, c)
-        if world > 1:
-            # descriptor all-gather of the m batches (registration matching),
-            # overlapped with the next launch on a side stream; double-buffered:
-            # the gather that last read this slot is waited for before the copy
-            slot = i & 1
-            if len(pending) == 2:
-                pending.pop(0).wait()
-            desc_in[slot][:m * b].copy_(src)
-            comm.wait_stream(torch.cuda.current_stream(dev))
-            with torch.cuda.stream(comm):
-                pending.append(dist.all_gather_into_tensor(
-                    desc_out[slot][:world * m * b], desc_in[slot][:m * b], async_op=True))
-
-    # the runner's timing events exist before the timed region (creating them
-    # synchronises the device)
-    # (the grid kernel of the last KTIMED steps of the timed region is timed:
-    # each timing pair costs the step ~1.5%, so not every step carries one)
-    KTIMED = 10
-    if not args.no_kernel_timing:
-        ex.reserve_timing(KTIMED)
-    # before the warm-up, outside the timed region: the runner's outputs are
-    # checked against the single-step (one call per stage) path on the same
-    # inputs, with every runner output poisoned first, so the timed number is
-    # for complete work (the check also brings the GPU up to clock)
-    verified = False if args.no_verify else verify_runner(ex, xyz, nrm, feat, args, dev)
-    for i, m in enumerate(chunks(args.warmup)):
-        launch(i, m)
-    for w in pending:
-        w.wait()
-    pending.clear()
+    wl = WORKLOADS[args.workload](args, dev, rank, world)
+    wl.prepare_timing()
+    # before the warm-up, outside the timed region: the outputs are checked
+    # (extract / pairs: runner vs single-step path, every output poisoned
+    # first), which also brings the GPU up to clock
+    verified = False if args.no_verify else wl.verify()
+    wl.run(args.warmup, timed=False)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    timed_chunks = chunks(args.steps)
-    for i, m in enumerate(timed_chunks):
-        # the last call of the timed region also brackets the grid kernel of
-        # its last KTIMED steps with timing events on its stream (in-step
-        # durations)
-        launch(i, m, timed=KTIMED if (i == len(timed_chunks) - 1 and not args.no_kernel_timing)
-               else False)
-    for w in pending:
-        w.wait()
-    pending.clear()
+    calls = wl.run(args.steps, timed=True)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -280,38 +573,16 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # dominant kernel (the dense-grid stream kernel), in step: HIP events on
-    # the stream it is launched on (ex.s_vox) around each of its launches in
-    # the last runner call of the timed region
-    grid_ms = ex.grid_kernel_times()
-    grid_avg_ms = sum(grid_ms) / len(grid_ms) if grid_ms else float("nan")
-    grid_bytes = stream_kernel_bytes_per_cloud(r, c) * b
-    grid_gbs = grid_bytes / (grid_avg_ms * 1e-3) / 1e9
-    kname = "vox_stream_kernel (sph-vox dense grid + cnt from the voxel means)"
-
-
-    total_clouds = b * world * args.steps
-    value = total_clouds / elapsed
-    step_bytes = algorithmic_bytes_per_cloud(n, k, r, c)["total"] * b
-    if args.workload == "pairs":
-        # matching: both clouds' [C, N] features read, corr12 / corr21 /
-        # idx1 / idx2 written (4 x 4N), per pair
-        step_bytes += (2 * 4 * c * n + 16 * n) * (b // 2)
-    step_gbs = step_bytes * args.steps / elapsed / 1e9
-    traffic = step_traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc_path):
-        try:
-            with open(pmc_path) as f:
-                pm = json.load(f)
-            if pm.get("config") == [b, n, k, r, c]:
-                traffic = pm.get("grid_kernel_hbm_bytes_per_launch")
-                step_traffic = pm.get("step_hbm_bytes")
-        except (OSError, ValueError):
-            traffic = None
-
+    step_traffic, kernel = wl.kernel_report()
+    value = args.batch * world * args.steps / elapsed
+    # per rank: every rank moves its own HBM
+    step_gbs = wl.step_bytes * args.steps / elapsed / 1e9
     result = {
-        "metric": "point-clouds/sec (1024 pts, k=32) PPF+sph-vox forward",
+        "metric": METRIC if args.workload in ("extract", "pairs") else
+        "point-clouds/sec (%d pts, k=%d) %s" % (args.points, args.k,
+                                                "forward+backward hot path (c3)"
+                                                if args.workload == "c3" else
+                                                "KNN+PPF+sph-vox+devox (c5)"),
         "value": round(value, 1),
         "unit": "point-clouds/sec",
         "n_gpus": world,
@@ -324,33 +595,13 @@ def main():
         "dtype": "f32",
         "data": "synthetic (seeded gaussian clouds, unit normals, U(-1,1) features)",
         "outputs_verified": verified,
-        "config": {"workload": ("sph-dg extractor forward: self-KNN k=%d + local PPF + "
-                                "sph-vox r=%d^3 + sph-devox + descriptor" % (k, r))
-                   if args.workload == "extract" else
-                   ("registration pairs (BASELINE c4): extractor forward over %d source + %d "
-                    "target clouds (self-KNN k=%d + local PPF + sph-vox r=%d^3 + sph-devox + "
-                    "descriptor), mutual-NN matching of each pair's devox features on-rank, "
-                    "descriptor all-gather" % (b // 2, b // 2, k, r)),
-                   "clouds_per_gpu": b, "pairs_per_gpu": b // 2 if args.workload == "pairs"
-                   else None, "points": n, "k": k, "resolution": r, "channels": c,
-                   "global_batch": b * world, "parallelism": "dp%d (clouds sharded, "
-                   "descriptor all-gather)" % world, "schedule": args.schedule,
-                   "runner_calls": [len(chunks(args.warmup)), len(timed_chunks)],
-                   "steps_per_launch": S},
-        # step level (the north-star quantity): SURVEY 8d algorithmic bytes of
-        # the whole step / ms_per_step; per rank, since every rank moves its
-        # own HBM
+        "config": wl.config(),
         "roofline": {"bound": "hbm", "achieved": round(step_gbs, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(step_gbs / HBM_PEAK_GBS, 4),
                      "traffic": step_traffic,
                      "level": "step: %d B/cloud x %d clouds per rank / ms_per_step"
-                              % (step_bytes // b, b),
-                     "kernel": {"name": kname, "avg_ms_in_step": round(grid_avg_ms, 5),
-                                "launches_timed": len(grid_ms),
-                                "bytes_per_launch": grid_bytes,
-                                "achieved": round(grid_gbs, 1),
-                                "frac": round(grid_gbs / HBM_PEAK_GBS, 4),
-                                "traffic": traffic}},
+                              % (wl.step_bytes // args.batch, args.batch),
+                     "kernel": kernel},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args)
@@ -361,7 +612,8 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

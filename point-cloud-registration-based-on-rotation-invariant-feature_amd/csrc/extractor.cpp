@@ -69,11 +69,6 @@ pcr_status knn_select_ppf(const pcr_extractor_args* a, int q, bool sorted, hipSt
   if (!sorted)  // no sorted path: the one-call selection + PPF
     return pcr_knn_local_ppf(a->xyz, a->normals, a->b, a->n, a->k, a->relative, a->knn_idx,
                              a->knn_dist, a->local_ppf, a->knn_ws[q], a->knn_ws_bytes, st);
-  static const int fuse = PCR_KNOB("PCR_RUN_FUSE", 0);
-  if (fuse)  // diagnostic: the PPF in the selection's epilogue
-    return pcr_knn_local_ppf_prepared(a->xyz, a->normals, a->b, a->n, a->k, a->relative,
-                                      a->knn_idx, a->knn_dist, a->local_ppf, a->knn_ws[q],
-                                      a->knn_ws_bytes, st);
   PCR_TRY(pcr_knn_local_ppf_prepared(a->xyz, a->normals, a->b, a->n, a->k, a->relative,
                                        a->knn_idx, a->knn_dist, nullptr, a->knn_ws[q],
                                        a->knn_ws_bytes, st));
@@ -200,55 +195,6 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
       continue;
     }
     const int q = s & 1;
-    // diagnostic builds only: PCR_RUN_SKIP drops launches to price each
-    // kernel's share of the step (1 select, 2 PPF, 4 grid stream, 8 prep,
-    // 16 means, 32 sort; 8/16/32 after the first two steps; 64: the grid
-    // stream does not wait for the means event, 128: no stream_done record,
-    // 256: prep does not wait for the slot, 512: PPF on its own stream;
-    // 64-512 break the ordering)
-    static const int skip = PCR_KNOB("PCR_RUN_SKIP", 0);
-    if (skip && schedule == 1) {
-      const bool warm = s >= 2;
-      if (!(warm && (skip & 8))) {
-        if (s >= 2 && !(skip & 256))
-          PCR_HIP(hipStreamWaitEvent(sp, stream_done[q], 0), "slot wait");
-        PCR_TRY(pcr_extractor_voxel_prep(a->xyz, a->b, a->n, a->r, a->norm_coords, a->ind,
-                                           a->dinds[q], a->dwgts[q], a->vox_ws[q],
-                                           a->vox_ws_bytes, sp));
-      }
-      if (!(warm && (skip & 16)))
-        PCR_TRY(pcr_extractor_voxel_means_devox(a->features, a->b, a->c, a->n, a->r, a->devox,
-                                                a->dinds[q], a->dwgts[q], desc, a->vox_ws[q],
-                                                a->vox_ws_bytes, sp));
-      PCR_HIP(hipEventRecord(means_done[q], sp), "means record");
-      if (!(skip & 64)) PCR_HIP(hipStreamWaitEvent(sv, means_done[q], 0), "means wait");
-      if (s >= t_first) PCR_HIP(hipEventRecord(rn->t0[s - t_first], sv), "timing record");
-      if (!(skip & 4))
-        PCR_TRY(pcr_extractor_voxel_stream(a->b, a->c, a->n, a->r, a->cnt, a->grid,
-                                           a->vox_ws[q], a->vox_ws_bytes, sv));
-      if (s >= t_first) PCR_HIP(hipEventRecord(rn->t1[s - t_first], sv), "timing record");
-      if (!(skip & 128)) PCR_HIP(hipEventRecord(stream_done[q], sv), "stream record");
-      // 1024: sort and PPF on `origin` with no waits (the selection alone on
-      // s_nbr; timing only, breaks the ordering)
-      if (!(warm && (skip & 32))) PCR_TRY(knn_sort(a, 0, (skip & 1024) && warm ? org : sn, &sorted));
-      else sorted = true;
-      if (!(skip & 1))
-        PCR_TRY(pcr_knn_local_ppf_prepared(a->xyz, a->normals, a->b, a->n, a->k, a->relative,
-                                           a->knn_idx, a->knn_dist, nullptr, a->knn_ws[0],
-                                           a->knn_ws_bytes, sn));
-      // 512: the PPF on `origin` after the selection's event (timing only:
-      // the next selection may overwrite the indices it reads)
-      hipStream_t sppf = (skip & 1024) && warm ? org : sn;
-      if (skip & 512) {
-        PCR_HIP(hipEventRecord(sel_done[q], sn), "select record");
-        PCR_HIP(hipStreamWaitEvent(org, sel_done[q], 0), "select wait");
-        sppf = org;
-      }
-      if (!(skip & 2))
-        PCR_TRY(pcr_local_ppf_forward(a->xyz, a->normals, a->xyz, a->normals, a->knn_idx, a->b,
-                                      a->n, a->n, a->k, 1, a->relative, a->local_ppf, sppf));
-      continue;
-    }
     if (schedule == 2) {
       if (s >= 2) PCR_HIP(hipStreamWaitEvent(sp, sel_done[q], 0), "knn slot wait");
       PCR_TRY(knn_sort(a, q, sp, &sorted));

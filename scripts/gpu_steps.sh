@@ -4,7 +4,8 @@
 # signal or timeout (anything else non-zero) stops the script: nothing more
 # touches the GPU after a fault.
 #   usage: scripts/gpu_steps.sh <step> [<step> ...]
-#   steps: smoke tests tests_all large c5 bench bench_drv prof pmc
+#   steps: smoke tests tests_all large c5 bench bench_drv bench_c3 bench_c5 bench_pairs
+#          prof prof_c3 prof_c5 pmc
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
@@ -26,6 +27,13 @@ for step in "$@"; do
     tests_all) run pytest_gpu 1200 python -m pytest tests -q -m gpu -p no:cacheprovider ;;
     bench) run bench 600 python bench.py ;;
     bench_drv) run bench_drv 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
+    bench_c3) run bench_c3 600 python bench.py --workload c3 ;;
+    bench_c5) run bench_c5 600 python bench.py --workload c5 ;;
+    bench_pairs) run bench_pairs 300 python bench.py --workload pairs --no-cpu-baseline ;;
+    prof_c3) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+          run rocprof_c3 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c3 -o run --output-format csv -- python3 bench.py --workload c3 --steps 10 --no-cpu-baseline ;;
+    prof_c5) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+          run rocprof_c5 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c5 -o run --output-format csv -- python3 bench.py --workload c5 --steps 5 --no-cpu-baseline ;;
     prof) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
           run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 80 --warmup 40 --no-cpu-baseline ;;
     pmc)  run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 5 --warmup 5 --steps-per-launch 5 --kernel-iters 5 --no-cpu-baseline
