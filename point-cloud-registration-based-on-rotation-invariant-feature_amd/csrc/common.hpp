@@ -133,15 +133,25 @@ __device__ inline bool diag_prio(int slot) {
 #define PCR_PRIO(slot) false
 #endif
 
-// Workgroup barrier that orders LDS only.  __syncthreads() also waits for the
-// thread's outstanding global stores (vmcnt(0)) before the barrier, so a
-// barrier after a burst of global writes stalls on their completion; this one
-// does not.  Use it only where threads exchange data through LDS, never
-// through global memory.
+// Workgroup barrier with LDS-scope fences.  On this toolchain (ROCm 7.2,
+// gfx950) it still compiles to s_waitcnt vmcnt(0) lgkmcnt(0) before the
+// s_barrier, exactly like __syncthreads(): every outstanding global load and
+// store of the wave is waited for.  Where a kernel keeps global prefetches or
+// stores in flight across a barrier it uses lds_only_barrier() below.
 __device__ inline void lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// Workgroup barrier that waits only for this wave's LDS operations
+// (s_waitcnt lgkmcnt(0); s_barrier; vmcnt and expcnt at their maxima, gfx9
+// encoding): outstanding global loads, stores and LDS-DMA transfers stay in
+// flight.  Only for data exchanged through LDS; an LDS-DMA target must be
+// waited for with vmcnt by the issuing wave before the barrier.
+__device__ inline void lds_only_barrier() {
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_s_barrier();
 }
 
 // Inclusive block-wide scan of one int per thread (blockDim.x threads,

@@ -110,7 +110,9 @@ __global__ __launch_bounds__(kFwdRowThreads) void devox_fwd_cube_row_kernel(
   const int tid = threadIdx.x;
   const int r3 = r * r * r;
   const float* f = feat + ((size_t)b * c + j) * r3;
-  if ((r3 & 3) == 0) {
+  // 16-byte loads only when every row starts 16-byte aligned (the C ABI
+  // accepts any 4-byte-aligned features pointer)
+  if ((r3 & 3) == 0 && (reinterpret_cast<uintptr_t>(feat) & 15) == 0) {
     const float4* f4 = (const float4*)f;
     float4* s4 = (float4*)row_s;
     for (int t = tid; t < (r3 >> 2); t += kFwdRowThreads) s4[t] = f4[t];
@@ -500,13 +502,33 @@ __global__ __launch_bounds__(kCubeOrderThreads) void devox_cube_order_kernel(
   lds_barrier();
   for (int v = tid; v < r3; v += kCubeOrderThreads) S[v] = cnt_s[cube_pad(v)];
   lds_barrier();
+  // placement by wave 0 alone, pairs in ascending order: one wave's LDS
+  // atomics complete in issue order, and the lanes of one instruction that
+  // hit the same counter are served in the LDS unit's fixed order, so every
+  // voxel's pairs land in the same order on every run -- the same summation
+  // order, hence the same bits.  (Placement atomics from 16 waves raced for a voxel's slots, and
+  // the gather's sum order changed from run to run.)  Eight pairs per lane
+  // per round: their loads are issued together and their atomics back to
+  // back, so the round trip is paid once per 512 pairs.
+  if (tid >= kWave) return;
   int2* P = pairs + (size_t)b * m;
-  for (int p = tid; p < m; p += kCubeOrderThreads) {
-    const int v = I[p];
-    if (v >= 0 && v < r3) {
-      const int pos = atomicAdd(&cnt_s[cube_pad(v)], 1);
-      P[pos] = make_int2(p % n, __float_as_int(W[p]));
+  constexpr int U = 8;
+  for (int p0 = 0; p0 < m; p0 += U * kWave) {
+    int v[U];
+    float w[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int p = p0 + u * kWave + tid;
+      v[u] = p < m ? I[p] : -1;
+      w[u] = p < m ? W[p] : 0.0f;
     }
+    int pos[U];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      pos[u] = (v[u] >= 0 && v[u] < r3) ? atomicAdd(&cnt_s[cube_pad(v[u])], 1) : -1;
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if (pos[u] >= 0) P[pos[u]] = make_int2((p0 + u * kWave + tid) % n, __float_as_int(w[u]));
   }
 }
 
@@ -559,13 +581,6 @@ __global__ __launch_bounds__(kCubeGatherThreads) void devox_cube_gather_kernel(
 // chunk i + 1 are in flight while chunk i sums from LDS and streams its
 // grad_x rows out.  Same pair order, so the same bits as
 // devox_cube_gather_kernel.
-// Workgroup barrier that waits only for this wave's LDS operations: the
-// compiler's fenced barriers (__syncthreads, and lds_barrier on this
-// toolchain) wait for vmcnt(0), i.e. for every outstanding global load and
-// store, so a prefetch issued before them would be waited for at once.
-__device__ inline void lds_only_barrier() {
-  __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
 constexpr int kCubeLdsThreads = 1024;
 constexpr int kCubeLdsG = 4;
 constexpr int kCubeVpt = 4;  // voxels per thread: a chunk is 4096 voxels

@@ -891,12 +891,6 @@ __device__ inline void wait_vmcnt() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
-// workgroup barrier after this wave's LDS operations (lgkmcnt(0)); outstanding
-// stores and LDS-DMA loads stay in flight
-__device__ inline void lds_only_barrier() {
-  __builtin_amdgcn_s_waitcnt(0xC07F);
-  __builtin_amdgcn_s_barrier();
-}
 
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 template <int NS, int NB, int U, int AUX, int G = kStreamG, int NG = kStreamNG>

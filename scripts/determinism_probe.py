@@ -1,8 +1,9 @@
 """Diagnostic: runs the extractor forward (c2 shape and the c3 per-cloud shape),
-the one-call KNN + local PPF, ball query and the voxelize forwards many times on
-the same inputs and reports any output that is not bit-identical to the first
-run (every forward output here has a fixed summation order, so any difference
-is a race).  usage: python scripts/determinism_probe.py [reps]"""
+the one-call KNN + local PPF, ball query, the voxelize forwards and the
+devoxelize / voxelize backwards (spherical and cube) many times on the same
+inputs and reports any output that is not bit-identical to the first run
+(every output here has a fixed summation order, so any difference is a
+race).  usage: python scripts/determinism_probe.py [reps]"""
 import os
 import sys
 
@@ -44,5 +45,16 @@ for b, n in ((32, 1024), (8, 2048)):
     nc = ops.spherical_normalize(xyz)
     total += probe("sph voxelize %dx%d" % (b, n),
                    lambda: list(ops.spherical_avg_voxelize_forward(feat, nc, 32)))
+    grid, ind, cnt = ops.spherical_avg_voxelize_forward(feat, nc, 32)
+    _, dinds, dwgts = ops.spherical_trilinear_devoxelize_forward(32, True, nc, grid, ind)
+    gy = torch.randn(feat.shape, generator=torch.Generator(device=dev).manual_seed(3), device=dev)
+    total += probe("sph devox backward %dx%d" % (b, n),
+                   lambda: [ops.spherical_trilinear_devoxelize_backward(gy, dinds, dwgts, 32)])
+    total += probe("sph vox backward %dx%d" % (b, n),
+                   lambda: [ops.spherical_avg_voxelize_backward(grid, ind, cnt)])
+    cc = ((xyz - xyz.mean(2, keepdim=True) + 1) / 2 * 32).clamp(0, 31).contiguous()
+    _, cinds, cwgts = ops.trilinear_devoxelize_forward(32, True, cc, grid)
+    total += probe("cube devox backward %dx%d" % (b, n),
+                   lambda: [ops.trilinear_devoxelize_backward(gy, cinds, cwgts, 32)])
 print("total differing runs:", total)
 sys.exit(1 if total else 0)

@@ -52,3 +52,56 @@ def assert_within_sum_order(got, exp, bound, floor=0.0):
     assert excess.max(initial=-1.0) <= 0, (
         "sum-order bound exceeded at %s: |diff| %.3g > bound %.3g"
         % (worst, diff[worst], bound[worst] + floor))
+
+
+def _bound(S, M):
+    return 2.0 * gamma(np.maximum(M - 1, 0)) * S
+
+
+def knn_backward_bound(x1, x2, gd1, gd2, idx1, idx2):
+    """Per-element bounds ([b, c, n], [b, c, m]) for knn_backward_cuda
+    (knn.cu:52-78, both launches of knn_grad_kernel): for every (query i,
+    slot q) with g = 2 gd[q, i] < 20000 the term t_p = g (x1[p, i] -
+    x2[p, id]) is added to grad1[p, i] and subtracted from grad2[p, id]; the
+    second launch swaps the roles.  Every output element is a sum of such
+    terms in atomic order."""
+    x1 = np.asarray(x1, np.float32)
+    x2 = np.asarray(x2, np.float32)
+    b, c, n = x1.shape
+    m = x2.shape[2]
+    S1 = np.zeros((b, c, n), np.float64)
+    S2 = np.zeros((b, c, m), np.float64)
+    M1 = np.zeros((b, 1, n), np.int64)
+    M2 = np.zeros((b, 1, m), np.int64)
+
+    def direction(xa, xb, gd, idx, Sa, Sb, Ma, Mb, na):
+        for bi in range(b):
+            g = (np.asarray(gd[bi], np.float32) * np.float32(2)).astype(np.float32)  # [k, na]
+            ok = g < np.float32(20000)
+            for q in range(g.shape[0]):
+                sel = np.nonzero(ok[q])[0]
+                ids = np.asarray(idx[bi, q], np.int64)[sel]
+                d = (xa[bi][:, sel] - xb[bi][:, ids]).astype(np.float32)
+                t = np.abs((g[q, sel][None, :] * d).astype(np.float32)).astype(np.float64)
+                Sa[bi][:, sel] += t
+                Ma[bi][0, sel] += 1
+                np.add.at(Sb[bi], (slice(None), ids), t)
+                np.add.at(Mb[bi][0], ids, 1)
+
+    direction(x1, x2, gd1, idx1, S1, S2, M1, M2, n)
+    direction(x2, x1, gd2, idx2, S2, S1, M2, M1, m)
+    return _bound(S1, M1), _bound(S2, M2)
+
+
+def grouping_backward_bound(grad_y, idx, n):
+    """Per-element bound [b, c, n] for grouping_backward (grouping.cu:58-77):
+    grad_x[c, idx[m, u]] += grad_y[c, m, u]."""
+    grad_y = np.asarray(grad_y, np.float32)
+    b, c, m, u = grad_y.shape
+    S = np.zeros((b, c, n), np.float64)
+    M = np.zeros((b, 1, n), np.int64)
+    for bi in range(b):
+        ids = np.asarray(idx[bi], np.int64).reshape(-1)
+        np.add.at(S[bi], (slice(None), ids), np.abs(grad_y[bi].reshape(c, -1)).astype(np.float64))
+        np.add.at(M[bi][0], ids, 1)
+    return _bound(S, M)

@@ -216,7 +216,7 @@ def test_cube_devox_forward_row_kernel(dev, r):
     assert np.array_equal(N(outs), eo)
 
 
-@pytest.mark.parametrize("r,n", [(5, 1500), (16, 1500), (32, 1500), (16, 3000)])
+@pytest.mark.parametrize("r,n", [(5, 1500), (16, 1500), (32, 1500), (16, 3000), (24, 600)])
 @pytest.mark.parametrize("path", ["lds_atomics", "voxel_gather", "small_ws"])
 def test_cube_devox_backward_entry_points(dev, r, n, path):
     """Cube grads through the C entry points: pcr_devoxelize_backward (LDS
@@ -245,8 +245,17 @@ def test_cube_devox_backward_entry_points(dev, r, n, path):
         rc = lib.pcr_devoxelize_backward(_ptr(tg), _ptr(ti), _ptr(tw), b, c, n, r, 0, _ptr(gx),
                                          _stream())
     else:
-        size = (lib.pcr_devoxelize_backward_workspace_size_r(b, n, r, 0) if path == "voxel_gather"
-                else lib.pcr_devoxelize_backward_workspace_size(b, n))
+        size_r = lib.pcr_devoxelize_backward_workspace_size_r(b, n, r, 0)
+        base = lib.pcr_devoxelize_backward_workspace_size(b, n)
+        if path == "voxel_gather":
+            size = size_r
+        else:
+            # just below what the gather needs, so the call must take the LDS
+            # kernel (at r = 5 the gather needs less than the base size, so
+            # no valid workspace can force the fallback there)
+            if size_r - 256 < base:
+                pytest.skip("r=%d n=%d: the gather fits in the base workspace" % (r, n))
+            size = size_r - 256
         ws = torch.empty(size, dtype=torch.uint8, device=dev)
         rc = lib.pcr_devoxelize_backward_ws(_ptr(tg), _ptr(ti), _ptr(tw), b, c, n, r, 0,
                                             _ptr(gx), _ptr(ws), ws.numel(), _stream())
@@ -255,3 +264,18 @@ def test_cube_devox_backward_entry_points(dev, r, n, path):
     exp = oracle.devoxelize_backward(gy, np.where(keep, ei, 0), np.where(keep, ew, 0), r,
                                      spherical=False)
     assert_within_sum_order(N(gx), exp, devox_backward_bound(gy, ei, ew, r ** 3))
+
+
+def test_cube_devox_backward_bitwise_repeatable(dev):
+    """The cube gather's pairs are placed by one wave in a fixed order
+    (devox_cube_order_kernel), so the gradient grid is bit-identical from run
+    to run at the c3 cube shape (one cloud's worth of waves per workgroup)."""
+    from pcr_amd import ops
+    b, n, c, r = 16, 2048, 64, 32
+    cc = cube_coords(b, n, r, seed=70)
+    _, ei, ew = oracle.trilinear_devoxelize_forward(r, cc, np.zeros((b, c, r ** 3), np.float32))
+    gy = T(np.random.default_rng(71).standard_normal((b, c, n)).astype(np.float32), dev)
+    ti, tw = T(ei, dev), T(ew, dev)
+    ref = ops.trilinear_devoxelize_backward(gy, ti, tw, r).clone()
+    for _ in range(10):
+        assert torch.equal(ops.trilinear_devoxelize_backward(gy, ti, tw, r), ref)

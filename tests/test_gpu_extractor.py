@@ -187,3 +187,38 @@ def test_device_math_bit_exact(dev):
                                      ti.data_ptr(), s), "st")
     assert np.array_equal(N(ti), oracle.sph_index(nc, 32))
     del ctypes
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_extractor_ind_vs_reference_fp32_normalisation(dev, seed):
+    """BASELINE c2 (32 x 1024, r = 32): the extractor's voxel indices (its
+    fixed-order fp64 normalisation) against the spherical voxelisation of
+    the coords the reference's Spherical_Voxelization.forward produces with
+    torch fp32 on the GPU (PVCNN/modules/spherical_vox.py:17-19).  Every
+    point in a different voxel must sit on a bin edge (tests/edges.py); the
+    count is printed."""
+    import edges
+    from pcr_amd import ops
+    from pcr_amd.extractor import SphExtractor
+    b, n, c, k, r = 32, 1024, 64, 32, 32
+    xyz, nrm, feat = gaussian_clouds(b, n, seed=seed, c=c)
+    tx, tn, tf = T(xyz, dev), T(nrm, dev), T(feat, dev)
+    ex = SphExtractor(b, n, c, k, r, device=dev)
+    out = ex.forward(tx, tn, tf)
+    ind_ext, nc_ext = N(out["ind"]).copy(), N(out["norm_coords"]).copy()
+    nc_ref = tx - tx.mean(2, keepdim=True)
+    nc_ref = nc_ref / (nc_ref.norm(dim=1, keepdim=True).max(dim=2, keepdim=True).values + 1e-20)
+    nc_ref = nc_ref.contiguous()
+    _, ind_ref, _ = ops.spherical_avg_voxelize_forward(tf, nc_ref, r)
+    torch.cuda.synchronize()
+    ind_ref, nc_ref = N(ind_ref), N(nc_ref)
+    assert np.abs(nc_ext - nc_ref).max() <= 1e-6
+    total = 0
+    for i in range(b):
+        d, e, worst = edges.explain(nc_ext[i], nc_ref[i], ind_ext[i], ind_ref[i], r)
+        total += d
+        assert d == e, "cloud %d: %d indices differ, %d on a bin edge (worst %.3g)" % (i, d, e,
+                                                                                      worst)
+    print("c2 seed %d: %d of %d points in a different voxel than under the reference's "
+          "torch-fp32 normalisation, all on bin edges" % (seed, total, b * n))
+    assert total <= b * n // 1000

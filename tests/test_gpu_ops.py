@@ -10,7 +10,8 @@ import torch
 
 import oracle
 from clouds import gaussian_clouds, edge_norm_coords
-from sumorder import assert_within_sum_order, devox_backward_bound
+from sumorder import (assert_within_sum_order, devox_backward_bound, grouping_backward_bound,
+                      knn_backward_bound)
 
 pytestmark = pytest.mark.gpu
 
@@ -107,10 +108,12 @@ def test_sph_devox_golden(dev):
 def test_sph_devox_backward(dev):
     from pcr_amd import ops
     g = GOLDEN
+    r = int(g["svox_r"])
     gx = ops.spherical_trilinear_devoxelize_backward(
-        T(g["sdevox_grad_y"], dev), T(g["sdevox_inds"], dev), T(g["sdevox_wgts"], dev),
-        int(g["svox_r"]))
-    close(N(gx), g["sdevox_grad_x"], 1e-4, SCATTER_RTOL)
+        T(g["sdevox_grad_y"], dev), T(g["sdevox_inds"], dev), T(g["sdevox_wgts"], dev), r)
+    bound = devox_backward_bound(g["sdevox_grad_y"], g["sdevox_inds"], g["sdevox_wgts"], r ** 3,
+                                 skip_neg=True)
+    assert_within_sum_order(N(gx), g["sdevox_grad_x"], bound)
 
 
 def test_cube_devox_golden(dev):
@@ -123,7 +126,8 @@ def test_cube_devox_golden(dev):
     assert np.array_equal(N(wgts), g["cdevox_wgts"])
     close(N(outs), g["cdevox_outs"])
     gx = ops.trilinear_devoxelize_backward(T(g["cdevox_grad_y"], dev), inds, wgts, rc)
-    close(N(gx), g["cdevox_grad_x"], 1e-4, SCATTER_RTOL)
+    bound = devox_backward_bound(g["cdevox_grad_y"], g["cdevox_inds"], g["cdevox_wgts"], rc ** 3)
+    assert_within_sum_order(N(gx), g["cdevox_grad_x"], bound)
 
 
 @pytest.mark.parametrize("b,n,c,r", [(4, 1024, 64, 32), (2, 2048, 16, 16)])
@@ -194,8 +198,33 @@ def test_knn_backward(dev):
     g = GOLDEN
     g1, g2 = ops.knn_backward_cuda(T(g["knn_x1"], dev), T(g["knn_x2"], dev), T(g["knn_gd1"], dev),
                                    T(g["knn_gd2"], dev), T(g["knn_i1"], dev), T(g["knn_i2"], dev))
-    close(N(g1), g["knn_g1"], 1e-4)
-    close(N(g2), g["knn_g2"], 1e-4)
+    b1, b2 = knn_backward_bound(g["knn_x1"], g["knn_x2"], g["knn_gd1"], g["knn_gd2"],
+                                g["knn_i1"], g["knn_i2"])
+    assert_within_sum_order(N(g1), g["knn_g1"], b1)
+    assert_within_sum_order(N(g2), g["knn_g2"], b2)
+
+
+@pytest.mark.parametrize("self_knn", [True, False])
+def test_knn_backward_c2_shape(dev, self_knn):
+    """knn_backward_cuda at the c2 shape (B=4, N=M=1024, k=32) against the
+    oracle (ascending order) under the per-element sum-order bound; some
+    gradients at the reference's skip value (2 gd >= 20000, knn.cu:68)."""
+    from pcr_amd import ops
+    b, n, k = 4, 1024, 32
+    x1, _, _ = gaussian_clouds(b, n, seed=21)
+    x2 = x1 if self_knn else gaussian_clouds(b, n, seed=22)[0]
+    _, _, i1, i2 = oracle.knn_forward(x1, x2, k)
+    rng = np.random.default_rng(23)
+    gd1 = rng.standard_normal((b, k, n)).astype(np.float32)
+    gd2 = rng.standard_normal((b, k, n)).astype(np.float32)
+    gd1[:, -1, ::7] = 10000.0
+    gd2[:, 0, ::5] = 10000.0
+    g1, g2 = ops.knn_backward_cuda(T(x1, dev), T(x2, dev), T(gd1, dev), T(gd2, dev),
+                                   T(i1, dev), T(i2, dev))
+    e1, e2 = oracle.knn_backward(x1, x2, gd1, gd2, i1, i2)
+    b1, b2 = knn_backward_bound(x1, x2, gd1, gd2, i1, i2)
+    assert_within_sum_order(N(g1), e1, b1)
+    assert_within_sum_order(N(g2), e2, b2)
 
 
 # ------------------------------------------------ ball query / grouping / PPF
@@ -208,7 +237,23 @@ def test_ball_query_grouping(dev):
     grp = ops.grouping_forward(pts, idx)
     assert np.array_equal(N(grp), g["bq_grouped"])
     gx = ops.grouping_backward(T(g["grp_grad_y"], dev), idx, pts.shape[2])
-    close(N(gx), g["grp_grad_x"], 1e-4, SCATTER_RTOL)
+    bound = grouping_backward_bound(g["grp_grad_y"], g["bq_idx"], pts.shape[2])
+    assert_within_sum_order(N(gx), g["grp_grad_x"], bound)
+
+
+def test_grouping_backward_model_shape(dev):
+    """grouping_backward at the sph-dg model's ball query (u = 128, radius
+    0.3) on 2048-point clouds (c3) against the oracle under the sum-order
+    bound: the hot points receive up to hundreds of terms."""
+    from pcr_amd import ops
+    b, n, u, c = 2, 2048, 128, 6
+    xyz, _, _ = gaussian_clouds(b, n, seed=31)
+    xyz = (xyz / np.abs(xyz).max()).astype(np.float32)
+    idx = oracle.ball_query(xyz, xyz, 0.3, u)
+    gy = np.random.default_rng(32).standard_normal((b, c, n, u)).astype(np.float32)
+    gx = ops.grouping_backward(T(gy, dev), T(idx, dev), n)
+    exp = oracle.grouping_backward(gy, idx, n)
+    assert_within_sum_order(N(gx), exp, grouping_backward_bound(gy, idx, n))
 
 
 def test_ball_query_large(dev):
