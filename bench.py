@@ -392,7 +392,7 @@ class ExtractWorkload:
 
 class C3Workload:
     """BASELINE c3: the path's share of the classify train step at 256 x
-    2048 points.  One step = the extractor forward (one native runner step)
+    2048 points.  One step = the extractor forward (SphExtractor.forward)
     + the backward of the spherical devoxelisation (a synthetic upstream
     gradient [B, C, N] -> gradient grid [B, C, r^3]) + the backward of the
     spherical voxelisation of that gradient grid (-> [B, C, N]).  Conv3d /
@@ -429,7 +429,9 @@ class C3Workload:
         ops, r = self.ops, self.args.res
         xyz, nrm, feat = self.inputs
         for s in range(steps):
-            out = self.ex.run_native(xyz, nrm, feat, 1, None, schedule=self.args.schedule)
+            # one step through the extractor's stage kernels (the native runner's
+            # split grid-stream kernel is built for N <= 1024)
+            out = self.ex.forward(xyz, nrm, feat)
             if timed and not self.args.no_kernel_timing:
                 self.ev[s][0].record()
             gg = ops.spherical_trilinear_devoxelize_backward(self.gy, out["dinds"], out["dwgts"], r)

@@ -93,6 +93,118 @@ __global__ __launch_bounds__(256) void devox_fwd_kernel(const float* __restrict_
   }
 }
 
+// Spherical forward with the corner voxels in LDS.  Every corner of a
+// valid point lies in a fixed set of 80 voxels (spherical_trilinear_devox.cu:
+// 67-105: gama_lo = (pos / r^2) / r is integer division, so 0; the alpha
+// index (int)(2 pi ga / r) + {0, 1} is 0..7; the beta index (int)(pi gb / r)
+// + {0, 1} is 0..4; gama adds 0 or r^2): voxel g r^2 + a r + b, slot
+// g * 40 + a * 5 + b.  One workgroup per (block of kSphFwdPts * 256 points,
+// group of up to kSphFwdCG channels, cloud) stages those 80 values of its
+// channels in LDS (a few KB from L2, shared by the cloud's workgroups), then
+// every point computes its corners once and every channel's eight gathers
+// are LDS reads; the outputs are coalesced stores.  A corner outside the set
+// (g_inds >= r^3, an invalid input) is read from global memory, bounds-
+// checked as devox_fwd_kernel does.  Same corners, weights and wsum8 order,
+// so the same bits as devox_fwd_kernel<true>.  (That kernel gathered every
+// corner from global memory: 8 C scattered 4-byte loads per point, bound by
+// the L1 / TA request rate, 0.31 ms at c5.)
+constexpr int kSphFwdThreads = 256;
+constexpr int kSphFwdPts = 4;   // points per thread
+constexpr int kSphFwdCG = 64;   // channels per workgroup: 80 x 64 x 4 = 20 KB of LDS
+constexpr int kSphSlots = 80;
+__device__ inline int sph_slot(int v, int r) {
+  const int r2 = r * r;
+  const int g = v / r2;
+  const int rem = v - g * r2;
+  const int a = rem / r;
+  const int bb = rem - a * r;
+  return (v >= 0 && g <= 1 && a <= 7 && bb <= 4) ? g * 40 + a * 5 + bb : -1;
+}
+__global__ __launch_bounds__(kSphFwdThreads) void devox_fwd_sph_lds_kernel(
+    const float* __restrict__ coords, const float* __restrict__ feat,
+    const int* __restrict__ g_inds, int c, int n, int r, float* __restrict__ outs,
+    int* __restrict__ inds, float* __restrict__ wgts) {
+  __shared__ float val_s[kSphFwdCG * kSphSlots];  // [channel][slot]
+  const int b = blockIdx.z;
+  const int c0 = blockIdx.y * kSphFwdCG;
+  const int cn = min(kSphFwdCG, c - c0);
+  const int tid = threadIdx.x;
+  const int r2 = r * r, r3 = r2 * r;
+  const float* F = feat + ((size_t)b * c + c0) * r3;
+  for (int t = tid; t < cn * kSphSlots; t += kSphFwdThreads) {
+    const int ch = t / kSphSlots;
+    const int sl = t - ch * kSphSlots;
+    const int g = sl / 40, a = (sl - g * 40) / 5, bb = sl - g * 40 - a * 5;
+    const int v = g * r2 + a * r + bb;
+    val_s[t] = v < r3 ? F[(size_t)ch * r3 + v] : 0.0f;
+  }
+  __syncthreads();
+  const float* x = coords + (size_t)b * 3 * n;
+  float* O = outs + ((size_t)b * c + c0) * n;
+#pragma unroll 1
+  for (int pp = 0; pp < kSphFwdPts; pp++) {
+    const int i = (blockIdx.x * kSphFwdPts + pp) * kSphFwdThreads + tid;
+    if (i >= n) break;
+    int idx[8];
+    float w[8];
+    bool ok;
+    const int pos = g_inds[(size_t)b * n + i];
+    if (pos == -1) {
+      ok = false;
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        idx[q] = q == 0 ? -1 : 0;
+        w[q] = 0.0f;
+      }
+    } else {
+      ok = pcr_sph_corners(x[i], x[i + n], x[i + 2 * n], pos, r, idx, w) != 0;
+      if (!ok) {
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+          idx[q] = 0;
+          w[q] = 0.0f;
+        }
+      }
+    }
+    if (blockIdx.y == 0) {
+      int* I = inds + (size_t)b * 8 * n;
+      float* Wt = wgts + (size_t)b * 8 * n;
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        I[i + (size_t)q * n] = idx[q];
+        Wt[i + (size_t)q * n] = w[q];
+      }
+    }
+    int sl[8];
+    bool all_lds = true;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      sl[q] = sph_slot(idx[q], r);
+      all_lds &= sl[q] >= 0;
+    }
+    if (__all(all_lds || !ok)) {
+      // every live point of the wave reads LDS only
+      for (int ch = 0; ch < cn; ch++) {
+        const float* vs = val_s + ch * kSphSlots;
+        float fv[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) fv[q] = vs[ok ? sl[q] : 0];
+        O[(size_t)ch * n + i] = ok ? pcr_wsum8(w, fv) : 0.0f;
+      }
+    } else {
+      for (int ch = 0; ch < cn; ch++) {
+        const float* vs = val_s + ch * kSphSlots;
+        float fv[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++)
+          fv[q] = sl[q] >= 0 ? vs[sl[q]]
+                             : ((idx[q] >= 0 && idx[q] < r3) ? F[(size_t)ch * r3 + idx[q]] : 0.0f);
+        O[(size_t)ch * n + i] = ok ? pcr_wsum8(w, fv) : 0.0f;
+      }
+    }
+  }
+}
+
 // Cube forward for grids whose channel row fits in LDS (r <= 32): one
 // workgroup per (cloud, channel) stages the whole row with coalesced 16-byte
 // loads, so the 8 corner gathers of every point are LDS reads instead of
@@ -363,6 +475,12 @@ static pcr_status devox_forward(bool sph, int r, const float* coords, const floa
     allow_big_lds(devox_fwd_cube_row_kernel, row_bytes);
     hipLaunchKernelGGL(devox_fwd_cube_row_kernel, dim3(c, b), dim3(kFwdRowThreads), row_bytes,
                        as_stream(stream), coords, features, c, n, r, outs, inds, wgts);
+    return launch_status(name);
+  }
+  if (sph) {
+    dim3 grid(ceil_div(n, kSphFwdPts * kSphFwdThreads), c > 0 ? ceil_div(c, kSphFwdCG) : 1, b);
+    hipLaunchKernelGGL(devox_fwd_sph_lds_kernel, grid, dim3(kSphFwdThreads), 0,
+                       as_stream(stream), coords, features, g_inds, c, n, r, outs, inds, wgts);
     return launch_status(name);
   }
   const int cg = 8;

@@ -360,3 +360,30 @@ def test_ball_query_paths(dev, b, m, n, radius, u, scale):
     pts[:, :, 5:9] = pts[:, :, 1:2]                             # duplicates
     idx = ops.ball_query(T(ctr, dev), T(pts, dev), radius, u)
     assert np.array_equal(N(idx), oracle.ball_query(ctr, pts, radius, u))
+
+
+@pytest.mark.parametrize("b,n,c,r", [(2, 1500, 67, 2), (2, 700, 5, 3), (1, 3000, 130, 4),
+                                     (2, 1025, 64, 7), (1, 4097, 16, 16), (1, 2048, 64, 64)])
+def test_sph_devox_forward_corner_staging(dev, b, n, c, r):
+    """The LDS-staged spherical devox forward (devox_fwd_sph_lds_kernel):
+    tiny grids whose 80 corner slots alias or run past r^3, channel counts
+    across the 64-channel groups, ragged point counts, dropped points
+    (g_inds = -1) and invalid voxel indices (>= r^3: corners outside the
+    staged set, read from global memory and bounds-checked) -- bit-exact
+    against the oracle."""
+    from pcr_amd import ops
+    xyz, _, _ = gaussian_clouds(b, n, seed=40 + r)
+    nc = oracle.normalize_sph(xyz)
+    ind = np.stack([oracle.sph_index(nc[i], r) for i in range(b)]).astype(np.int32)
+    ind[:, 3::97] = -1
+    if r >= 4:
+        ind[0, 5::113] = r ** 3 + 7 * r  # invalid: corners beyond the 80-slot set
+    grid = np.random.default_rng(41).standard_normal((b, c, r ** 3)).astype(np.float32)
+    outs, inds, wgts = ops.spherical_trilinear_devoxelize_forward(r, True, T(nc, dev),
+                                                                  T(grid, dev), T(ind, dev))
+    eo, ei, ew = oracle.spherical_trilinear_devoxelize_forward(r, nc, grid, ind)
+    assert np.array_equal(N(inds), ei)
+    assert np.array_equal(N(wgts), ew)
+    # out-of-range corners contribute 0 in both (the reference would read
+    # out of bounds there)
+    assert np.array_equal(N(outs), eo)
