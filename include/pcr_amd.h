@@ -241,6 +241,15 @@ pcr_status pcr_extractor_voxel_devox(const float *features, int b, int c, int n,
                                      float *devox, const int *dinds, const float *dwgts,
                                      float *desc, void *workspace, size_t workspace_bytes,
                                      void *stream);
+/* devox + descriptor from the dense grid the grid launch wrote (on the same
+ * stream, after it): every spherical corner lies in a fixed set of 80 voxels
+ * (spherical_trilinear_devox.cu:67-105), whose values are staged in LDS per
+ * channel; corners from prep's dinds / dwgts.  n <= 4096.  Same outputs as
+ * pcr_extractor_voxel_devox (which re-forms the voxel means from the
+ * features instead of reading the grid). */
+pcr_status pcr_extractor_grid_devox(const float *grid, const int *dinds, const float *dwgts,
+                                    int b, int c, int n, int r, float *devox, float *desc,
+                                    void *stream);
 /* grid + devox + descriptor in one launch after prep (the devox tail gathers
  * the voxel means the workgroup already holds in LDS, through prep's corner
  * -> segment map): what pcr_extractor_voxel_stage launches after prep. */

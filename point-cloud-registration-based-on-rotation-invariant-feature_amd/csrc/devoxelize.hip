@@ -205,6 +205,99 @@ __global__ __launch_bounds__(kSphFwdThreads) void devox_fwd_sph_lds_kernel(
   }
 }
 
+// The extractor's devoxelisation from the dense grid it just wrote: the
+// same 80-slot LDS staging as devox_fwd_sph_lds_kernel, with the corner
+// indices / weights prep already computed (dinds / dwgts) and the per-cloud
+// max-pooled descriptor.  One workgroup of 1024 threads per (cloud, group of
+// up to 64 channels) covers every point of its cloud (n <= 4096, up to four
+// points per thread, their corner slots and weights in registers), so the
+// descriptor needs no cross-workgroup step.  Replaces re-forming every
+// voxel mean from the features per channel group (vox_grid_kernel<2>, 0.94
+// ms at the c3 shape) with a read of the 80 corner values per channel.
+constexpr int kGridDevoxThreads = 1024;
+constexpr int kGridDevoxPts = 4;
+__global__ __launch_bounds__(kGridDevoxThreads) void devox_grid_desc_kernel(
+    const float* __restrict__ grid, const int* __restrict__ dinds,
+    const float* __restrict__ dwgts, int c, int n, int r, float* __restrict__ devox,
+    float* __restrict__ desc) {
+  // [channel][81]: the 80 corner slots and a zero (the slot of every
+  // zero-weight corner, e.g. all of a dropped point's: +0 * 0 terms, so the
+  // point's output is +0 like the reference's untouched zero)
+  constexpr int kStride = kSphSlots + 1;
+  __shared__ float val_s[kSphFwdCG * kStride];
+  __shared__ float red_s[kGridDevoxThreads / kWave][kSphFwdCG];
+  const int b = blockIdx.y;
+  const int c0 = blockIdx.x * kSphFwdCG;
+  const int cn = min(kSphFwdCG, c - c0);
+  const int tid = threadIdx.x;
+  const int r2 = r * r, r3 = r2 * r;
+  const float* F = grid + ((size_t)b * c + c0) * r3;
+  for (int t = tid; t < cn * kStride; t += kGridDevoxThreads) {
+    const int ch = t / kStride;
+    const int sl = t - ch * kStride;
+    const int g = sl / 40, a = (sl - g * 40) / 5, bb = sl - g * 40 - a * 5;
+    const int v = g * r2 + a * r + bb;
+    val_s[t] = (sl < kSphSlots && v < r3) ? F[(size_t)ch * r3 + v] : 0.0f;
+  }
+  // corners of this thread's points (prep's dinds / dwgts; a dropped point
+  // has inds {-1, 0, ...} and zero weights)
+  int sl[kGridDevoxPts][8], gi[kGridDevoxPts][8];
+  float w[kGridDevoxPts][8];
+  bool all_lds = true;
+  const int* I = dinds + (size_t)b * 8 * n;
+  const float* Wt = dwgts + (size_t)b * 8 * n;
+#pragma unroll
+  for (int u = 0; u < kGridDevoxPts; u++) {
+    const int i = u * kGridDevoxThreads + tid;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const int v = i < n ? I[i + (size_t)q * n] : 0;
+      w[u][q] = i < n ? Wt[i + (size_t)q * n] : 0.0f;
+      gi[u][q] = v;
+      sl[u][q] = w[u][q] == 0.0f ? kSphSlots : sph_slot(v, r);
+      if (i < n && sl[u][q] < 0) all_lds = false;
+    }
+  }
+  const bool fast = __syncthreads_and(all_lds);  // also the staging barrier
+  float* O = devox + ((size_t)b * c + c0) * n;
+  const int wv = tid >> 6;
+  for (int ch = 0; ch < cn; ch++) {
+    const float* vs = val_s + ch * kStride;
+    float m = -__builtin_inff();
+#pragma unroll
+    for (int u = 0; u < kGridDevoxPts; u++) {
+      const int i = u * kGridDevoxThreads + tid;
+      if (i < n) {
+        float fv[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+          if (fast)
+            fv[q] = vs[sl[u][q]];
+          else
+            fv[q] = sl[u][q] >= 0 ? vs[sl[u][q]]
+                                  : ((gi[u][q] >= 0 && gi[u][q] < r3)
+                                         ? F[(size_t)ch * r3 + gi[u][q]] : 0.0f);
+        }
+        const float v = pcr_wsum8(w[u], fv);
+        O[(size_t)ch * n + i] = v;
+        m = fmaxf(m, v);
+      }
+    }
+    if (desc) {
+      m = wave_max(m);
+      if ((tid & 63) == 0) red_s[wv][ch] = m;
+    }
+  }
+  if (desc) {
+    lds_only_barrier();
+    if (tid < cn) {
+      float m = red_s[0][tid];
+      for (int q = 1; q < kGridDevoxThreads / kWave; q++) m = fmaxf(m, red_s[q][tid]);
+      desc[(size_t)b * c + c0 + tid] = m;
+    }
+  }
+}
+
 // Cube forward for grids whose channel row fits in LDS (r <= 32): one
 // workgroup per (cloud, channel) stages the whole row with coalesced 16-byte
 // loads, so the 8 corner gathers of every point are LDS reads instead of
@@ -503,6 +596,20 @@ extern "C" pcr_status pcr_spherical_trilinear_devoxelize_forward(int r, int is_t
   (void)is_training;
   return devox_forward(true, r, coords, features, g_inds, b, c, n, outs, inds, wgts, stream,
                        "spherical_trilinear_devoxelize_forward");
+}
+
+extern "C" pcr_status pcr_extractor_grid_devox(const float* grid, const int* dinds,
+                                               const float* dwgts, int b, int c, int n, int r,
+                                               float* devox, float* desc, void* stream) {
+  PCR_REQUIRE(b >= 0 && c >= 1 && n >= 1 && n <= kGridDevoxPts * kGridDevoxThreads && r >= 1,
+              "extractor_grid_devox: invalid sizes b=%d c=%d n=%d r=%d (n <= %d)", b, c, n, r,
+              kGridDevoxPts * kGridDevoxThreads);
+  PCR_REQUIRE((int64_t)r * r * r < (1ll << 31) / 64, "extractor_grid_devox: resolution too large");
+  if (b == 0) return PCR_OK;
+  hipLaunchKernelGGL(devox_grid_desc_kernel, dim3(ceil_div(c, kSphFwdCG), b),
+                     dim3(kGridDevoxThreads), 0, as_stream(stream), grid, dinds, dwgts, c, n, r,
+                     devox, desc);
+  return launch_status("extractor_grid_devox");
 }
 
 extern "C" pcr_status pcr_trilinear_devoxelize_forward(int r, int is_training, const float* coords,

@@ -834,6 +834,11 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
 #pragma unroll
     for (int a = 0; a < 6; a++) bl[j][a] = ok ? boxes[(size_t)blk * 8 + a] : 0.0f;
   }
+  // the query block's box (scalar loads; the register-box sweep's prefilter)
+  float qbx[6];
+#pragma unroll
+  for (int a = 0; a < 6; a++)
+    qbx[a] = breg ? qs.box[((size_t)b * qs.nblk + qblk) * 8 + a] : 0.0f;
   // visits this wave's blocks in order: g(blk, box[6]) (register boxes only)
   auto for_blocks = [&](auto&& g) {
 #pragma unroll
@@ -849,6 +854,12 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     }
   };
   int cj_cur = 0;  // original index of candidate `lane` of the block in process
+  // register-box path: blocks a count round already visited (excluded from
+  // the next round) and whether this visit records its blocks there
+  unsigned long long vskip[kBoxJ];
+#pragma unroll
+  for (int j = 0; j < kBoxJ; j++) vskip[j] = 0ull;
+  bool vrecord = false;
   auto visit = [&](float lim, auto want_j, auto&& f) {
     constexpr bool WANT_J = decltype(want_j)::value;
     if (CL) {
@@ -914,18 +925,40 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
           if (__any(box_lb(qx, qy, qz, b6) < lim)) vm[0] |= 1ull << l;
         }
       } else {
+        // lane l tests block wv + NW (64 j + l) against the box of the
+        // query block with the largest limit of its queries (the same
+        // rounding chain, so it is a lower bound of every query's box
+        // distance: a block failing it is needed by no query); only the
+        // blocks passing it get the per-query test (one box test + ballot
+        // each), instead of a sweep of all 64 queries for every block
+        float mlim = lim;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) mlim = fmaxf(mlim, __shfl_xor(mlim, off, kWave));
 #pragma unroll
         for (int j = 0; j < kBoxJ; j++) {
-          bool need = false;
-          for (int q = 0; q < kBlk; q++) {
-            const float lq = readlane_f(lim, q);
-            const float lb =
-                box_lb(readlane_f(qx, q), readlane_f(qy, q), readlane_f(qz, q), bl[j]);
-            need |= lb < lq;
+          const float gx = fmaxf(fmaxf(bl[j][0] - qbx[3], qbx[0] - bl[j][3]), 0.0f);
+          const float gy = fmaxf(fmaxf(bl[j][1] - qbx[4], qbx[1] - bl[j][4]), 0.0f);
+          const float gz = fmaxf(fmaxf(bl[j][2] - qbx[5], qbx[2] - bl[j][5]), 0.0f);
+          float bb = gx * gx;
+          bb = __builtin_fmaf(gy, gy, bb);
+          bb = __builtin_fmaf(gz, gz, bb);
+          unsigned long long cand =
+              __ballot(bb < mlim && wv + NW * (j * kBlk + lane) < nblk);
+          vm[j] = 0ull;
+          while (cand) {
+            const int l = __builtin_ctzll(cand);
+            cand &= cand - 1ull;
+            float b6[6];
+#pragma unroll
+            for (int a = 0; a < 6; a++) b6[a] = readlane_f(bl[j][a], l);
+            if (__any(box_lb(qx, qy, qz, b6) < lim)) vm[j] |= 1ull << l;
           }
-          need &= wv + NW * (j * kBlk + lane) < nblk;
-          vm[j] = __ballot(need);
         }
+      }
+#pragma unroll
+      for (int j = 0; j < kBoxJ; j++) {
+        vm[j] &= ~vskip[j];
+        if (vrecord) vskip[j] |= vm[j];
       }
       // the visited blocks in order, the next one's candidates loaded (one
       // per lane) while the current one is evaluated from the wave's LDS slot
@@ -1067,7 +1100,7 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
 #ifdef PCR_DIAG
   int diag_reason = fallback ? 1 : 0;
 #endif
-  auto count_cut = [&](float lim) {
+  auto count_visit = [&](float lim) {
     unsigned* hw = hist_s + (size_t)(wv / FPD) * (kNB + 1) * kBlk + lane;
     const unsigned inc = 1u << ((wv % FPD) * CB);
     // counter of bin e (clamped to [base, base + kNB]; the last = not
@@ -1083,6 +1116,44 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
                                __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     });
+  };
+  // upper edge of the first bin where the lane's count so far reaches k
+  // (every count is a real candidate, so kth(q) lies below it), else `lim`
+  auto running_cut = [&](float lim) {
+    int cum = 0;
+    float t = lim;
+    bool found = false;
+    for (int bin = 0; bin < kNB; bin++) {
+#pragma unroll
+      for (int g = 0; g < NG; g++) cum += (int)field_sum<CB>(hist_s[(g * (kNB + 1) + bin) * kBlk + lane]);
+      if (!found && cum >= k) {
+        found = true;
+        t = __uint_as_float((unsigned)(base + bin + 1) << shift);
+      }
+      if (__all(found)) break;
+    }
+    return fminf(t, lim);
+  };
+  auto count_cut = [&](float lim) {
+    if (!CL && breg) {
+      // large clouds: two rounds.  D_q is several times kth (its bin top
+      // reaches past most of the cloud's near blocks), so the blocks near
+      // the queries (lower bound below D_q / 8) are counted first; their
+      // counts give each query an upper bound of kth (the first bin where
+      // the count reaches k), and the second round adds only the blocks
+      // below that tighter bound.  Every block a query may need is still
+      // counted for it: an unvisited block has every lane's lower bound at
+      // or above that lane's limit, and the final cut never exceeds it.
+      vrecord = true;
+      count_visit(lim * 0.125f);
+      vrecord = false;
+      __syncthreads();
+      count_visit(qlive ? running_cut(lim) : 0.0f);
+#pragma unroll
+      for (int j = 0; j < kBoxJ; j++) vskip[j] = 0ull;
+    } else {
+      count_visit(lim);
+    }
     __syncthreads();
     PCR_STAMP(2);
     // wave 0 finds the cut of the 64 queries (the other waves would repeat

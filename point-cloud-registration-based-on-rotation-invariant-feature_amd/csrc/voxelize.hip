@@ -1094,14 +1094,19 @@ static int grid_wgs(int nitems) {
 
 // ------------------------------------------------------ backward gather
 // grad_x[b,j,i] = grad_y[b,j,ind[i]] * (1/cnt)  (spherical_vox.cu:151-162)
+// One thread per point and kGradCG channels: the point's voxel and count are
+// loaded once and all kGradCG gathers are issued before any is used (a
+// runtime-length channel loop waited for each gather in turn: a chain of
+// dependent HBM round trips per thread).
+constexpr int kGradCG = 16;
 __global__ __launch_bounds__(256) void avg_vox_grad_kernel(const float* __restrict__ grad_y,
                                                            const int* __restrict__ ind,
                                                            const int* __restrict__ cnt, int c,
-                                                           int n, int r3, int cg,
+                                                           int n, int r3,
                                                            float* __restrict__ grad_x) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   const int b = blockIdx.z;
-  const int j0 = blockIdx.y * cg;
+  const int j0 = blockIdx.y * kGradCG;
   if (i >= n) return;
   const int pos = ind[(size_t)b * n + i];
   float inv = 0.0f;
@@ -1111,12 +1116,15 @@ __global__ __launch_bounds__(256) void avg_vox_grad_kernel(const float* __restri
     ok = ct > 0;
     if (ok) inv = pcr_inv_count(ct);
   }
-  const int j1 = min(c, j0 + cg);
-  for (int j = j0; j < j1; j++) {
-    float v = 0.0f;
-    if (ok) v = grad_y[((size_t)b * c + j) * r3 + pos] * inv;
-    grad_x[((size_t)b * c + j) * n + i] = v;
-  }
+  const int jn = min(kGradCG, c - j0);
+  const float* gy = grad_y + ((size_t)b * c + j0) * r3 + (ok ? pos : 0);
+  float v[kGradCG];
+#pragma unroll
+  for (int j = 0; j < kGradCG; j++) v[j] = (ok && j < jn) ? gy[(size_t)j * r3] : 0.0f;
+  float* gx = grad_x + ((size_t)b * c + j0) * n + i;
+#pragma unroll
+  for (int j = 0; j < kGradCG; j++)
+    if (j < jn) gx[(size_t)j * n] = v[j] * inv;
 }
 
 // ------------------------------------------------------ normalize only
@@ -1645,9 +1653,8 @@ extern "C" pcr_status pcr_avg_voxelize_backward(const float* grad_y, const int* 
                                                 float* grad_x, void* stream) {
   PCR_REQUIRE(b >= 0 && c >= 0 && n >= 0 && r3 >= 1, "avg_voxelize_backward: invalid sizes");
   if (b == 0 || c == 0 || n == 0) return PCR_OK;
-  const int cg = 8;
-  hipLaunchKernelGGL(avg_vox_grad_kernel, dim3(ceil_div(n, 256), ceil_div(c, cg), b), dim3(256),
-                     0, as_stream(stream), grad_y, ind, cnt, c, n, r3, cg, grad_x);
+  hipLaunchKernelGGL(avg_vox_grad_kernel, dim3(ceil_div(n, 256), ceil_div(c, kGradCG), b),
+                     dim3(256), 0, as_stream(stream), grad_y, ind, cnt, c, n, r3, grad_x);
   return launch_status("avg_voxelize_backward");
 }
 

@@ -51,6 +51,7 @@ SIGNATURES = {
     "pcr_extractor_voxel_prep": (ST, [P, I, I, I, P, P, P, P, P, SZ, P]),
     "pcr_extractor_voxel_grid": (ST, [P, I, I, I, I, P, P, P, SZ, P]),
     "pcr_extractor_voxel_devox": (ST, [P, I, I, I, I, P, P, P, P, P, SZ, P]),
+    "pcr_extractor_grid_devox": (ST, [P, P, P, I, I, I, I, P, P, P]),
     "pcr_extractor_voxel_grid_devox": (ST, [P, I, I, I, I, P, P, P, P, P, P, P, SZ, P]),
     "pcr_extractor_voxel_means_devox": (ST, [P, I, I, I, I, P, P, P, P, P, SZ, P]),
     "pcr_extractor_voxel_stream": (ST, [I, I, I, I, P, P, P, SZ, P]),

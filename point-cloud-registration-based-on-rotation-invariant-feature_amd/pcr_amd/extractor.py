@@ -9,11 +9,11 @@ features [B,C,N], all resident on the GPU):
   neighbours (stream A): self-KNN (k) -> local PPF [B,4,k,N]
       = knn_forward_cuda + the model's local-PPF block
         (PVCNN/models/pvcnn_classify.py:252-269), one kernel
-  grid (stream B): spherical_avg_voxelize's dense grid [B,C,r^3] + cnt
-  devox (stream C): spherical_trilinear_devoxelize of that grid ([B,C,N] +
-      inds/wgts) + per-cloud descriptor (max over points) [B,C]; it re-forms
-      the voxel means in LDS instead of re-reading the grid, so it runs beside
-      the grid kernel
+  grid (stream B): spherical_avg_voxelize's dense grid [B,C,r^3] + cnt, then
+      spherical_trilinear_devoxelize of that grid ([B,C,N] + inds/wgts) +
+      per-cloud descriptor (max over points) [B,C], reading only the 80
+      corner voxels per channel every spherical corner lies in (clouds of
+      more than 4096 points: the devox re-forms the voxel means on stream C)
 
 The streams are forked from and joined back to the caller's stream.
 ``forward()`` enqueues one step from Python; ``capture()`` records one step
@@ -167,6 +167,15 @@ class SphExtractor:
             self.b, self.c, self.n, self.r, _ptr(self.cnt), _ptr(self.grid), _ptr(ws),
             ws.numel(), stream), "extractor_voxel_stream")
 
+    def grid_devox(self, stream, desc=None, slot=0):
+        """Devox + descriptor from the dense grid (after voxel_grid on the
+        same stream): the 80 corner voxels per channel staged in LDS."""
+        _, _, dinds, dwgts, _ = self._set(slot)
+        d = self.desc if desc is None else desc
+        _lib.check(_lib.load().pcr_extractor_grid_devox(
+            _ptr(self.grid), _ptr(dinds), _ptr(dwgts), self.b, self.c, self.n, self.r,
+            _ptr(self.devox), _ptr(d), stream), "extractor_grid_devox")
+
     def voxel_devox(self, features, stream, desc=None, slot=0):
         _, ws, dinds, dwgts, _ = self._set(slot)
         d = self.desc if desc is None else desc
@@ -199,8 +208,7 @@ class SphExtractor:
         """Enqueue one step on the extractor's streams, no fork/join:
           s_pre: KNN Morton sort, voxel prep (both small, one workgroup per cloud)
           s_nbr: KNN selection + local PPF      (after the sort)
-          s_vox: voxel grid                     (after prep)
-          s_dev: devoxelisation + descriptor    (after prep)
+          s_vox: voxel grid, then devox + descriptor from that grid (after prep)
         `reuse` = events after which the previous users of buffer set `slot`
         are done (s_pre waits for them before overwriting it).  With
         `events`, returns this step's events on buffer set `slot`."""
@@ -217,8 +225,13 @@ class SphExtractor:
         self.knn_select(xyz, normals, self.s_nbr.cuda_stream, slot, sorted_ok)
         self.s_vox.wait_event(e_prep)
         self.voxel_grid(features, self.s_vox.cuda_stream, slot)
-        self.s_dev.wait_event(e_prep)
-        self.voxel_devox(features, self.s_dev.cuda_stream, desc, slot)
+        if self.n <= 4096:
+            # the devox reads the 80 corner voxels per channel of the grid
+            # just written (same stream)
+            self.grid_devox(self.s_vox.cuda_stream, desc, slot)
+        else:
+            self.s_dev.wait_event(e_prep)
+            self.voxel_devox(features, self.s_dev.cuda_stream, desc, slot)
         if not events:
             return None
         evs = []

@@ -161,3 +161,29 @@ def test_sph_vox_large_without_feature_copy(dev):
     eo, _, _ = oracle.spherical_avg_voxelize_forward(feat, nc, r)
     assert np.array_equal(N(out).reshape(eo.shape), eo)
     assert torch.equal(out, ref[0]) and torch.equal(ind, ref[1]) and torch.equal(cnt, ref[2])
+
+
+@pytest.mark.parametrize("shape", ["gauss", "clusters"])
+def test_knn_c5_k64_query_sample_vs_oracle(dev, shape):
+    """BASELINE c5 KNN (65,536 points, k = 64): 1,024 sampled queries per
+    cloud bit-exact (indices and distances) against the oracle's reference
+    scan, for Gaussian clouds and for tight clusters with a sparse halo
+    (queries whose k-th distance is far below D_q, and outliers whose
+    neighbours are far away) -- the large-cloud selection's two count rounds."""
+    from pcr_amd import ops
+    n, k = 65536, 64
+    xyz, nrm, _ = gaussian_clouds(2, n, seed=47)
+    if shape == "clusters":
+        rng = np.random.default_rng(48)
+        cen = rng.standard_normal((2, 3, 8)).astype(np.float32) * 3
+        lab = rng.integers(0, 8, (2, n))
+        for b in range(2):
+            xyz[b] = cen[b][:, lab[b]] + 0.02 * xyz[b]
+        xyz[:, :, :200] *= 40  # sparse halo / outliers
+    idx, _, dist = ops.knn_local_ppf(T(xyz, dev), T(nrm, dev), k, want_dist=True)
+    i, d = N(idx), N(dist)
+    samp = np.random.default_rng(49).choice(n, 1024, replace=False)
+    samp[:64] = np.arange(64)  # include halo points
+    ref_d, ref_i = oracle.knn_dir(np.ascontiguousarray(xyz[:, :, samp]), xyz, k)
+    assert np.array_equal(i[:, :, samp], ref_i)
+    assert np.array_equal(d[:, :, samp], ref_d)
