@@ -107,6 +107,16 @@ pcr_status pcr_knn_local_ppf_prepared(const float *xyz, const float *normals, in
                                       int relative, int *idx, float *dist, float *ppf,
                                       const void *workspace, size_t workspace_bytes,
                                       void *stream);
+/* Selection + local PPF of a prepared workspace in two launches whose only
+ * scattered traffic is a read: the selection emits its neighbour ids in
+ * sorted (Morton) query order into the workspace -- whole rows -- and the PPF
+ * kernel reads them back through the sort's inverse permutation while it
+ * writes knn_idx [b,k,n] (original order) and ppf [b,4,k,n].  k <= 32 and
+ * n <= 2048 take that path; other shapes run pcr_knn_local_ppf_prepared +
+ * pcr_local_ppf_forward.  Same outputs as those two calls. */
+pcr_status pcr_knn_select_ppf(const float *xyz, const float *normals, int b, int n, int k,
+                              int relative, int *idx, float *ppf, const void *workspace,
+                              size_t workspace_bytes, void *stream);
 
 /* ------------------------------------------------ ball query / grouping --
  * ball_query (ball_query/ball_query.cpp:6-30, kernel ball_query.cu:19-50):

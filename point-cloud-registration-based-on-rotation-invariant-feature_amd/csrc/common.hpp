@@ -52,6 +52,11 @@ pcr_status knn_spatial(const float* xyz1, const float* xyz2, int b, int n, int m
                        float* dist1, int* idx1, float* dist2, int* idx2, const float* nrm1,
                        const float* nrm2, int relative, float* ppf1, void* ws, size_t ws_bytes,
                        bool self, hipStream_t st, int stages = 3);
+// stage 4 (with 2): the selection writes its neighbour ids in sorted query
+// order into the workspace (k <= 32, clouds of <= 2048 points); these are the
+// views of that output and of the sort's inverse permutation
+constexpr int kKnnSortedK = 32;
+bool knn_sorted_views(void* ws, int b, int n, const int** sidx, const int** inv, int* npad);
 
 // ---------------------------------------------------------------- device
 constexpr int kWave = 64;

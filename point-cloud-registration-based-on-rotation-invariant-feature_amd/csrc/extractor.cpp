@@ -69,11 +69,16 @@ pcr_status knn_select_ppf(const pcr_extractor_args* a, int q, bool sorted, hipSt
   if (!sorted)  // no sorted path: the one-call selection + PPF
     return pcr_knn_local_ppf(a->xyz, a->normals, a->b, a->n, a->k, a->relative, a->knn_idx,
                              a->knn_dist, a->local_ppf, a->knn_ws[q], a->knn_ws_bytes, st);
-  PCR_TRY(pcr_knn_local_ppf_prepared(a->xyz, a->normals, a->b, a->n, a->k, a->relative,
-                                       a->knn_idx, a->knn_dist, nullptr, a->knn_ws[q],
-                                       a->knn_ws_bytes, st));
-  return pcr_local_ppf_forward(a->xyz, a->normals, a->xyz, a->normals, a->knn_idx, a->b, a->n,
-                               a->n, a->k, 1, a->relative, a->local_ppf, st);
+  if (a->knn_dist) {  // distances requested: the selection writes in original order
+    PCR_TRY(pcr_knn_local_ppf_prepared(a->xyz, a->normals, a->b, a->n, a->k, a->relative,
+                                         a->knn_idx, a->knn_dist, nullptr, a->knn_ws[q],
+                                         a->knn_ws_bytes, st));
+    return pcr_local_ppf_forward(a->xyz, a->normals, a->xyz, a->normals, a->knn_idx, a->b, a->n,
+                                 a->n, a->k, 1, a->relative, a->local_ppf, st);
+  }
+  // selection in sorted query order, the PPF launch writes knn_idx + PPF
+  return pcr_knn_select_ppf(a->xyz, a->normals, a->b, a->n, a->k, a->relative, a->knn_idx,
+                            a->local_ppf, a->knn_ws[q], a->knn_ws_bytes, st);
 }
 
 // the step's registration matching (source clouds [0, P) against targets
@@ -218,17 +223,9 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
     PCR_HIP(hipEventRecord(stream_done[q], sv), "stream record");
     if (schedule == 2) {
       PCR_HIP(hipStreamWaitEvent(sn, sort_done[q], 0), "sort wait");
-      if (sorted) {
-        PCR_TRY(pcr_knn_local_ppf_prepared(a->xyz, a->normals, a->b, a->n, a->k, a->relative,
-                                           a->knn_idx, a->knn_dist, nullptr, a->knn_ws[q],
-                                           a->knn_ws_bytes, sn));
-        PCR_HIP(hipEventRecord(sel_done[q], sn), "select record");
-        PCR_TRY(pcr_local_ppf_forward(a->xyz, a->normals, a->xyz, a->normals, a->knn_idx, a->b,
-                                      a->n, a->n, a->k, 1, a->relative, a->local_ppf, sn));
-      } else {
-        PCR_TRY(knn_select_ppf(a, q, false, sn));
-        PCR_HIP(hipEventRecord(sel_done[q], sn), "select record");
-      }
+      // (the PPF launch reads the workspace too: the slot is free after it)
+      PCR_TRY(knn_select_ppf(a, q, sorted, sn));
+      PCR_HIP(hipEventRecord(sel_done[q], sn), "select record");
     } else {
       // the first step's neighbour stream starts after that step's voxel
       // means: prep + means (the grid stream's chain) get the chip first, so

@@ -40,10 +40,21 @@ struct KnnSet {
   int* pcell;    // [b][n] cell of each point
   int* pslot;    // [b][n] arrival slot inside the cell
   float* frame;  // [b][8] lo xyz, scale xyz
+  // clouds of <= kSortedMaxN points (the LDS-cached selection):
+  int* inv;   // [b][n] sorted position of every point (the sort's inverse)
+  int* sidx;  // [b][kSortedK][npad] neighbour ids in sorted query order
   int n, npad, nblk;
 };
 
 static inline size_t al256(size_t v) { return (v + 255) / 256 * 256; }
+
+// the cached selection can emit its neighbour ids in sorted (Morton) query
+// order -- whole 256-byte rows -- and the local PPF kernel un-permutes them
+// while it writes its own outputs (knn_select_ppf_sorted); writing them in
+// original order from the selection is one scattered 4-byte store per
+// (query, slot): ~7x the write requests of the 4 MB they carry at c2
+constexpr int kSortedMaxN = 2048;
+constexpr int kSortedK = kKnnSortedK;
 
 static size_t knn_set_layout(int b, int n, KnnSet* s, char* base, size_t off) {
   const int nblk = (n + kBlk - 1) / kBlk;
@@ -63,7 +74,12 @@ static size_t knn_set_layout(int b, int n, KnnSet* s, char* base, size_t off) {
   int* pcell = big ? (int*)take((size_t)b * n * 4) : nullptr;
   int* pslot = big ? (int*)take((size_t)b * n * 4) : nullptr;
   float* frame = big ? (float*)take((size_t)b * 8 * 4) : nullptr;
+  const bool sorted_out = n <= kSortedMaxN;
+  int* inv = sorted_out ? (int*)take((size_t)b * n * 4) : nullptr;
+  int* sidx = sorted_out ? (int*)take((size_t)b * kSortedK * npad * 4) : nullptr;
   if (s) {
+    s->inv = inv;
+    s->sidx = sidx;
     s->cell = cell;
     s->pcell = pcell;
     s->pslot = pslot;
@@ -211,6 +227,7 @@ __global__ __launch_bounds__(NT) void knn_sort_kernel(const float* __restrict__ 
       x = P[j];
       y = P[n + j];
       z = P[2 * n + j];
+      if (s.inv) s.inv[(size_t)b * n + j] = p;
     }
     s.x[base + p] = x;
     s.y[base + p] = y;
@@ -765,7 +782,7 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     KnnSet qs, KnnSet cs, int k, float* __restrict__ dist, int* __restrict__ idx,
     const float* __restrict__ qxyz, const float* __restrict__ qnrm,
     const float* __restrict__ cxyz, const float* __restrict__ cnrm, int relative,
-    float* __restrict__ ppf) {
+    float* __restrict__ ppf, int sorted_emit) {
   constexpr int FPD = 32 / CB;              // wave fields per counter dword
   constexpr int NG = (NW + FPD - 1) / FPD;  // counter dwords per (bin, lane)
   // the histogram is dead once the cut is chosen: the collected keys reuse it
@@ -1392,7 +1409,10 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
         const size_t o = ((size_t)b * k + sl) * n + qj;
         jn[u] = key_idx(x);
         if (dist) dist[o] = key_dist(x);
-        idx[o] = jn[u];
+        if (sorted_emit)  // sorted query order: whole rows (see kSortedMaxN)
+          qs.sidx[((size_t)b * kSortedK + sl) * qs.npad + (size_t)qblk * kBlk + lane] = jn[u];
+        else
+          idx[o] = jn[u];
       }
     }
     if (PPF) {
@@ -1466,7 +1486,10 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     const kkey x = buf_s[s2 * kBlk + lane];
     const size_t o = ((size_t)b * k + s2) * n + qj;
     if (dist) dist[o] = key_dist(x);
-    idx[o] = key_idx(x);
+    if (sorted_emit)
+      qs.sidx[((size_t)b * kSortedK + s2) * qs.npad + (size_t)qblk * kBlk + lane] = key_idx(x);
+    else
+      idx[o] = key_idx(x);
   }
   if (PPF) {
     const float* qo = qxyz + (size_t)b * 3 * n;
@@ -1489,14 +1512,15 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
 template <int NW, bool PPF, int CAP = kCap, int KSEL = kSelMaxK>
 static void launch_select(const KnnSet& qs, const KnnSet& cs, int b, int k, float* dist,
                           int* idx, const float* qxyz, const float* qnrm, const float* cxyz,
-                          const float* cnrm, int relative, float* ppf, hipStream_t st) {
+                          const float* cnrm, int relative, float* ppf, hipStream_t st,
+                          int sorted_emit = 0) {
   // a wave sees ceil(nblk / NW) * 64 candidates: byte fields when that fits
   PCR_PRIO_INIT();
   const int per_wave = ceil_div(cs.nblk, NW) * kBlk;
   const dim3 grid(qs.nblk, b), blk(NW * 64);
 #define PCR_SEL(CBV, CLV, CACHEV)                                                             \
   hipLaunchKernelGGL((knn_select_kernel<NW, CBV, CLV, PPF, CAP, KSEL, CACHEV>), grid, blk, 0, st, \
-                     qs, cs, k, dist, idx, qxyz, qnrm, cxyz, cnrm, relative, ppf)
+                     qs, cs, k, dist, idx, qxyz, qnrm, cxyz, cnrm, relative, ppf, sorted_emit)
   if constexpr (CAP == kCap) {
     // c3 clouds (2048 points): 32 KB of candidates in LDS, two workgroups per CU
     if (cs.npad > kSelCache && cs.npad <= 2 * kSelCache) {
@@ -1565,14 +1589,16 @@ static void launch_block_k(const KnnSet& qs, const KnnSet& cs, int b, int k, flo
 template <bool PPF>
 static pcr_status launch_block(const KnnSet& qs, const KnnSet& cs, int b, int k, float* dist,
                                int* idx, const float* qxyz, const float* qnrm, const float* cxyz,
-                               const float* cnrm, int relative, float* ppf, hipStream_t st) {
+                               const float* cnrm, int relative, float* ppf, hipStream_t st,
+                               int sorted_emit = 0) {
 #ifdef PCR_DIAG
   static const int impl = getenv("PCR_KNN_IMPL") ? atoi(getenv("PCR_KNN_IMPL")) : 0;
 #else
   constexpr int impl = 0;
 #endif
   if (k <= kSelMaxK && impl == 0) {
-    launch_select<8, PPF>(qs, cs, b, k, dist, idx, qxyz, qnrm, cxyz, cnrm, relative, ppf, st);
+    launch_select<8, PPF>(qs, cs, b, k, dist, idx, qxyz, qnrm, cxyz, cnrm, relative, ppf, st,
+                          sorted_emit);
   } else if (k <= kSelMaxK64 && cs.npad > kSelCache && impl == 0) {
     // large clouds (BASELINE c5, k = 64): the pruned threshold selection with
     // room for 2.75 k collected keys per query
@@ -1610,6 +1636,15 @@ pcr_status knn_spatial(const float* xyz1, const float* xyz2, int b, int n, int m
   if (!(stages & 2)) return PCR_OK;
   const KnnSet& c1 = self ? s1 : s2;
   pcr_status rc;
+  if (stages & 4) {
+    // selection only, neighbour ids in sorted query order into s1.sidx (the
+    // cached selection, k <= kSortedK); the caller's PPF launch un-permutes
+    if (!self || ppf1 || dist1 || idx2 || k > kSortedK || k > kSelMaxK || s1.sidx == nullptr ||
+        s1.npad > 2 * kSelCache)
+      return PCR_ERR_UNSUPPORTED;
+    return launch_block<false>(s1, c1, b, k, nullptr, idx1, nullptr, nullptr, nullptr, nullptr,
+                               0, nullptr, st, 1);
+  }
   if (ppf1)
     rc = launch_block<true>(s1, c1, b, k, dist1, idx1, xyz1, nrm1, xyz2, nrm2, relative, ppf1, st);
   else
@@ -1619,6 +1654,16 @@ pcr_status knn_spatial(const float* xyz1, const float* xyz2, int b, int n, int m
   if (idx2) rc = launch_block<false>(c1, s1, b, k, dist2, idx2, nullptr, nullptr, nullptr, nullptr,
                                      0, nullptr, st);
   return rc;
+}
+
+// the sorted-order outputs of a self KNN workspace (knn_spatial stage 4)
+bool knn_sorted_views(void* ws, int b, int n, const int** sidx, const int** inv, int* npad) {
+  KnnSet s;
+  knn_set_layout(b, n, &s, (char*)ws, 0);
+  *sidx = s.sidx;
+  *inv = s.inv;
+  *npad = s.npad;
+  return s.sidx != nullptr;
 }
 
 }  // namespace pcr

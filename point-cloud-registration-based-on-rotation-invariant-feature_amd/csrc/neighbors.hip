@@ -275,7 +275,10 @@ __global__ __launch_bounds__(NT) void local_ppf_self_kernel(const float* __restr
                                                              const float* __restrict__ nrm,
                                                              const int* __restrict__ idx, int n,
                                                              int k, int relative,
-                                                             float* __restrict__ out) {
+                                                             float* __restrict__ out,
+                                                             const int* __restrict__ sidx,
+                                                             const int* __restrict__ inv,
+                                                             int npad, int* __restrict__ idx_out) {
   extern __shared__ __align__(16) float cl_s[];  // [6][n]: x y z nx ny nz
   (void)PCR_PRIO(2);
   const int tid = threadIdx.x;
@@ -285,9 +288,22 @@ __global__ __launch_bounds__(NT) void local_ppf_self_kernel(const float* __restr
   const float* P = xyz + (size_t)b * 3 * n;
   const float* Nn = nrm + (size_t)b * 3 * n;
   int id[SL];
+  if (sidx) {
+    // neighbour ids in the selection's sorted query order: this point's row
+    // position from the sort's inverse permutation; the ids are written out
+    // in original order here, whole rows (the KNN output knn_idx)
+    const int p = j < n ? inv[(size_t)b * n + j] : 0;
 #pragma unroll
-  for (int s = 0; s < SL; s++)
-    id[s] = (j < n && q0 + s < k) ? idx[((size_t)b * k + q0 + s) * n + j] : 0;
+    for (int s = 0; s < SL; s++)
+      id[s] = (j < n && q0 + s < k) ? sidx[((size_t)b * kKnnSortedK + q0 + s) * npad + p] : 0;
+#pragma unroll
+    for (int s = 0; s < SL; s++)
+      if (j < n && q0 + s < k) idx_out[((size_t)b * k + q0 + s) * n + j] = id[s];
+  } else {
+#pragma unroll
+    for (int s = 0; s < SL; s++)
+      id[s] = (j < n && q0 + s < k) ? idx[((size_t)b * k + q0 + s) * n + j] : 0;
+  }
   constexpr int E = kPpfSelfMaxN / NT;
   float st[E][6];
 #pragma unroll
@@ -662,6 +678,44 @@ extern "C" pcr_status pcr_knn_local_ppf_prepared(const float* xyz, const float* 
   return launch_status("knn_local_ppf_prepared");
 }
 
+// Selection + local PPF of a prepared (sorted) workspace with the neighbour
+// ids passed in sorted query order (knn_spatial stage 4): the selection
+// writes whole rows of the workspace, the PPF kernel reads them back through
+// the sort's inverse permutation and writes knn_idx [b,k,n] in original
+// order together with the PPF [b,4,k,n].  Shapes outside that path (k > 32,
+// clouds of more than 2048 points, no sorted views) take the two calls it
+// replaces, with the same outputs.
+extern "C" pcr_status pcr_knn_select_ppf(const float* xyz, const float* normals, int b, int n,
+                                         int k, int relative, int* idx, float* ppf,
+                                         const void* workspace, size_t workspace_bytes,
+                                         void* stream) {
+  PCR_REQUIRE(b >= 0 && n >= 1 && k >= 1 && k <= 128, "knn_select_ppf: invalid sizes (k<=128)");
+  PCR_REQUIRE(idx != nullptr && ppf != nullptr, "knn_select_ppf: idx and ppf required");
+  if (b == 0) return PCR_OK;
+  hipStream_t st = as_stream(stream);
+  const int* sidx = nullptr;
+  const int* inv = nullptr;
+  int npad = 0;
+  // (knn_spatial checks the workspace size before launching anything)
+  const bool views = workspace != nullptr &&
+                     knn_sorted_views(const_cast<void*>(workspace), b, n, &sidx, &inv, &npad);
+  if (views && n <= kPpfSelfMaxN &&
+      knn_spatial(xyz, xyz, b, n, n, k, nullptr, idx, nullptr, nullptr, nullptr, nullptr, 0,
+                  nullptr, const_cast<void*>(workspace), workspace_bytes, true, st, 2 | 4) ==
+          PCR_OK) {
+    constexpr int SL = 8;
+    hipLaunchKernelGGL((local_ppf_self_kernel<SL>), dim3(ceil_div(n, 256), ceil_div(k, SL), b),
+                       dim3(256), (size_t)6 * n * 4, st, xyz, normals, nullptr, n, k, relative,
+                       ppf, sidx, inv, npad, idx);
+    return launch_status("knn_select_ppf");
+  }
+  const pcr_status rc = pcr_knn_local_ppf_prepared(xyz, normals, b, n, k, relative, idx, nullptr,
+                                                   nullptr, workspace, workspace_bytes, stream);
+  if (rc != PCR_OK) return rc;
+  return pcr_local_ppf_forward(xyz, normals, xyz, normals, idx, b, n, n, k, 1, relative, ppf,
+                               stream);
+}
+
 extern "C" pcr_status pcr_spherical_ppf_forward(const float* coords, const float* center,
                                                 const float* normals, const float* center_normal,
                                                 int b, int n, float* feat, void* stream) {
@@ -689,7 +743,7 @@ extern "C" pcr_status pcr_local_ppf_forward(const float* points, const float* no
 #define PCR_PPF_SELF(SLV)                                                                     \
   hipLaunchKernelGGL((local_ppf_self_kernel<SLV>), dim3(ceil_div(n, 256), ceil_div(u, SLV), b), \
                      dim3(256), (size_t)6 * n * 4, as_stream(stream), points, normals, idx, n,  \
-                     u, relative, out)
+                     u, relative, out, nullptr, nullptr, 0, nullptr)
 #define PCR_PPF_SELF_NT(SLV, NTV)                                                               \
   hipLaunchKernelGGL((local_ppf_self_kernel<SLV, NTV>), dim3(ceil_div(n, NTV), ceil_div(u, SLV), b), \
                      dim3(NTV), (size_t)6 * n * 4, as_stream(stream), points, normals, idx, n,  \

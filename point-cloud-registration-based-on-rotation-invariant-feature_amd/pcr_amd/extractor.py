@@ -107,6 +107,13 @@ class SphExtractor:
                 kws.numel(), stream), "knn_local_ppf")
             return
         lib = _lib.load()
+        if self.split_ppf and ppf and self.knn_dist is None:
+            # selection in sorted query order + the PPF launch that writes
+            # knn_idx and the PPF (pcr_knn_select_ppf)
+            _lib.check(lib.pcr_knn_select_ppf(
+                _ptr(xyz), _ptr(normals), self.b, self.n, self.k, int(self.relative), _ptr(idx),
+                _ptr(self.local_ppf), _ptr(kws), kws.numel(), stream), "knn_select_ppf")
+            return
         _lib.check(lib.pcr_knn_local_ppf_prepared(
             _ptr(xyz), _ptr(normals), self.b, self.n, self.k, int(self.relative),
             _ptr(idx), _ptr(self.knn_dist), None if self.split_ppf else

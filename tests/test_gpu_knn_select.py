@@ -117,3 +117,35 @@ def test_select_two_sets(dev):
     got = ops.knn_forward_cuda(T(x1, dev), T(x2, dev), 32)
     for a, b in zip(got, oracle.knn_forward(x1, x2, 32)):
         assert np.array_equal(N(a), b)
+
+
+@pytest.mark.parametrize("b,n,k,kind", [(4, 1024, 32, "gauss"), (2, 2048, 32, "gauss"),
+                                        (2, 1000, 16, "gauss"), (2, 1024, 32, "edge"),
+                                        (2, 1024, 48, "gauss"), (1, 3000, 32, "gauss")])
+def test_select_ppf_sorted_emit(dev, b, n, k, kind):
+    """pcr_knn_select_ppf (the extractor's selection + PPF): the selection
+    writes its ids in sorted query order and the PPF launch un-permutes them
+    into knn_idx (k <= 32, n <= 2048); the other shapes take the two-call
+    path.  Both bit-exact vs the oracle; every output poisoned first."""
+    import torch
+    from pcr_amd import _lib
+    from pcr_amd.ops import _ptr, _stream
+    if kind == "edge":
+        xyz = edge_clouds_for_knn(b, n)
+    else:
+        xyz, _, _ = gaussian_clouds(b, n, seed=n + k)
+    xyz = np.ascontiguousarray(xyz, dtype=np.float32)
+    nrm = np.ascontiguousarray(np.roll(xyz, 1, axis=1))
+    tx, tn = T(xyz, dev), T(nrm, dev)
+    lib = _lib.load()
+    ws = torch.full((lib.pcr_knn_workspace_size(b, n, n),), 0xA5, dtype=torch.uint8, device=dev)
+    idx = torch.full((b, k, n), -7, dtype=torch.int32, device=dev)
+    ppf = torch.full((b, 4, k, n), float("nan"), device=dev)
+    _lib.check(lib.pcr_knn_prepare(_ptr(tx), b, n, _ptr(ws), ws.numel(), _stream()), "prepare")
+    _lib.check(lib.pcr_knn_select_ppf(_ptr(tx), _ptr(tn), b, n, k, 1, _ptr(idx), _ptr(ppf),
+                                      _ptr(ws), ws.numel(), _stream()), "select_ppf")
+    torch.cuda.synchronize()
+    _, ei = oracle.knn_dir(xyz, xyz, k)
+    assert np.array_equal(N(idx), ei)
+    ep = oracle.local_ppf(xyz, nrm, xyz, nrm, ei, kmajor=True, relative=True)
+    assert np.array_equal(N(ppf), ep, equal_nan=True)
