@@ -744,16 +744,8 @@ extern "C" pcr_status pcr_local_ppf_forward(const float* points, const float* no
   hipLaunchKernelGGL((local_ppf_self_kernel<SLV>), dim3(ceil_div(n, 256), ceil_div(u, SLV), b), \
                      dim3(256), (size_t)6 * n * 4, as_stream(stream), points, normals, idx, n,  \
                      u, relative, out, nullptr, nullptr, 0, nullptr)
-#define PCR_PPF_SELF_NT(SLV, NTV)                                                               \
-  hipLaunchKernelGGL((local_ppf_self_kernel<SLV, NTV>), dim3(ceil_div(n, NTV), ceil_div(u, SLV), b), \
-                     dim3(NTV), (size_t)6 * n * 4, as_stream(stream), points, normals, idx, n,  \
-                     u, relative, out)
 #ifdef PCR_DIAG
-    static const int pnt = PCR_KNOB("PCR_PPF_NT", 256);
-    if (pnt == 512) PCR_PPF_SELF_NT(8, 512);
-    else if (pnt == 1024) PCR_PPF_SELF_NT(8, 1024);
-    else if (pnt == 1025) PCR_PPF_SELF_NT(16, 1024);
-    else if (sl == 16) PCR_PPF_SELF(16);
+    if (sl == 16) PCR_PPF_SELF(16);
     else if (sl == 32) PCR_PPF_SELF(32);
     else if (sl == 4) PCR_PPF_SELF(4);
     else
