@@ -353,15 +353,26 @@ constexpr int kBwdMaxG = 4;
 
 __global__ __launch_bounds__(kBwdThreads) void devox_bwd_kernel(
     const float* __restrict__ grad_y, const int* __restrict__ inds, const float* __restrict__ wgts,
-    int c, int n, int r3, int G, int hw, int skip_neg, float* __restrict__ grad_x, int dbg,
+    int c, int n, int r, int G, int hw, int skip_neg, float* __restrict__ grad_x, int dbg,
     const int* __restrict__ order) {
   extern __shared__ __align__(16) float acc_s[];  // [G][hw]
+  // spherical grads: each wave's segment sums for the 80 corner voxels
+  // (every regular spherical corner lies there; devox_fwd_sph_lds_kernel),
+  // folded into the window in wave order at the end.  One wave's LDS
+  // atomics complete in issue order and the lanes of one instruction in a
+  // fixed order, so the sums -- and the gradient -- are the same on every
+  // run; tail adds of all waves into the one window raced.
+  __shared__ float priv_s[kBwdThreads / kWave][kBwdMaxG][kSphSlots];
+  const int r3 = r * r * r;
+  const bool use_priv = skip_neg && r >= 8;  // slot -> voxel is one-to-one
   const int grp = blockIdx.x;
   const int b = blockIdx.y;
   const int tid = threadIdx.x;
   const int c0 = grp * G;
   const int gcount = min(G, c - c0);
   for (int t = tid; t < G * hw; t += kBwdThreads) acc_s[t] = 0.0f;
+  for (int t = tid; t < (kBwdThreads / kWave) * kBwdMaxG * kSphSlots; t += kBwdThreads)
+    (&priv_s[0][0][0])[t] = 0.0f;
   __syncthreads();
   const int* I = inds + (size_t)b * 8 * n;
   const float* Wt = wgts + (size_t)b * 8 * n;
@@ -472,11 +483,38 @@ __global__ __launch_bounds__(kBwdThreads) void devox_bwd_kernel(
                   e4 = (int)((mykey >> 13) & 0x3FFFFF);
         const int cq[8] = {c0, c0 + e1, c0 + e2, c0 + e2 + e1,
                            c0 + e4, c0 + e4 + e1, c0 + e4 + e2, c0 + e4 + e2 + e1};
+        int sq[8];
+        bool in80 = use_priv;
 #pragma unroll
-        for (int q = 0; q < 8; q++)
+        for (int q = 0; q < 8; q++) {
+          sq[q] = sph_slot(cq[q], r);
+          in80 &= sq[q] >= 0;
+        }
+        if (in80) {
 #pragma unroll
-          for (int g = 0; g < kBwdMaxG; g++)
-            if (g < gcount) atomicAdd(&acc_s[g * hw + cq[q]], v[q][g]);
+          for (int q = 0; q < 8; q++)
+#pragma unroll
+            for (int g = 0; g < kBwdMaxG; g++)
+              if (g < gcount) atomicAdd(&priv_s[wv][g][sq[q]], v[q][g]);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 8; q++)
+#pragma unroll
+            for (int g = 0; g < kBwdMaxG; g++)
+              if (g < gcount) atomicAdd(&acc_s[g * hw + cq[q]], v[q][g]);
+        }
+      }
+    }
+    if (use_priv) {
+      __syncthreads();
+      for (int t = tid; t < gcount * kSphSlots; t += kBwdThreads) {
+        const int g = t / kSphSlots, sl = t - g * kSphSlots;
+        float sum = priv_s[0][g][sl];
+#pragma unroll
+        for (int w = 1; w < kBwdThreads / kWave; w++) sum += priv_s[w][g][sl];
+        const int gg = sl / 40, a = (sl - gg * 40) / 5, bb = sl - gg * 40 - a * 5;
+        const int vx = gg * r * r + a * r + bb;
+        if (vx < hw) acc_s[g * hw + vx] += sum;
       }
     }
   }
@@ -1017,7 +1055,7 @@ static pcr_status devox_backward(const float* grad_y, const int* inds, const flo
   if (hw > r3) hw = r3;
   allow_big_lds(devox_bwd_kernel, (size_t)G * hw * 4);
   hipLaunchKernelGGL(devox_bwd_kernel, dim3(ceil_div(c, G), b), dim3(kBwdThreads),
-                     (size_t)G * hw * 4, as_stream(stream), grad_y, inds, wgts, c, n, r3, G, hw,
+                     (size_t)G * hw * 4, as_stream(stream), grad_y, inds, wgts, c, n, r, G, hw,
                      skip_neg, grad_x, PCR_KNOB("PCR_DEVOX_BWD_DBG", 0), order);
   return launch_status("devoxelize_backward");
 }
