@@ -40,9 +40,12 @@ struct KnnSet {
   int* pcell;    // [b][n] cell of each point
   int* pslot;    // [b][n] arrival slot inside the cell
   float* frame;  // [b][8] lo xyz, scale xyz
-  // clouds of <= kSortedMaxN points (the LDS-cached selection):
   int* inv;   // [b][n] sorted position of every point (the sort's inverse)
+  // clouds of <= kSortedMaxN points (the LDS-cached selection):
   int* sidx;  // [b][kSortedK][npad] neighbour ids in sorted query order
+  // larger clouds: the selection's keys, query-major in sorted query order
+  double* skey;  // [b][npad][kSkeyK] (d bits << 32 | index), see make_key
+  float* rec;    // [b][n][8] x y z nx ny nz - -: the emit kernel's neighbour gathers
   int n, npad, nblk;
 };
 
@@ -55,6 +58,13 @@ static inline size_t al256(size_t v) { return (v + 255) / 256 * 256; }
 // (query, slot): ~7x the write requests of the 4 MB they carry at c2
 constexpr int kSortedMaxN = 2048;
 constexpr int kSortedK = kKnnSortedK;
+// past kSortedMaxN queries the selection writes its k keys per query as one
+// contiguous row in sorted query order (a workgroup's 64 rows are one
+// contiguous range) and knn_emit_kernel un-permutes them into the outputs:
+// writing them from the selection in original order was one scattered
+// 4-byte store per (query, slot, output) -- at c5 5 x 134 M stores, which
+// slowed the whole launch by ~30%
+constexpr int kSkeyK = 64;
 
 static size_t knn_set_layout(int b, int n, KnnSet* s, char* base, size_t off) {
   const int nblk = (n + kBlk - 1) / kBlk;
@@ -75,11 +85,15 @@ static size_t knn_set_layout(int b, int n, KnnSet* s, char* base, size_t off) {
   int* pslot = big ? (int*)take((size_t)b * n * 4) : nullptr;
   float* frame = big ? (float*)take((size_t)b * 8 * 4) : nullptr;
   const bool sorted_out = n <= kSortedMaxN;
-  int* inv = sorted_out ? (int*)take((size_t)b * n * 4) : nullptr;
+  int* inv = (int*)take((size_t)b * n * 4);
   int* sidx = sorted_out ? (int*)take((size_t)b * kSortedK * npad * 4) : nullptr;
+  double* skey = sorted_out ? nullptr : (double*)take((size_t)b * npad * kSkeyK * 8);
+  float* rec = (float*)take((size_t)b * n * 8 * 4);
   if (s) {
+    s->rec = rec;
     s->inv = inv;
     s->sidx = sidx;
+    s->skey = skey;
     s->cell = cell;
     s->pcell = pcell;
     s->pslot = pslot;
@@ -347,6 +361,7 @@ __global__ __launch_bounds__(256) void knn_big_scatter_kernel(const float* __res
     s.y[o] = P[i + n];
     s.z[o] = P[i + 2 * (size_t)n];
     s.j[o] = i;
+    s.inv[(size_t)b * n + i] = (int)(o - base);
   } else if (i < s.npad) {
     s.x[base + i] = s.y[base + i] = s.z[base + i] = __builtin_nanf("");
     s.j[base + i] = -1;
@@ -1013,15 +1028,31 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
           pz = cs.z[cp];
           pj = cs.j[cp];
         }
-#pragma unroll 4
-        for (int t = 0; t < kBlk; t += 4) {
-          const float4 X = *(const float4*)(cw + t);
-          const float4 Y = *(const float4*)(cw + kBlk + t);
-          const float4 Z = *(const float4*)(cw + 2 * kBlk + t);
+        // ping-pong register sets: the next group's LDS reads are issued
+        // before this group's callback (its LDS atomics / stores), so its
+        // wait never covers them (LDS operations complete in order)
+        auto rd4 = [&](int t, float4& X, float4& Y, float4& Z) __attribute__((always_inline)) {
+          X = *(const float4*)(cw + t);
+          Y = *(const float4*)(cw + kBlk + t);
+          Z = *(const float4*)(cw + 2 * kBlk + t);
+        };
+        auto ev4 = [&](int t, const float4& X, const float4& Y, const float4& Z)
+                       __attribute__((always_inline)) {
           const pf2 d0 = cand_dist2(qx2, qy2, qz2, pf2{X.x, X.y}, pf2{Y.x, Y.y}, pf2{Z.x, Z.y});
           const pf2 d1 = cand_dist2(qx2, qy2, qz2, pf2{X.z, X.w}, pf2{Y.z, Y.w}, pf2{Z.z, Z.w});
           const float d[4] = {d0[0], d0[1], d1[0], d1[1]};
           f(cur * kBlk + t, d, uint2{0u, 0u});
+        };
+        float4 AX, AY, AZ, BX, BY, BZ;
+        rd4(0, AX, AY, AZ);
+#pragma unroll 2
+        for (int t = 0; t < kBlk; t += 8) {
+          rd4(t + 4, BX, BY, BZ);
+          __builtin_amdgcn_sched_barrier(0);
+          ev4(t, AX, AY, AZ);
+          if (t + 8 < kBlk) rd4(t + 8, AX, AY, AZ);
+          __builtin_amdgcn_sched_barrier(0);
+          ev4(t + 4, BX, BY, BZ);
         }
         cur = nxt;
       }
@@ -1073,7 +1104,23 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     // query is almost always there): the boxes are read by scalar loads, not
     // one readlane sweep over all of this wave's blocks
     constexpr int kBoundWin = 64;
-    if (!CL && qs.x == cs.x && nblk > 2 * kBoundWin + NW) {
+    if (!CL && qs.x == cs.x && nblk > 2 * kBoundWin + NW && breg) {
+      // the window's boxes of this wave are lanes [l0, l1] of its register
+      // boxes (block wv + NW (64 j + l)): v_readlane, no scalar-load chain
+      const int lo = max(0, qblk - kBoundWin), hi = min(nblk - 1, qblk + kBoundWin);
+#pragma unroll
+      for (int j = 0; j < kBoxJ; j++) {
+        const int f0 = lo - wv - NW * j * kBlk, f1 = hi - wv - NW * j * kBlk;
+        const int l0 = max(0, (f0 + NW - 1 + NW * kBlk) / NW - kBlk), l1 = min(kBlk - 1, f1 >= 0 ? f1 / NW : -1);
+        for (int l = l0; l <= l1; l++) {
+          const int blk = wv + NW * (j * kBlk + l);
+          float b6[6];
+#pragma unroll
+          for (int a = 0; a < 6; a++) b6[a] = readlane_f(bl[j][a], l);
+          if (min(kBlk, m - blk * kBlk) >= k) dq = fminf(dq, box_ub(qx, qy, qz, b6));
+        }
+      }
+    } else if (!CL && qs.x == cs.x && nblk > 2 * kBoundWin + NW) {
       const int lo = max(0, qblk - kBoundWin), hi = min(nblk - 1, qblk + kBoundWin);
       for (int blk = lo + wv; blk <= hi; blk += NW) {
         const int real = min(kBlk, m - blk * kBlk);
@@ -1394,6 +1441,21 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     }
     __syncthreads();
     PCR_STAMP(5);
+    if (sorted_emit == 2) {
+      // the workgroup's 64 rows of kSkeyK keys are one contiguous range:
+      // consecutive threads store consecutive keys (knn_emit_kernel
+      // un-permutes them)
+      kkey* rows = qs.skey + ((size_t)b * qs.npad + (size_t)qblk * kBlk) * kSkeyK;
+      for (int e = threadIdx.x; e < kBlk * k; e += NW * kBlk) {
+        const int q = e / k, sl = e - q * k;
+        rows[(size_t)q * kSkeyK + sl] = buf_s[sl * kBlk + q];
+      }
+#ifdef PCR_DIAG
+      if (threadIdx.x == 0 && PCR_WG_LINEAR < 1024)
+        pcr_diag_stamps[PCR_WG_LINEAR][15] = __builtin_amdgcn_s_memrealtime();
+#endif
+      return;
+    }
     if (!qlive) return;
 
     // output slots wv, wv + NW, ...
@@ -1481,6 +1543,11 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     }
   }
   if (!qlive) return;
+  if (sorted_emit == 2) {
+    kkey* row = qs.skey + ((size_t)b * qs.npad + (size_t)qblk * kBlk + lane) * kSkeyK;
+    for (int s2 = 0; s2 < k; s2++) row[s2] = buf_s[s2 * kBlk + lane];
+    return;
+  }
   const int n = qs.n;
   for (int s2 = 0; s2 < k; s2++) {
     const kkey x = buf_s[s2 * kBlk + lane];
@@ -1507,6 +1574,122 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
       for (int ch = 0; ch < 4; ch++) ppf[(((size_t)b * 4 + ch) * k + s2) * n + qj] = f[ch];
     }
   }
+}
+
+// Un-permutes the selection's sorted-order keys (qs.skey, sorted_emit 2)
+// into the reference's [b][k][n] outputs (knn/knn.cu:40-47 layout) and
+// computes the local PPF of every (query, slot) on the way
+// (models/pvcnn_classify.py:252-269, the same pcr_local_ppf call as the
+// selection's own epilogue).  One wave per 64 consecutive original queries
+// and 16 slots (16 contiguous keys of each query's row: one 128-byte line
+// per lane); every output store is a whole 256-byte row.
+// XCD-aware: the dispatcher deals workgroups round-robin over the 8 XCDs, so
+// work unit (blockIdx.x % 8) * (grid / 8) + blockIdx.x / 8 keeps a run of
+// consecutive query blocks -- one cloud's neighbour gathers -- in one L2.
+template <bool PPF>
+__global__ __launch_bounds__(256) void knn_emit_kernel(KnnSet qs, int k, int nqb, float* dist,
+                                                       int* idx, const float* __restrict__ qxyz,
+                                                       const float* __restrict__ qnrm,
+                                                       const float* __restrict__ crec, int m,
+                                                       int relative, float* ppf) {
+  constexpr int kChunk = kSkeyK / 4;  // slots per wave
+  constexpr int kG = 4;               // slots whose neighbours are gathered together
+  const int total = gridDim.x;
+  int u = blockIdx.x;
+  if ((total & 7) == 0) u = (u & 7) * (total >> 3) + (u >> 3);
+  const int b = u / nqb, qb = u - b * nqb;
+  const int n = qs.n;
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int qj = qb * kBlk + lane;
+  const int s0 = wv * kChunk;
+  if (qj >= n || s0 >= k) return;  // no barrier below
+  const int ns = min(k - s0, kChunk);
+  const int p = qs.inv[(size_t)b * n + qj];
+  // the wave's 16 keys of the query's row at once (one 128-byte line per
+  // lane; the row always holds kSkeyK keys, so no guard): each line is
+  // fetched once, not once per slot
+  const double2* row = (const double2*)(qs.skey + ((size_t)b * qs.npad + p) * kSkeyK + s0);
+  kkey key[kChunk];
+#pragma unroll
+  for (int i = 0; i < kChunk / 2; i++) {
+    const double2 v = row[i];
+    key[i * 2] = v.x;
+    key[i * 2 + 1] = v.y;
+  }
+  float ox = 0.0f, oy = 0.0f, oz = 0.0f, cnx = 0.0f, cny = 0.0f, cnz = 0.0f;
+  // a neighbour's point and normal as one 32-byte record (two dwordx4): one
+  // line per gather instead of six
+  const float4* rb = (const float4*)(crec + (size_t)b * m * 8);
+  if (PPF) {
+    const float* qo = qxyz + (size_t)b * 3 * n;
+    const float* qnr = qnrm + (size_t)b * 3 * n;
+    ox = qo[qj];
+    oy = qo[qj + n];
+    oz = qo[qj + 2 * n];
+    cnx = qnr[qj];
+    cny = qnr[qj + n];
+    cnz = qnr[qj + 2 * n];
+  }
+#pragma unroll
+  for (int g = 0; g < kChunk; g += kG) {
+    if (g >= ns) break;
+    float nbr[kG][6];
+#pragma unroll
+    for (int t = 0; t < kG; t++) {
+      const int j = g + t < ns ? key_idx(key[g + t]) : 0;
+      if (PPF) {
+        const float4 r0 = rb[2 * (size_t)j], r1 = rb[2 * (size_t)j + 1];
+        nbr[t][0] = r0.x;
+        nbr[t][1] = r0.y;
+        nbr[t][2] = r0.z;
+        nbr[t][3] = r0.w;
+        nbr[t][4] = r1.x;
+        nbr[t][5] = r1.y;
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < kG; t++) {
+      if (g + t >= ns) break;
+      const int sl = s0 + g + t;
+      const size_t o = ((size_t)b * k + sl) * n + qj;
+      if (idx) idx[o] = key_idx(key[g + t]);
+      if (dist) dist[o] = key_dist(key[g + t]);
+      if (PPF) {
+        float f[4];
+        pcr_local_ppf(ox, oy, oz, cnx, cny, cnz, nbr[t][0], nbr[t][1], nbr[t][2], nbr[t][3],
+                      nbr[t][4], nbr[t][5], relative, f);
+#pragma unroll
+        for (int ch = 0; ch < 4; ch++) ppf[(((size_t)b * 4 + ch) * k + sl) * n + qj] = f[ch];
+      }
+    }
+  }
+}
+
+// [b][3][m] points + normals -> [b][m][8] records (x y z nx ny nz 0 0)
+__global__ __launch_bounds__(256) void knn_pack_rec_kernel(const float* __restrict__ xyz,
+                                                           const float* __restrict__ nrm, int m,
+                                                           float* __restrict__ rec) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int b = blockIdx.y;
+  if (i >= m) return;
+  const float* P = xyz + (size_t)b * 3 * m;
+  const float* N = nrm + (size_t)b * 3 * m;
+  float4* r = (float4*)(rec + ((size_t)b * m + i) * 8);
+  r[0] = float4{P[i], P[i + m], P[i + 2 * (size_t)m], N[i]};
+  r[1] = float4{N[i + m], N[i + 2 * (size_t)m], 0.0f, 0.0f};
+}
+
+template <bool PPF>
+static void launch_emit(const KnnSet& qs, const KnnSet& cs, int b, int k, float* dist, int* idx,
+                        const float* qxyz, const float* qnrm, const float* cxyz,
+                        const float* cnrm, int relative, float* ppf, hipStream_t st) {
+  const int nqb = ceil_div(qs.n, kBlk);
+  // the candidates' records, in the candidate set's workspace
+  if (PPF)
+    hipLaunchKernelGGL(knn_pack_rec_kernel, dim3(ceil_div(cs.n, 256), b), dim3(256), 0, st, cxyz,
+                       cnrm, cs.n, cs.rec);
+  hipLaunchKernelGGL((knn_emit_kernel<PPF>), dim3(nqb * b), dim3(256), 0, st, qs, k, nqb, dist,
+                     idx, qxyz, qnrm, cs.rec, cs.n, relative, ppf);
 }
 
 template <int NW, bool PPF, int CAP = kCap, int KSEL = kSelMaxK>
@@ -1596,6 +1779,18 @@ static pcr_status launch_block(const KnnSet& qs, const KnnSet& cs, int b, int k,
 #else
   constexpr int impl = 0;
 #endif
+  const bool sel = impl == 0 && (k <= kSelMaxK || (k <= kSelMaxK64 && cs.npad > kSelCache));
+  if (sel && sorted_emit == 0 && qs.skey != nullptr) {
+    // queries past kSortedMaxN: keys in sorted query order, then un-permuted
+    if (k <= kSelMaxK)
+      launch_select<8, false>(qs, cs, b, k, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                              0, nullptr, st, 2);
+    else
+      launch_select<8, false, kCap64, kSelMaxK64>(qs, cs, b, k, nullptr, nullptr, nullptr,
+                                                  nullptr, nullptr, nullptr, 0, nullptr, st, 2);
+    launch_emit<PPF>(qs, cs, b, k, dist, idx, qxyz, qnrm, cxyz, cnrm, relative, ppf, st);
+    return PCR_OK;
+  }
   if (k <= kSelMaxK && impl == 0) {
     launch_select<8, PPF>(qs, cs, b, k, dist, idx, qxyz, qnrm, cxyz, cnrm, relative, ppf, st,
                           sorted_emit);

@@ -1,7 +1,8 @@
-"""Per-phase s_memtime stamps of the KNN selection at BASELINE c2 (diagnostic
-library lib/libpcr_amd_diag.so, `make -C <pkg>/csrc diag`).  Phases: 0->1
-bound, 1->2 count, 2->3 cut + collect, 3->4 rank, 4->5 scatter.  Not part of
-the product."""
+"""Per-phase s_memtime stamps of the KNN selection at BASELINE c2, or c5 with
+C5=1 (diagnostic library lib/libpcr_amd_diag.so, `make -C <pkg>/csrc diag`).
+Phases: 0->1 bound, 1->2 count, 2->3 cut + collect, 3->4 rank, 4->5 scatter.
+Only the first 1024 workgroups are stamped (c5: cloud 0).  Not part of the
+product."""
 import ctypes
 import os
 import sys
@@ -15,17 +16,30 @@ import torch  # noqa: E402
 from pcr_amd import _lib  # noqa: E402
 from pcr_amd.extractor import SphExtractor  # noqa: E402
 
-b, n, k = int(os.environ.get("B", 32)), int(os.environ.get("N", 1024)), 32
+C5 = os.environ.get("C5") == "1"
+b, n, k = (8, 65536, 64) if C5 else (int(os.environ.get("B", 32)), int(os.environ.get("N", 1024)), 32)
 dev = torch.device("cuda:0")
 g = torch.Generator(device=dev).manual_seed(0)
 xyz = torch.randn((b, 3, n), generator=g, device=dev)
 xyz = (xyz - xyz.mean(2, keepdim=True)).contiguous()
 nrm = torch.randn((b, 3, n), generator=g, device=dev)
-ex = SphExtractor(b, n, 8, k, 8, device=dev)
-s = torch.cuda.current_stream().cuda_stream
-ok = ex.knn_sort(xyz, s)
-for _ in range(3):
-    ex.knn_select(xyz, nrm, s, sorted_ok=ok, ppf=False)
+if C5:
+    from pcr_amd import ops  # noqa: E402
+    for _ in range(2):
+        ops.knn_local_ppf(xyz, nrm, k)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(5):
+        ops.knn_local_ppf(xyz, nrm, k)
+    e1.record()
+    torch.cuda.synchronize()
+    print("c5 knn_local_ppf: %.3f ms per call (incl. sort)" % (e0.elapsed_time(e1) / 5))
+else:
+    ex = SphExtractor(b, n, 8, k, 8, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    ok = ex.knn_sort(xyz, s)
+    for _ in range(3):
+        ex.knn_select(xyz, nrm, s, sorted_ok=ok, ppf=False)
 torch.cuda.synchronize()
 buf = (ctypes.c_ulonglong * (1024 * 16))()
 _lib.load().pcr_diag_read_knn(buf)
@@ -37,16 +51,23 @@ for p in range(1, 7):
     okp = (a[:, p] > 0) & (a[:, p - 1] > 0)
     if okp.any():
         print("phase %d->%d: median %d max %d cycles" % (p - 1, p, np.median(d[okp]), d[okp].max()))
-t0, t5 = a[:, 0][a[:, 0] > 0], a[:, 6][a[:, 6] > 0]
+t0 = a[:, 0][a[:, 0] > 0]
+t5 = a[:, 6][a[:, 6] > 0] if (a[:, 6] > 0).any() else a[:, 5][a[:, 5] > 0]
 fb = a[:, 8]
 for code in sorted(set(int(v) for v in fb if v)):
     w = np.where(fb == code)[0]
     print("cut flags %d (1 no bound, 2 cut below range, 4 over capacity, 8 refined): "
           "%d workgroups, first %s" % (code, len(w), [int(v) for v in w[:6]]))
+nv = a[:, 10]
+print("wave-0 visited blocks (all passes): median %d p90 %d max %d" % (
+    np.median(nv), np.percentile(nv, 90), nv.max()))
 print("span %d cycles over %d workgroups" % (t5.max() - t0.min(), nwg))
 rt = (a[:, 15] - a[:, 14]).astype(np.float64)
 cy = (a[:, 6] - a[:, 0]).astype(np.float64)
 okr = (a[:, 15] > 0) & (a[:, 14] > 0) & (a[:, 6] > 0)
+if not okr.any():  # sorted-key emission ends at stamp 5
+    cy = (a[:, 5] - a[:, 0]).astype(np.float64)
+    okr = (a[:, 15] > 0) & (a[:, 14] > 0) & (a[:, 5] > 0)
 if okr.any():
     print("shader clock (s_memtime / s_memrealtime at 100 MHz): median %.0f MHz; "
           "phase 0->6 median %.1f us" % (np.median(cy[okr] / rt[okr]) * 100,
