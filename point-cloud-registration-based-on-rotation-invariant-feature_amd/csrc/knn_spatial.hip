@@ -29,6 +29,12 @@ constexpr int kBigCellBits = 15;          // top Morton bits of the global sort 
 constexpr int kBigCells = 1 << kBigCellBits;
 constexpr int kBlk = 64;
 
+#ifdef PCR_DIAG
+// per wave of the first 1024 workgroups: count end, count visits, collect
+// end, collect visits, collect start (s_memtime)
+static __device__ unsigned long long pcr_diag_wave[1024][8][8];
+#endif
+
 struct KnnSet {
   float* x;   // [b][npad] sorted coordinates (NaN padding)
   float* y;
@@ -1218,6 +1224,12 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     } else {
       count_visit(lim);
     }
+#ifdef PCR_DIAG
+    if (lane == 0 && PCR_WG_LINEAR < 1024) {
+      pcr_diag_wave[PCR_WG_LINEAR][wv][0] = __builtin_amdgcn_s_memtime();
+      pcr_diag_wave[PCR_WG_LINEAR][wv][1] = (unsigned long long)nvisit;
+    }
+#endif
     __syncthreads();
     PCR_STAMP(2);
     // wave 0 finds the cut of the 64 queries (the other waves would repeat
@@ -1325,6 +1337,10 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     // 4. collect
     const float fcut = __uint_as_float(ucut);
     int slot_cut = cut0 + (slot - slot_lo);
+#ifdef PCR_DIAG
+    const int nv0 = nvisit;
+    if (lane == 0 && PCR_WG_LINEAR < 1024) pcr_diag_wave[PCR_WG_LINEAR][wv][4] = __builtin_amdgcn_s_memtime();
+#endif
     visit(fcut, std::true_type(), [&](int pos, const float (&d)[4], uint2 jp) {
       bool take[4];
 #pragma unroll
@@ -1357,6 +1373,12 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
       for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off, kWave));
       return __builtin_amdgcn_readfirstlane(v);
     };
+#ifdef PCR_DIAG
+    if (lane == 0 && PCR_WG_LINEAR < 1024) {
+      pcr_diag_wave[PCR_WG_LINEAR][wv][2] = __builtin_amdgcn_s_memtime();
+      pcr_diag_wave[PCR_WG_LINEAR][wv][3] = (unsigned long long)(nvisit - nv0);
+    }
+#endif
     const int smax = wave_max_i(lo_total), cmax = wave_max_i(cnt_c);
     const int spad = (smax + 3) & ~3, cpad = (cmax + 3) & ~3;
     for (int i = lo_total + wv; i < spad; i += NW) buf_s[i * kBlk + lane] = PCR_KEY_PAD;
@@ -1870,4 +1892,7 @@ extern "C" size_t pcr_knn_workspace_size(int b, int n, int m) {
 
 #ifdef PCR_DIAG
 PCR_DIAG_READER(pcr_diag_read_knn)
+extern "C" int pcr_diag_read_knn_wave(unsigned long long* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(pcr::pcr_diag_wave), sizeof(pcr::pcr_diag_wave));
+}
 #endif

@@ -74,3 +74,20 @@ if okr.any():
                                          np.median(rt[okr]) / 100.0))
     t14, t15 = a[:, 14][okr], a[:, 15][okr]
     print("realtime span of stamped phases over workgroups: %.1f us" % ((t15.max() - t14.min()) / 100.0))
+
+# per-wave count / collect times and visits (diagnostic library only)
+try:
+    wbuf = (ctypes.c_ulonglong * (1024 * 8 * 8))()
+    _lib.load().pcr_diag_read_knn_wave(wbuf)
+    w = np.frombuffer(wbuf, dtype=np.uint64).reshape(1024, 8, 8).astype(np.int64)[:nwg]
+    ok = (w[:, :, 0] > 0).all(1) & (a[:, 1] > 0)
+    if ok.any():
+        cnt_t = w[ok, :, 0] - a[ok, 1][:, None]
+        col_t = w[ok, :, 2] - w[ok, :, 4]
+        for name, t, v in (("count", cnt_t, w[ok, :, 1]), ("collect", col_t, w[ok, :, 3])):
+            print("%s: wave time median %d, max/mean over a workgroup's waves median %.2f; "
+                  "visits per wave mean %.1f max %.1f; cycles per visit (sum t / sum v) %.0f" % (
+                      name, np.median(t), np.median(t.max(1) / np.maximum(t.mean(1), 1)),
+                      v.mean(), v.max(1).mean(), t.sum() / max(v.sum(), 1)))
+except AttributeError:
+    pass
