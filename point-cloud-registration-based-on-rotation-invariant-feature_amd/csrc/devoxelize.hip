@@ -209,13 +209,24 @@ __global__ __launch_bounds__(kSphFwdThreads) void devox_fwd_sph_lds_kernel(
 // same 80-slot LDS staging as devox_fwd_sph_lds_kernel, with the corner
 // indices / weights prep already computed (dinds / dwgts) and the per-cloud
 // max-pooled descriptor.  One workgroup of 1024 threads per (cloud, group of
-// up to 64 channels) covers every point of its cloud (n <= 4096, up to four
-// points per thread, their corner slots and weights in registers), so the
-// descriptor needs no cross-workgroup step.  Replaces re-forming every
-// voxel mean from the features per channel group (vox_grid_kernel<2>, 0.94
-// ms at the c3 shape) with a read of the 80 corner values per channel.
+// up to 64 channels) covers every point of its cloud (n <= 4096), so the
+// descriptor needs no cross-workgroup step.  Lane = channel: the points are
+// taken in chunks of 1024 whose corner slots and weights go to LDS once;
+// then each wave walks 64 consecutive points of the chunk, reading a point's
+// slots and weights as broadcasts and its eight corner values at
+// channel * 81 + slot, which are 32 distinct banks for 32 consecutive
+// channels (81 = 17 mod 32, odd): no conflicts.  (Lane = point made the
+// eight reads random slots of one channel row, ~4-way conflicts: 211 us at
+// the c3 shape.)  Four consecutive points' outputs of a channel leave as one
+// 16-byte store.  Replaces re-forming every voxel mean from the features per
+// channel group (vox_grid_kernel<2>, 0.94 ms at the c3 shape) with a read of
+// the 80 corner values per channel.  Same corners, weights and wsum8 order
+// as the reference path, so the same bits; the descriptor is a max (order
+// free).
 constexpr int kGridDevoxThreads = 1024;
-constexpr int kGridDevoxPts = 4;
+constexpr int kGridDevoxChunk = 1024;  // points whose corners sit in LDS at once
+constexpr int kGridDevoxOut = 255;     // slot byte of a corner outside the 80-slot set
+constexpr int kGridDevoxMaxN = 4096;
 __global__ __launch_bounds__(kGridDevoxThreads) void devox_grid_desc_kernel(
     const float* __restrict__ grid, const int* __restrict__ dinds,
     const float* __restrict__ dwgts, int c, int n, int r, float* __restrict__ devox,
@@ -224,12 +235,17 @@ __global__ __launch_bounds__(kGridDevoxThreads) void devox_grid_desc_kernel(
   // zero-weight corner, e.g. all of a dropped point's: +0 * 0 terms, so the
   // point's output is +0 like the reference's untouched zero)
   constexpr int kStride = kSphSlots + 1;
+  constexpr int kW = kGridDevoxThreads / kWave;
   __shared__ float val_s[kSphFwdCG * kStride];
-  __shared__ float red_s[kGridDevoxThreads / kWave][kSphFwdCG];
+  __shared__ __align__(16) float pw_s[kGridDevoxChunk][8];              // corner weights
+  __shared__ __align__(8) unsigned char psl_s[kGridDevoxChunk][8];     // corner slots
+  __shared__ int pgi_s[kGridDevoxChunk][8];                            // corner voxels (slow path)
+  __shared__ float red_s[kW][kSphFwdCG];
   const int b = blockIdx.y;
   const int c0 = blockIdx.x * kSphFwdCG;
   const int cn = min(kSphFwdCG, c - c0);
   const int tid = threadIdx.x;
+  const int wv = tid >> 6, lane = tid & 63;
   const int r2 = r * r, r3 = r2 * r;
   const float* F = grid + ((size_t)b * c + c0) * r3;
   for (int t = tid; t < cn * kStride; t += kGridDevoxThreads) {
@@ -239,61 +255,93 @@ __global__ __launch_bounds__(kGridDevoxThreads) void devox_grid_desc_kernel(
     const int v = g * r2 + a * r + bb;
     val_s[t] = (sl < kSphSlots && v < r3) ? F[(size_t)ch * r3 + v] : 0.0f;
   }
-  // corners of this thread's points (prep's dinds / dwgts; a dropped point
-  // has inds {-1, 0, ...} and zero weights)
-  int sl[kGridDevoxPts][8], gi[kGridDevoxPts][8];
-  float w[kGridDevoxPts][8];
-  bool all_lds = true;
   const int* I = dinds + (size_t)b * 8 * n;
   const float* Wt = dwgts + (size_t)b * 8 * n;
-#pragma unroll
-  for (int u = 0; u < kGridDevoxPts; u++) {
-    const int i = u * kGridDevoxThreads + tid;
-#pragma unroll
-    for (int q = 0; q < 8; q++) {
-      const int v = i < n ? I[i + (size_t)q * n] : 0;
-      w[u][q] = i < n ? Wt[i + (size_t)q * n] : 0.0f;
-      gi[u][q] = v;
-      sl[u][q] = w[u][q] == 0.0f ? kSphSlots : sph_slot(v, r);
-      if (i < n && sl[u][q] < 0) all_lds = false;
-    }
-  }
-  const bool fast = __syncthreads_and(all_lds);  // also the staging barrier
-  float* O = devox + ((size_t)b * c + c0) * n;
-  const int wv = tid >> 6;
-  for (int ch = 0; ch < cn; ch++) {
-    const float* vs = val_s + ch * kStride;
-    float m = -__builtin_inff();
-#pragma unroll
-    for (int u = 0; u < kGridDevoxPts; u++) {
-      const int i = u * kGridDevoxThreads + tid;
-      if (i < n) {
-        float fv[8];
+  const int ch = lane;
+  const bool live = ch < cn;
+  const float* vs = val_s + (live ? ch : 0) * kStride;
+  const float* Fc = F + (size_t)(live ? ch : 0) * r3;
+  float* O = devox + ((size_t)b * c + c0 + (live ? ch : 0)) * n;
+  // 16-byte stores when every channel row starts 16-byte aligned
+  const bool vec4 = (n & 3) == 0 && (reinterpret_cast<uintptr_t>(devox) & 15) == 0;
+  float m = -__builtin_inff();
+  for (int p0 = 0; p0 < n; p0 += kGridDevoxChunk) {
+    // corners of the chunk's points (prep's dinds / dwgts; a dropped point
+    // has inds {-1, 0, ...} and zero weights)
+    bool all_lds = true;
+    {
+      const int i = p0 + tid;
+      if (tid < kGridDevoxChunk && i < n) {
+        unsigned lo = 0u, hi = 0u;
 #pragma unroll
         for (int q = 0; q < 8; q++) {
-          if (fast)
-            fv[q] = vs[sl[u][q]];
+          const int v = I[i + (size_t)q * n];
+          const float w = Wt[i + (size_t)q * n];
+          int sl = w == 0.0f ? kSphSlots : sph_slot(v, r);
+          if (sl < 0) {
+            all_lds = false;
+            sl = kGridDevoxOut;
+          }
+          pw_s[tid][q] = w;
+          pgi_s[tid][q] = v;
+          if (q < 4)
+            lo |= (unsigned)sl << (8 * q);
           else
-            fv[q] = sl[u][q] >= 0 ? vs[sl[u][q]]
-                                  : ((gi[u][q] >= 0 && gi[u][q] < r3)
-                                         ? F[(size_t)ch * r3 + gi[u][q]] : 0.0f);
+            hi |= (unsigned)sl << (8 * (q - 4));
         }
-        const float v = pcr_wsum8(w[u], fv);
-        O[(size_t)ch * n + i] = v;
-        m = fmaxf(m, v);
+        *(uint2*)psl_s[tid] = uint2{lo, hi};
       }
     }
-    if (desc) {
-      m = wave_max(m);
-      if ((tid & 63) == 0) red_s[wv][ch] = m;
+    const bool fast = __syncthreads_and(all_lds);  // also the staging barrier
+    const int pn = min(kGridDevoxChunk, n - p0);
+    // wave wv: points [wv * 64, wv * 64 + 64) of the chunk, four at a time
+    const int q0 = wv * kWave;
+    for (int qq = q0; qq < min(pn, q0 + kWave); qq += 4) {
+      float v4[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int pi = qq + u;
+        v4[u] = 0.0f;
+        if (pi < pn) {
+          const uint2 sp = *(const uint2*)psl_s[pi];
+          const float4 wa = *(const float4*)&pw_s[pi][0];
+          const float4 wb = *(const float4*)&pw_s[pi][4];
+          const float w[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
+          float fv[8];
+#pragma unroll
+          for (int q = 0; q < 8; q++) {
+            const int sl = (int)(((q < 4 ? sp.x : sp.y) >> (8 * (q & 3))) & 0xFFu);
+            if (fast || sl != kGridDevoxOut) {
+              fv[q] = vs[sl];
+            } else {
+              const int gi = pgi_s[pi][q];
+              fv[q] = (gi >= 0 && gi < r3) ? Fc[gi] : 0.0f;
+            }
+          }
+          v4[u] = pcr_wsum8(w, fv);
+          m = fmaxf(m, v4[u]);
+        }
+      }
+      if (live) {
+        const int i = p0 + qq;
+        if (vec4 && qq + 4 <= pn) {
+          *(float4*)(O + i) = float4{v4[0], v4[1], v4[2], v4[3]};
+        } else {
+#pragma unroll
+          for (int u = 0; u < 4; u++)
+            if (qq + u < pn) O[i + u] = v4[u];
+        }
+      }
     }
+    lds_only_barrier();  // the chunk's corner reads are done before the next chunk's writes
   }
   if (desc) {
+    red_s[wv][ch] = m;
     lds_only_barrier();
     if (tid < cn) {
-      float m = red_s[0][tid];
-      for (int q = 1; q < kGridDevoxThreads / kWave; q++) m = fmaxf(m, red_s[q][tid]);
-      desc[(size_t)b * c + c0 + tid] = m;
+      float mm = red_s[0][tid];
+      for (int q = 1; q < kW; q++) mm = fmaxf(mm, red_s[q][tid]);
+      desc[(size_t)b * c + c0 + tid] = mm;
     }
   }
 }
@@ -639,9 +687,9 @@ extern "C" pcr_status pcr_spherical_trilinear_devoxelize_forward(int r, int is_t
 extern "C" pcr_status pcr_extractor_grid_devox(const float* grid, const int* dinds,
                                                const float* dwgts, int b, int c, int n, int r,
                                                float* devox, float* desc, void* stream) {
-  PCR_REQUIRE(b >= 0 && c >= 1 && n >= 1 && n <= kGridDevoxPts * kGridDevoxThreads && r >= 1,
+  PCR_REQUIRE(b >= 0 && c >= 1 && n >= 1 && n <= kGridDevoxMaxN && r >= 1,
               "extractor_grid_devox: invalid sizes b=%d c=%d n=%d r=%d (n <= %d)", b, c, n, r,
-              kGridDevoxPts * kGridDevoxThreads);
+              kGridDevoxMaxN);
   PCR_REQUIRE((int64_t)r * r * r < (1ll << 31) / 64, "extractor_grid_devox: resolution too large");
   if (b == 0) return PCR_OK;
   hipLaunchKernelGGL(devox_grid_desc_kernel, dim3(ceil_div(c, kSphFwdCG), b),
