@@ -804,6 +804,16 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     const float* __restrict__ qxyz, const float* __restrict__ qnrm,
     const float* __restrict__ cxyz, const float* __restrict__ cnrm, int relative,
     float* __restrict__ ppf, int sorted_emit) {
+#ifdef PCR_DIAG
+  // experiment bits (diagnostic build only): 1 count without LDS atomics,
+  // 2 candidates from registers instead of LDS, 4 stop after the count,
+  // 8 stop after the collect, 16 collect without stores
+  const int dbg = sorted_emit >> 8;
+  sorted_emit &= 0xFF;
+  int dbg_sink = 0;
+#else
+  constexpr int dbg = 0;
+#endif
   constexpr int FPD = 32 / CB;              // wave fields per counter dword
   constexpr int NG = (NW + FPD - 1) / FPD;  // counter dwords per (bin, lane)
   // the histogram is dead once the cut is chosen: the collected keys reuse it
@@ -911,6 +921,17 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
       // the ids of the wave's 8 candidates (u16) are read with them only
       // when the callback uses them (the collect pass)
       auto rd = [&](int o, float4 (&X)[2], float4 (&Y)[2], float4 (&Z)[2], uint4& J) {
+        if (dbg & 2) {
+          const float f = (float)o * 1e-3f;
+#pragma unroll
+          for (int h = 0; h < 2; h++) {
+            X[h] = float4{f, f + 1.0f, f + 2.0f, f + 3.0f};
+            Y[h] = float4{f - 1.0f, f, f + 0.5f, f - 0.5f};
+            Z[h] = float4{f * 0.5f, f * 0.25f, f, f + 0.25f};
+          }
+          if (WANT_J) J = uint4{(unsigned)o, (unsigned)o + 1u, (unsigned)o + 2u, (unsigned)o + 3u};
+          return;
+        }
 #pragma unroll
         for (int h = 0; h < 2; h++) {
           X[h] = *(const float4*)(cand_s + o + 4 * h);
@@ -1182,6 +1203,12 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
 #pragma unroll
       for (int h = 0; h < 4; h++) {
         const int e = med3_i32((int)(__float_as_uint(d[h]) >> sh), base, top);
+#ifdef PCR_DIAG
+        if (dbg & 1) {
+          dbg_sink += e;
+          continue;
+        }
+#endif
         __hip_atomic_fetch_add(hwb + e * kBlk, inc, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_WORKGROUP);
       }
@@ -1317,6 +1344,12 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
       diag_reason |= 8;
 #endif
     }
+#ifdef PCR_DIAG
+    if (dbg & 4) {
+      if (dbg_sink == 0x7fffffff) hist_s[lane] = (unsigned)dbg_sink;
+      return;
+    }
+#endif
     fallback = __any(qlive && bstar < 0) || __any(overflow());
     if (qlive && !fallback) {
       ucut = (unsigned)(base + bstar + 1) << shift;
@@ -1354,7 +1387,7 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
 #pragma unroll
         for (int h = 0; h < 4; h++) {
           // exec-masked: only the taking lanes store (few lanes of a wave)
-          if (take[h]) {
+          if (take[h] && !(dbg & 16)) {
             const bool lo = __float_as_uint(d[h]) < ulo;
             buf_s[(lo ? slot_lo : slot_cut) * kBlk + lane] = make_key(d[h], j4[h]);
             slot_lo += lo ? 1 : 0;
@@ -1367,6 +1400,9 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     // rows past a lane's own count, up to the wave-wide maximum rounded to
     // four (the sweep reads four rows per wait: eight made this phase the
     // kernel's VGPR peak, 94 instead of 72), read as padding
+#ifdef PCR_DIAG
+    if (dbg & 8) return;
+#endif
     const int cnt_c = total - lo_total;
     auto wave_max_i = [&](int v) {
 #pragma unroll
@@ -1725,7 +1761,8 @@ static void launch_select(const KnnSet& qs, const KnnSet& cs, int b, int k, floa
   const dim3 grid(qs.nblk, b), blk(NW * 64);
 #define PCR_SEL(CBV, CLV, CACHEV)                                                             \
   hipLaunchKernelGGL((knn_select_kernel<NW, CBV, CLV, PPF, CAP, KSEL, CACHEV>), grid, blk, 0, st, \
-                     qs, cs, k, dist, idx, qxyz, qnrm, cxyz, cnrm, relative, ppf, sorted_emit)
+                     qs, cs, k, dist, idx, qxyz, qnrm, cxyz, cnrm, relative, ppf,              \
+                     sorted_emit | (PCR_KNOB("PCR_KNN_DBG", 0) << 8))
   if constexpr (CAP == kCap) {
     // c3 clouds (2048 points): 32 KB of candidates in LDS, two workgroups per CU
     if (cs.npad > kSelCache && cs.npad <= 2 * kSelCache) {
