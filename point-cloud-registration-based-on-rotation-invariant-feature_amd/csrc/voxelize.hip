@@ -1127,6 +1127,128 @@ __global__ __launch_bounds__(256) void avg_vox_grad_kernel(const float* __restri
     if (j < jn) gx[(size_t)j * n] = v[j] * inv;
 }
 
+// The same gather for clouds of <= 2048 points, in voxel-row order: one
+// workgroup of 1024 threads per (cloud, kGradSortCG channels) counting-sorts
+// its points by 32-voxel row (ind >> 5, one 128-byte line of a channel's
+// gradient row) in LDS, so each wave's gathers of a channel fall in a few
+// lines instead of 64 (a point-order wave touches ~64 lines of a 128 KB row:
+// the kernel above is bound by that request rate, 0.49 ms at the c3 shape);
+// the values go to LDS at the points' original positions and leave as
+// coalesced rows.  Each output is the same single product as above, in any
+// order, so the same bits.
+constexpr int kGradSortThreads = 1024;
+constexpr int kGradSortMaxN = 2048;
+constexpr int kGradSortCG = 16;  // channels per workgroup
+constexpr int kGradSortU = 4;    // channels gathered per pass
+constexpr int kGradSortMaxRows = 8192;
+__global__ __launch_bounds__(kGradSortThreads) void avg_vox_grad_sorted_kernel(
+    const float* __restrict__ grad_y, const int* __restrict__ ind, const int* __restrict__ cnt,
+    int c, int n, int r3, float* __restrict__ grad_x) {
+  constexpr int PT = kGradSortMaxN / kGradSortThreads;  // points per thread
+  // row counters (then starts), reused as the output staging rows
+  __shared__ int un_s[kGradSortU * kGradSortMaxN > kGradSortMaxRows + 1
+                          ? kGradSortU * kGradSortMaxN : kGradSortMaxRows + 1];
+  __shared__ int spos_s[kGradSortMaxN];              // voxel of sorted point s (0 if dropped)
+  __shared__ float sinv_s[kGradSortMaxN];            // 1 / count of its voxel (0 if dropped)
+  __shared__ unsigned short sidx_s[kGradSortMaxN];   // its original index
+  __shared__ int scan_s[kGradSortThreads / kWave + 1];
+  int* cnt_s = un_s;
+  float* out_s = (float*)un_s;
+  const int b = blockIdx.y;
+  const int c0 = blockIdx.x * kGradSortCG;
+  const int cn = min(kGradSortCG, c - c0);
+  const int tid = threadIdx.x;
+  const int rows = (r3 + 31) >> 5;  // + 1: the bin of dropped points
+  for (int t = tid; t <= rows; t += kGradSortThreads) cnt_s[t] = 0;
+  lds_only_barrier();
+  int key[PT], slot[PT], pos[PT];
+  float inv[PT];
+#pragma unroll
+  for (int u = 0; u < PT; u++) {
+    const int i = u * kGradSortThreads + tid;
+    key[u] = -1;
+    if (i < n) {
+      int p = ind[(size_t)b * n + i];
+      bool ok = p >= 0 && p < r3;
+      float iv = 0.0f;
+      if (ok) {
+        const int ct = cnt[(size_t)b * r3 + p];
+        ok = ct > 0;
+        if (ok) iv = pcr_inv_count(ct);
+      }
+      pos[u] = ok ? p : 0;
+      inv[u] = iv;
+      key[u] = ok ? (p >> 5) : rows;
+      slot[u] = atomicAdd(&cnt_s[key[u]], 1);
+    }
+  }
+  lds_only_barrier();
+  // exclusive scan of rows + 1 counters, kGradSortMaxRows / 1024 + 1 per thread
+  {
+    constexpr int CPT = (kGradSortMaxRows + 1 + kGradSortThreads - 1) / kGradSortThreads;
+    int v[CPT], sum = 0;
+#pragma unroll
+    for (int q = 0; q < CPT; q++) {
+      const int rr = tid * CPT + q;
+      v[q] = rr <= rows ? cnt_s[rr] : 0;
+      sum += v[q];
+    }
+    int run = block_inclusive_scan(sum, scan_s) - sum;
+#pragma unroll
+    for (int q = 0; q < CPT; q++) {
+      const int rr = tid * CPT + q;
+      if (rr <= rows) cnt_s[rr] = run;
+      run += v[q];
+    }
+  }
+  lds_only_barrier();
+#pragma unroll
+  for (int u = 0; u < PT; u++) {
+    if (key[u] >= 0) {
+      const int s2 = cnt_s[key[u]] + slot[u];
+      spos_s[s2] = pos[u];
+      sinv_s[s2] = inv[u];
+      sidx_s[s2] = (unsigned short)(u * kGradSortThreads + tid);
+    }
+  }
+  lds_only_barrier();  // counters dead: un_s becomes the output rows
+  for (int j0 = 0; j0 < cn; j0 += kGradSortU) {
+    const int jn = min(kGradSortU, cn - j0);
+    const float* gy = grad_y + ((size_t)b * c + c0 + j0) * r3;
+    float v[PT][kGradSortU];
+#pragma unroll
+    for (int u = 0; u < PT; u++) {
+      const int s2 = u * kGradSortThreads + tid;
+      const int p = s2 < n ? spos_s[s2] : 0;
+#pragma unroll
+      for (int q = 0; q < kGradSortU; q++) v[u][q] = (s2 < n && q < jn) ? gy[(size_t)q * r3 + p] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < PT; u++) {
+      const int s2 = u * kGradSortThreads + tid;
+      if (s2 < n) {
+        const float iv = sinv_s[s2];
+        const int i = sidx_s[s2];
+#pragma unroll
+        for (int q = 0; q < kGradSortU; q++) out_s[q * kGradSortMaxN + i] = v[u][q] * iv;
+      }
+    }
+    lds_only_barrier();
+    float* gx = grad_x + ((size_t)b * c + c0 + j0) * n;
+#pragma unroll
+    for (int q = 0; q < kGradSortU; q++) {
+      if (q < jn) {
+#pragma unroll
+        for (int u = 0; u < PT; u++) {
+          const int i = u * kGradSortThreads + tid;
+          if (i < n) gx[(size_t)q * n + i] = out_s[q * kGradSortMaxN + i];
+        }
+      }
+    }
+    lds_only_barrier();  // rows read before the next pass writes them
+  }
+}
+
 // ------------------------------------------------------ normalize only
 __global__ __launch_bounds__(kPrepThreads) void sph_normalize_kernel(
     const float* __restrict__ coords, int n, int E, float* __restrict__ out) {
@@ -1653,6 +1775,12 @@ extern "C" pcr_status pcr_avg_voxelize_backward(const float* grad_y, const int* 
                                                 float* grad_x, void* stream) {
   PCR_REQUIRE(b >= 0 && c >= 0 && n >= 0 && r3 >= 1, "avg_voxelize_backward: invalid sizes");
   if (b == 0 || c == 0 || n == 0) return PCR_OK;
+  if (n <= kGradSortMaxN && (r3 + 31) / 32 <= kGradSortMaxRows) {
+    hipLaunchKernelGGL(avg_vox_grad_sorted_kernel, dim3(ceil_div(c, kGradSortCG), b),
+                       dim3(kGradSortThreads), 0, as_stream(stream), grad_y, ind, cnt, c, n, r3,
+                       grad_x);
+    return launch_status("avg_voxelize_backward");
+  }
   hipLaunchKernelGGL(avg_vox_grad_kernel, dim3(ceil_div(n, 256), ceil_div(c, kGradCG), b),
                      dim3(256), 0, as_stream(stream), grad_y, ind, cnt, c, n, r3, grad_x);
   return launch_status("avg_voxelize_backward");
