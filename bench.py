@@ -86,6 +86,11 @@ def parse(argv=None):
                     help="diagnostic: no timing events around the dominant kernel")
     ap.add_argument("--no-verify", action="store_true",
                     help="diagnostic: skip the output check before the warm-up")
+    ap.add_argument("--c3-schedule", choices=("pipelined", "serial"), default="pipelined",
+                    help="c3: pipelined = each batch's KNN + local PPF on a side stream one "
+                         "batch ahead, overlapping the previous step's backwards "
+                         "(SphExtractor.pipelined_steps); serial = forward (joined), then "
+                         "the backwards")
     ap.add_argument("--steps-per-launch", type=int, default=40,
                     help="most pipelined steps per native runner call (extract / pairs); "
                          "--steps and --warmup are split into calls of at most this many")
@@ -418,26 +423,74 @@ class C3Workload:
         self.step_bytes = fwd * b + self.devox_bwd_bytes + vox_bwd * b
         self.t = []
 
+    def _backward(self, out, ev=None):
+        """The step's backward share: devox backward of the synthetic
+        upstream gradient, then voxelize backward of the gradient grid."""
+        ops = self.ops
+        if ev is not None:
+            ev[0].record()
+        gg = ops.spherical_trilinear_devoxelize_backward(self.gy, out["dinds"], out["dwgts"],
+                                                         self.args.res)
+        if ev is not None:
+            ev[1].record()
+        gx = ops.spherical_avg_voxelize_backward(gg, out["ind"], out["cnt"])
+        return gg, gx
+
+    def _serial(self, steps, timed, keep=None):
+        xyz, nrm, feat = self.inputs
+        for s in range(steps):
+            out = self.ex.forward(xyz, nrm, feat)
+            res = self._backward(out, self.ev[s] if timed else None)
+            if keep is not None:
+                keep.append((out, res))
+
+    def _pipelined(self, steps, timed, keep=None):
+        def consume(s, out):
+            res = self._backward(out, self.ev[s] if timed else None)
+            if keep is not None:
+                keep.append(({kk: v.clone() for kk, v in out.items()}, res))
+        self.ex.pipelined_steps(steps, lambda s: self.inputs, consume)
+
     def verify(self):
-        return None
+        """Three pipelined steps vs the serial forward + backwards: every
+        forward output of the last step and both backward results must be
+        identical (outputs poisoned first)."""
+        if self.args.c3_schedule == "serial":
+            return None
+        ref = []
+        self._serial(1, False, ref)
+        ref = ({kk: v.clone() for kk, v in ref[0][0].items()}, [t.clone() for t in ref[0][1]])
+        for t in [self.ex.local_ppf, self.ex.knn_idx, self.ex.grid, self.ex.devox, self.ex.ind,
+                  self.ex.cnt] + [self.ex._ppf(1), self.ex._set(1)[4]]:
+            t.view(-1).view(torch.uint8).fill_(0xFF)
+        got = []
+        self._pipelined(3, False, got)
+        torch.cuda.synchronize(self.dev)
+        out, res = got[-1]
+        for key in ("knn_idx", "local_ppf", "ind", "cnt", "grid", "devox", "desc"):
+            if not torch.equal(out[key], ref[0][key]) and not torch.allclose(
+                    out[key], ref[0][key], equal_nan=True):
+                raise SystemExit("bench: pipelined c3 output %s differs from the serial path"
+                                 % key)
+        # the backwards are atomics-free gathers: bit-identical run to run
+        for name, a, b in zip(("devox backward", "vox backward"), res, ref[1]):
+            if not torch.equal(a, b):
+                raise SystemExit("bench: pipelined c3 %s differs from the serial path" % name)
+        return True
 
     def prepare_timing(self):
         self.ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                    for _ in range(self.args.steps)]
 
     def run(self, steps, timed):
-        ops, r = self.ops, self.args.res
-        xyz, nrm, feat = self.inputs
-        for s in range(steps):
-            # one step through the extractor's stage kernels (the native runner's
-            # split grid-stream kernel is built for N <= 1024)
-            out = self.ex.forward(xyz, nrm, feat)
-            if timed and not self.args.no_kernel_timing:
-                self.ev[s][0].record()
-            gg = ops.spherical_trilinear_devoxelize_backward(self.gy, out["dinds"], out["dwgts"], r)
-            if timed and not self.args.no_kernel_timing:
-                self.ev[s][1].record()
-            ops.spherical_avg_voxelize_backward(gg, out["ind"], out["cnt"])
+        # the extractor's stage kernels from Python (pipelined: the split
+        # voxel stage -- means + devox, then the dense-grid stream -- on the
+        # caller's stream, KNN + PPF one batch ahead on s_nbr)
+        t = timed and not self.args.no_kernel_timing
+        if self.args.c3_schedule == "serial":
+            self._serial(steps, t)
+        else:
+            self._pipelined(steps, t)
         self.timed_steps = steps if timed else 0
         return steps
 
@@ -463,7 +516,8 @@ class C3Workload:
                 "clouds_per_gpu": a.batch, "points": a.points, "k": a.k,
                 "resolution": a.res, "channels": a.channels,
                 "global_batch": a.batch * self.world,
-                "parallelism": "dp%d (clouds sharded, no collective)" % self.world}
+                "parallelism": "dp%d (clouds sharded, no collective)" % self.world,
+                "schedule": a.c3_schedule}
 
 
 class C5Workload:

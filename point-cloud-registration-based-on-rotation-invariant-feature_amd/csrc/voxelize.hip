@@ -723,13 +723,13 @@ __global__ __launch_bounds__(NT) void vox_grid_kernel(
 // before any is used: one round trip instead of a chain of dependent loads,
 // which under the grid stream's write traffic take microseconds each.
 constexpr int kMeansNT = 256;
-constexpr int kMeansMaxN = 1024;
-template <int G>
-__global__ __launch_bounds__(kMeansNT) void vox_means_kernel(
+constexpr int kMeansPB = 4;  // points per thread: clouds of <= 4 NT points
+constexpr int kMeansMaxN = 2 * kMeansPB * kMeansNT;  // NT = 512 past 4 kMeansNT points (c3)
+template <int G, int NT>
+__global__ __launch_bounds__(NT) void vox_means_kernel(
     const float* __restrict__ feat, int c, int n, VoxWs ws, const float* __restrict__ dwgts,
     float* __restrict__ devox, float* __restrict__ desc, int ngrp) {
-  constexpr int NT = kMeansNT;
-  constexpr int PB = kMeansMaxN / NT;  // points per thread
+  constexpr int PB = kMeansPB;
   extern __shared__ __align__(16) unsigned char smem_raw[];
   // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs, so with
   // a batch of a multiple of 8 clouds XCD x runs every channel group of
@@ -879,7 +879,7 @@ __global__ __launch_bounds__(kMeansNT) void vox_means_kernel(
 constexpr int kStreamG = 2;      // channels per item
 constexpr int kStreamNG = 9;     // 1 KB LDS-DMA pieces per item: two rows of ms <= 1152 floats
 constexpr int kStreamNB = 3;     // means buffers (item t streams, t+1 ready, t+2 landing)
-constexpr int kStreamMaxN = 1024;
+constexpr int kStreamMaxN = 2048;  // two rows of ms <= 2052 floats: 17 pieces past 1024 points
 constexpr int kStreamMaxW = 1024;  // occupancy words (r^3 <= 32768)
 
 typedef __attribute__((address_space(3))) void* lds_void_p;
@@ -1843,17 +1843,20 @@ extern "C" pcr_status pcr_extractor_voxel_means_devox(const float* features, int
     // G channels per workgroup (G = 2: ~24 KB of LDS, so it fits beside the
     // KNN selection's workgroups); every workgroup of a cloud reads the
     // cloud's corner data, so a larger G reads less of it in all
-#define PCR_LAUNCH_MEANS(GV)                                                                  \
+#define PCR_LAUNCH_MEANS(GV, NTV)                                                             \
   do {                                                                                       \
     const int ngrp = ceil_div(c, GV);                                                        \
     const size_t smem = ((size_t)GV * n + (size_t)GV * (n + 1) + n + (n + 1)) * 4;           \
-    allow_big_lds(vox_means_kernel<GV>, smem);                                               \
-    hipLaunchKernelGGL((vox_means_kernel<GV>), dim3(ngrp * b), dim3(kMeansNT), smem,         \
+    allow_big_lds(vox_means_kernel<GV, NTV>, smem);                                          \
+    hipLaunchKernelGGL((vox_means_kernel<GV, NTV>), dim3(ngrp * b), dim3(NTV), smem,         \
                        as_stream(stream), features, c, n, ws, dwgts, devox, desc, ngrp);     \
   } while (0)
-    if (mg == 4) PCR_LAUNCH_MEANS(4);
-    else if (mg == 8) PCR_LAUNCH_MEANS(8);
-    else PCR_LAUNCH_MEANS(2);
+    // clouds of more than 1024 points (c3: 2048): 512 threads, the same four
+    // points per thread
+    if (n > kMeansPB * kMeansNT) PCR_LAUNCH_MEANS(2, 2 * kMeansNT);
+    else if (mg == 4) PCR_LAUNCH_MEANS(4, kMeansNT);
+    else if (mg == 8) PCR_LAUNCH_MEANS(8, kMeansNT);
+    else PCR_LAUNCH_MEANS(2, kMeansNT);
 #undef PCR_LAUNCH_MEANS
     return launch_status(name);
   }
@@ -1908,9 +1911,11 @@ extern "C" pcr_status pcr_extractor_voxel_stream(int b, int c, int n, int r, int
   // slower in the step despite half the index work per store)
   static const int gk = PCR_KNOB("PCR_STREAM_G", kStreamG);
   static const int nbk = PCR_KNOB("PCR_STREAM_NB", 0);
-  const int G = gk == 8 ? 8 : gk == 4 ? 4 : 2;
-  const int NGP = G == 8 ? 33 : G == 4 ? 17 : 9;  // 1 KB pieces holding G rows of ms floats
-  const int NB = G == 2 ? kStreamNB : (G == 4 && nbk == 3) ? 3 : 2;
+  // clouds of more than 1024 points (c3): two channels, 17 pieces per item
+  const bool wide = n > 1024;
+  const int G = wide ? 2 : gk == 8 ? 8 : gk == 4 ? 4 : 2;
+  const int NGP = G == 8 ? 33 : (G == 4 || wide) ? 17 : 9;  // 1 KB pieces holding G rows of ms floats
+  const int NB = (G == 2 || wide) ? kStreamNB : (G == 4 && nbk == 3) ? 3 : 2;
   PCR_REQUIRE(G * ws.ms * 4 <= NGP * 1024, "%s: means rows too long", name);
   const int ngrp = ceil_div(c, G);
   // a few workgroups per cloud (about one per CU in all), each a contiguous
@@ -1936,6 +1941,8 @@ extern "C" pcr_status pcr_extractor_voxel_stream(int b, int c, int n, int r, int
                        dim3((NSV + 1) * 64), smem, as_stream(stream), c, n, r3, ws, grid, cnt, \
                        ngrp, wpc, per, dbg);                                                  \
   } while (0)
+  if (wide) PCR_LAUNCH_STREAM(4, kStreamNB, 2, 16, kStreamG, 17);
+  else
 #ifdef PCR_DIAG
   if (G == 4 && NB == 3) PCR_LAUNCH_STREAM(4, 3, 2, 16, 4, 17);
   else if (G == 4) PCR_LAUNCH_STREAM(4, 2, 2, 16, 4, 17);

@@ -65,6 +65,7 @@ class SphExtractor:
         self._runner, self._runner_cap = None, 0
         self._static_in = None
         self._set1 = None
+        self._ppf1 = None
 
     # ---------------------------------------------------------------- stages
     # Buffers a later stage of the same step reads (the two workspaces and the
@@ -78,6 +79,15 @@ class SphExtractor:
             self._set1 = (e(self.knn_ws), e(self.ws), e(self.dinds), e(self.dwgts),
                           e(self.knn_idx))
         return self._set1
+
+    def _ppf(self, slot):
+        """The local PPF output of index set `slot` (set 1's is made on first
+        use: only the train-step pipeline alternates PPF outputs)."""
+        if slot == 0:
+            return self.local_ppf
+        if self._ppf1 is None:
+            self._ppf1 = torch.empty_like(self.local_ppf)
+        return self._ppf1
 
     def neighbor_stage(self, xyz, normals, stream):
         """Sort + select + PPF in one call (the eager, unsplit path)."""
@@ -100,10 +110,11 @@ class SphExtractor:
     def knn_select(self, xyz, normals, stream, slot=0, sorted_ok=True, ppf=True):
         """Selection (+ local PPF unless ppf=False) into index set `slot`."""
         kws, idx = self._set(slot)[0], self._set(slot)[4]
+        ppf_out = self._ppf(slot)
         if not sorted_ok:
             _lib.check(_lib.load().pcr_knn_local_ppf(
                 _ptr(xyz), _ptr(normals), self.b, self.n, self.k, int(self.relative),
-                _ptr(idx), _ptr(self.knn_dist), _ptr(self.local_ppf), _ptr(kws),
+                _ptr(idx), _ptr(self.knn_dist), _ptr(ppf_out), _ptr(kws),
                 kws.numel(), stream), "knn_local_ppf")
             return
         lib = _lib.load()
@@ -112,17 +123,17 @@ class SphExtractor:
             # knn_idx and the PPF (pcr_knn_select_ppf)
             _lib.check(lib.pcr_knn_select_ppf(
                 _ptr(xyz), _ptr(normals), self.b, self.n, self.k, int(self.relative), _ptr(idx),
-                _ptr(self.local_ppf), _ptr(kws), kws.numel(), stream), "knn_select_ppf")
+                _ptr(ppf_out), _ptr(kws), kws.numel(), stream), "knn_select_ppf")
             return
         _lib.check(lib.pcr_knn_local_ppf_prepared(
             _ptr(xyz), _ptr(normals), self.b, self.n, self.k, int(self.relative),
             _ptr(idx), _ptr(self.knn_dist), None if self.split_ppf else
-            _ptr(self.local_ppf), _ptr(kws), kws.numel(), stream), "knn_local_ppf_prepared")
+            _ptr(ppf_out), _ptr(kws), kws.numel(), stream), "knn_local_ppf_prepared")
         if self.split_ppf and ppf:
             # PPF as its own launch: one thread per (slot, point), coalesced
             _lib.check(lib.pcr_local_ppf_forward(
                 _ptr(xyz), _ptr(normals), _ptr(xyz), _ptr(normals), _ptr(idx), self.b,
-                self.n, self.n, self.k, 1, int(self.relative), _ptr(self.local_ppf), stream),
+                self.n, self.n, self.k, 1, int(self.relative), _ptr(ppf_out), stream),
                 "local_ppf_forward")
 
     def voxel_stage(self, xyz, features, stream, desc=None):
@@ -256,10 +267,76 @@ class SphExtractor:
         self._join(cur)
         return self.outputs()
 
+    # ------------------------------------------------- train-step pipeline
+    def enqueue_neighbors(self, xyz, normals, slot, after=None):
+        """Self-KNN (Morton sort + selection) + local PPF of one batch on
+        s_nbr into index set `slot` (its knn_idx / local_ppf).  `after`: an
+        event recorded once the set's previous consumer is done with it.
+        Returns the event this batch's consumer waits on."""
+        if after is not None:
+            self.s_nbr.wait_event(after)
+        sorted_ok = self.knn_sort(xyz, self.s_nbr.cuda_stream, slot)
+        self.knn_select(xyz, normals, self.s_nbr.cuda_stream, slot, sorted_ok)
+        ev = torch.cuda.Event()
+        ev.record(self.s_nbr)
+        return ev
+
+    def enqueue_voxels(self, xyz, features, stream, slot=0, desc=None):
+        """The voxel side of one batch on `stream`: normalisation + voxel
+        index + devox corners (prep), the dense grid + cnt, then devox +
+        descriptor (from the grid's 80 corner voxels per channel, or from
+        the re-formed means past 4096 points).  Clouds of <= 2048 points on
+        grids the streaming kernel takes (r^3 a multiple of 2048, <= 32^3)
+        use the split stage: voxel means + devox + descriptor in one launch,
+        then the dense grid streamed from the compact means (c3: 0.60 +
+        0.16 ms -> see DESIGN.md 4)."""
+        self.voxel_prep(xyz, stream, slot)
+        r3 = self.r ** 3
+        if self.n <= 2048 and r3 % 2048 == 0 and r3 <= 32768:
+            self.voxel_means_devox(features, stream, desc, slot)
+            self.voxel_stream(stream, slot)
+            return
+        self.voxel_grid(features, stream, slot)
+        if self.n <= 4096:
+            self.grid_devox(stream, desc, slot)
+        else:
+            self.voxel_devox(features, stream, desc, slot)
+
+    def pipelined_steps(self, steps, batch, consume):
+        """`steps` train steps whose neighbour side runs one batch ahead.
+
+        A batch's self-KNN + local PPF depend on its coordinates and normals
+        only (pvcnn_classify.py:252-269 computes them from the input, before
+        any weight), so batch s+1's neighbours run on s_nbr while batch s's
+        backward runs on the caller's stream: the VALU-bound selection
+        overlaps the HBM-bound voxel passes and backwards.  Per step s, on
+        the caller's stream: the voxel side of batch s, a wait for batch s's
+        neighbours (the head of the network needs them), then
+        consume(s, outputs) -- the rest of the step (the bench: the devox and
+        voxelize backwards).  Index sets alternate; batch s+2's neighbours
+        wait until step s's consume is done with set s % 2.  batch(s)
+        returns (xyz, normals, features) of step s; nothing is skipped:
+        every step's neighbours, voxels and consume run once."""
+        cur = torch.cuda.current_stream(self.device)
+        self.s_nbr.wait_stream(cur)
+        done = [None, None]
+        for s in range(steps):
+            xyz, normals, features = batch(s)
+            self._check_inputs(xyz, normals, features)
+            q = s & 1
+            e_nbr = self.enqueue_neighbors(xyz, normals, q, after=done[q])
+            self.enqueue_voxels(xyz, features, cur.cuda_stream, q)
+            cur.wait_event(e_nbr)
+            consume(s, self.outputs(slot=q, idx_slot=q))
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            done[q] = ev
+        cur.wait_stream(self.s_nbr)
+
     def outputs(self, slot=0, idx_slot=0):
         _, _, dinds, dwgts, _ = self._set(slot)
         return {
-            "knn_idx": self._set(idx_slot)[4], "local_ppf": self.local_ppf,
+            "knn_idx": self._set(idx_slot)[4], "local_ppf": self._ppf(idx_slot),
             "norm_coords": self.norm_coords,
             "ind": self.ind, "cnt": self.cnt, "grid": self.grid, "devox": self.devox,
             "dinds": dinds, "dwgts": dwgts, "desc": self.desc,

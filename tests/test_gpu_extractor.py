@@ -222,3 +222,36 @@ def test_extractor_ind_vs_reference_fp32_normalisation(dev, seed):
     print("c2 seed %d: %d of %d points in a different voxel than under the reference's "
           "torch-fp32 normalisation, all on bin edges" % (seed, total, b * n))
     assert total <= b * n // 1000
+
+
+@pytest.mark.parametrize("b,n,c,k,r", [(4, 1024, 16, 32, 16), (2, 2048, 32, 32, 32),
+                                       (3, 1500, 7, 16, 16)])
+def test_extractor_pipelined_steps(dev, b, n, c, k, r):
+    """SphExtractor.pipelined_steps (bench.py c3: each batch's KNN + local
+    PPF on s_nbr one batch ahead of the caller's voxel side and backwards):
+    every step sees exactly its own batch's outputs, equal to the oracle,
+    and the consume callback's devox backward equals the serial one."""
+    from pcr_amd import ops
+    from pcr_amd.extractor import SphExtractor
+    batches = [gaussian_clouds(b, n, seed=40 + s, c=c) for s in range(4)]
+    tb = [tuple(T(a, dev) for a in bt) for bt in batches]
+    gy = torch.randn((b, c, n), generator=torch.Generator().manual_seed(5)).to(dev)
+    ex = SphExtractor(b, n, c, k, r, device=dev)
+    poison(ex)
+    got = []
+
+    def consume(s, out):
+        gg = ops.spherical_trilinear_devoxelize_backward(gy, out["dinds"], out["dwgts"], r)
+        got.append(({kk: v.clone() for kk, v in out.items()}, gg))
+
+    ex.pipelined_steps(4, lambda s: tb[s], consume)
+    torch.cuda.synchronize()
+    assert len(got) == 4
+    for s, (out, gg) in enumerate(got):
+        exp = expected_step(*batches[s], k, r)
+        for key in ("knn_idx", "ind", "cnt", "dinds", "grid", "devox", "desc"):
+            assert np.array_equal(N(out[key]), exp[key]), (s, key)
+        assert np.array_equal(N(out["local_ppf"]), exp["local_ppf"], equal_nan=True), s
+        ref = ops.spherical_trilinear_devoxelize_backward(gy, T(exp["dinds"], dev),
+                                                          T(exp["dwgts"], dev), r)
+        assert torch.equal(gg, ref), s
