@@ -61,6 +61,7 @@ class SphExtractor:
         self.s_nbr = torch.cuda.Stream(device=dev)
         self.s_vox = torch.cuda.Stream(device=dev)
         self.s_dev = torch.cuda.Stream(device=dev)
+        self.s_main = None  # pipelined_steps' high-priority step stream
         self.graph = None
         self._runner, self._runner_cap = None, 0
         self._static_in = None
@@ -302,7 +303,7 @@ class SphExtractor:
         else:
             self.voxel_devox(features, stream, desc, slot)
 
-    def pipelined_steps(self, steps, batch, consume):
+    def pipelined_steps(self, steps, batch, consume, priority=True):
         """`steps` train steps whose neighbour side runs one batch ahead.
 
         A batch's self-KNN + local PPF depend on its coordinates and normals
@@ -316,21 +317,33 @@ class SphExtractor:
         voxelize backwards).  Index sets alternate; batch s+2's neighbours
         wait until step s's consume is done with set s % 2.  batch(s)
         returns (xyz, normals, features) of step s; nothing is skipped:
-        every step's neighbours, voxels and consume run once."""
+        every step's neighbours, voxels and consume run once.
+
+        The step chain (voxel side + consume) is the critical one, so it runs
+        on a high-priority stream forked from the caller's (its workgroups
+        are dispatched ahead of the neighbour side's; c3 2.02 -> 1.97 ms),
+        with consume() called under that stream; both are joined back into
+        the caller's stream at the end."""
         cur = torch.cuda.current_stream(self.device)
+        if self.s_main is None:
+            self.s_main = torch.cuda.Stream(device=self.device, priority=-1)
+        main = self.s_main if priority else cur
+        main.wait_stream(cur)
         self.s_nbr.wait_stream(cur)
         done = [None, None]
-        for s in range(steps):
-            xyz, normals, features = batch(s)
-            self._check_inputs(xyz, normals, features)
-            q = s & 1
-            e_nbr = self.enqueue_neighbors(xyz, normals, q, after=done[q])
-            self.enqueue_voxels(xyz, features, cur.cuda_stream, q)
-            cur.wait_event(e_nbr)
-            consume(s, self.outputs(slot=q, idx_slot=q))
-            ev = torch.cuda.Event()
-            ev.record(cur)
-            done[q] = ev
+        with torch.cuda.stream(main):
+            for s in range(steps):
+                xyz, normals, features = batch(s)
+                self._check_inputs(xyz, normals, features)
+                q = s & 1
+                e_nbr = self.enqueue_neighbors(xyz, normals, q, after=done[q])
+                self.enqueue_voxels(xyz, features, main.cuda_stream, q)
+                main.wait_event(e_nbr)
+                consume(s, self.outputs(slot=q, idx_slot=q))
+                ev = torch.cuda.Event()
+                ev.record(main)
+                done[q] = ev
+        cur.wait_stream(main)
         cur.wait_stream(self.s_nbr)
 
     def outputs(self, slot=0, idx_slot=0):
