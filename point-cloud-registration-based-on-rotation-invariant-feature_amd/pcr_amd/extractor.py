@@ -67,6 +67,7 @@ class SphExtractor:
         self._static_in = None
         self._set1 = None
         self._ppf1 = None
+        self._args, self._args_key = None, None
 
     # ---------------------------------------------------------------- stages
     # Buffers a later stage of the same step reads (the two workspaces and the
@@ -79,7 +80,18 @@ class SphExtractor:
             e = torch.empty_like
             self._set1 = (e(self.knn_ws), e(self.ws), e(self.dinds), e(self.dwgts),
                           e(self.knn_idx))
+            self._order_new_buffers()
         return self._set1
+
+    def _order_new_buffers(self):
+        """Buffers made lazily come from the current stream's pool, possibly
+        a block freed with kernels still pending on that stream; the
+        extractor's streams, which write them, wait for the current stream
+        first."""
+        cur = torch.cuda.current_stream(self.device)
+        for st in (self.s_pre, self.s_nbr, self.s_vox, self.s_dev, self.s_main):
+            if st is not None:
+                st.wait_stream(cur)
 
     def _ppf(self, slot):
         """The local PPF output of index set `slot` (set 1's is made on first
@@ -88,6 +100,7 @@ class SphExtractor:
             return self.local_ppf
         if self._ppf1 is None:
             self._ppf1 = torch.empty_like(self.local_ppf)
+            self._order_new_buffers()
         return self._ppf1
 
     def neighbor_stage(self, xyz, normals, stream):
@@ -325,6 +338,14 @@ class SphExtractor:
         with consume() called under that stream; both are joined back into
         the caller's stream at the end."""
         cur = torch.cuda.current_stream(self.device)
+        # set 1's buffers are made here, on the caller's stream, before both
+        # streams fork from it.  Made lazily inside the loop they came from
+        # `main`'s pool -- possibly a block the previous step's consume had
+        # just freed with its kernels still pending on `main` -- and s_nbr
+        # wrote them with no order against those kernels (an illegal-address
+        # fault on the GPU when the KNN workspace landed there).
+        self._set(1)
+        self._ppf(1)
         if self.s_main is None:
             self.s_main = torch.cuda.Stream(device=self.device, priority=-1)
         main = self.s_main if priority else cur
@@ -398,24 +419,9 @@ class SphExtractor:
                                                      ctypes.byref(cnt)), "runner_grid_times")
         return list(ms[:cnt.value])
 
-    def run_native(self, xyz, normals, features, steps, desc_steps=None, schedule=1,
-                   timed=False, match=None):
-        """`steps` pipelined steps enqueued by the library's native runner
-        (pcr_extractor_run): schedule 1 = three streams (prep + means / devox
-        on s_pre, the grid stream on s_vox, sort + select + PPF on s_nbr,
-        voxel buffer sets alternating), 2 = as 1 with the Morton sort on
-        s_pre, 0 = two streams with the fused grid kernel.  One ctypes call
-        for all steps.  timed: bracket the grid-stream kernel of every step
-        (True) or of the last N steps (an int N) with timing events (read
-        back with grid_kernel_times()).  match: a
-        registration.PairMatch whose buffers receive, every step, the
-        mutual-NN matching of clouds [0, B/2) against [B/2, B)."""
-        self._check_inputs(xyz, normals, features)
-        # timed: True = every step, an int N = the last N steps
-        ntimed = min(steps, (steps if timed is True else int(timed)) if timed else 0)
-        runner = self._get_runner(ntimed)
-        if self._runner_cap:
-            _lib.check(_lib.load().pcr_runner_set_timed(runner, ntimed), "runner_set_timed")
+    def _make_args(self, xyz, normals, features, match):
+        """pcr_extractor_args (include/pcr_amd.h) over these inputs and the
+        extractor's buffers."""
         s1 = self._set(1)
         a = _lib.ExtractorArgs()
         a.b, a.n, a.c, a.k, a.r, a.relative = self.b, self.n, self.c, self.k, self.r, \
@@ -441,6 +447,33 @@ class SphExtractor:
             a.idx1, a.idx2, a.match_count = _ptr(match.idx1), _ptr(match.idx2), \
                 _ptr(match.count)
             a.match_ws, a.match_ws_bytes = _ptr(match.ws), match.ws.numel()
+        return a
+
+    def run_native(self, xyz, normals, features, steps, desc_steps=None, schedule=1,
+                   timed=False, match=None):
+        """`steps` pipelined steps enqueued by the library's native runner
+        (pcr_extractor_run): schedule 1 = three streams (prep + means / devox
+        on s_pre, the grid stream on s_vox, sort + select + PPF on s_nbr,
+        voxel buffer sets alternating), 2 = as 1 with the Morton sort on
+        s_pre, 0 = two streams with the fused grid kernel.  One ctypes call
+        for all steps.  timed: bracket the grid-stream kernel of every step
+        (True) or of the last N steps (an int N) with timing events (read
+        back with grid_kernel_times()).  match: a
+        registration.PairMatch whose buffers receive, every step, the
+        mutual-NN matching of clouds [0, B/2) against [B/2, B)."""
+        self._check_inputs(xyz, normals, features)
+        # timed: True = every step, an int N = the last N steps
+        ntimed = min(steps, (steps if timed is True else int(timed)) if timed else 0)
+        runner = self._get_runner(ntimed)
+        if self._runner_cap:
+            _lib.check(_lib.load().pcr_runner_set_timed(runner, ntimed), "runner_set_timed")
+        # the argument block is built once per (inputs, match) and reused:
+        # every other pointer is an extractor buffer, fixed for its life
+        key = (xyz.data_ptr(), normals.data_ptr(), features.data_ptr(), match)
+        if self._args_key != key:
+            self._args = self._make_args(xyz, normals, features, match)
+            self._args_key = key
+        a = self._args
         if desc_steps is not None and tuple(desc_steps.shape) != (steps, self.b, self.c):
             raise RuntimeError("desc_steps must be [steps, B, C]")
         cur = torch.cuda.current_stream(self.device)
