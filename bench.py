@@ -91,9 +91,6 @@ def parse(argv=None):
                          "batch ahead, overlapping the previous step's backwards "
                          "(SphExtractor.pipelined_steps); serial = forward (joined), then "
                          "the backwards")
-    ap.add_argument("--c3-no-priority", action="store_true",
-                    help="diagnostic: c3 pipelined step chain on the caller's stream instead "
-                         "of the extractor's high-priority stream")
     ap.add_argument("--steps-per-launch", type=int, default=40,
                     help="most pipelined steps per native runner call (extract / pairs); "
                          "--steps and --warmup are split into calls of at most this many")
@@ -452,8 +449,7 @@ class C3Workload:
             res = self._backward(out, self.ev[s] if timed else None)
             if keep is not None:
                 keep.append(({kk: v.clone() for kk, v in out.items()}, res))
-        self.ex.pipelined_steps(steps, lambda s: self.inputs, consume,
-                                priority=not self.args.c3_no_priority)
+        self.ex.pipelined_steps(steps, lambda s: self.inputs, consume)
 
     def verify(self):
         """Three pipelined steps vs the serial forward + backwards: every

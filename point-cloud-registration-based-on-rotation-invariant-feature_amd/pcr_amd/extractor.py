@@ -61,7 +61,6 @@ class SphExtractor:
         self.s_nbr = torch.cuda.Stream(device=dev)
         self.s_vox = torch.cuda.Stream(device=dev)
         self.s_dev = torch.cuda.Stream(device=dev)
-        self.s_main = None  # pipelined_steps' high-priority step stream
         self.graph = None
         self._runner, self._runner_cap = None, 0
         self._static_in = None
@@ -89,9 +88,8 @@ class SphExtractor:
         extractor's streams, which write them, wait for the current stream
         first."""
         cur = torch.cuda.current_stream(self.device)
-        for st in (self.s_pre, self.s_nbr, self.s_vox, self.s_dev, self.s_main):
-            if st is not None:
-                st.wait_stream(cur)
+        for st in (self.s_pre, self.s_nbr, self.s_vox, self.s_dev):
+            st.wait_stream(cur)
 
     def _ppf(self, slot):
         """The local PPF output of index set `slot` (set 1's is made on first
@@ -316,7 +314,7 @@ class SphExtractor:
         else:
             self.voxel_devox(features, stream, desc, slot)
 
-    def pipelined_steps(self, steps, batch, consume, priority=True):
+    def pipelined_steps(self, steps, batch, consume):
         """`steps` train steps whose neighbour side runs one batch ahead.
 
         A batch's self-KNN + local PPF depend on its coordinates and normals
@@ -330,41 +328,29 @@ class SphExtractor:
         voxelize backwards).  Index sets alternate; batch s+2's neighbours
         wait until step s's consume is done with set s % 2.  batch(s)
         returns (xyz, normals, features) of step s; nothing is skipped:
-        every step's neighbours, voxels and consume run once.
-
-        The step chain (voxel side + consume) is the critical one, so it runs
-        on a high-priority stream forked from the caller's (its workgroups
-        are dispatched ahead of the neighbour side's; c3 2.02 -> 1.97 ms),
-        with consume() called under that stream; both are joined back into
-        the caller's stream at the end."""
+        every step's neighbours, voxels and consume run once."""
         cur = torch.cuda.current_stream(self.device)
-        # set 1's buffers are made here, on the caller's stream, before both
-        # streams fork from it.  Made lazily inside the loop they came from
-        # `main`'s pool -- possibly a block the previous step's consume had
-        # just freed with its kernels still pending on `main` -- and s_nbr
-        # wrote them with no order against those kernels (an illegal-address
-        # fault on the GPU when the KNN workspace landed there).
+        # set 1's buffers are made here, before s_nbr forks from the caller's
+        # stream.  Made lazily inside the loop they could reuse a block the
+        # previous step's consume had just freed with its kernels still
+        # pending on the caller's stream, and s_nbr wrote them with no order
+        # against those kernels (an illegal-address fault on the GPU when the
+        # KNN workspace landed there).
         self._set(1)
         self._ppf(1)
-        if self.s_main is None:
-            self.s_main = torch.cuda.Stream(device=self.device, priority=-1)
-        main = self.s_main if priority else cur
-        main.wait_stream(cur)
         self.s_nbr.wait_stream(cur)
         done = [None, None]
-        with torch.cuda.stream(main):
-            for s in range(steps):
-                xyz, normals, features = batch(s)
-                self._check_inputs(xyz, normals, features)
-                q = s & 1
-                e_nbr = self.enqueue_neighbors(xyz, normals, q, after=done[q])
-                self.enqueue_voxels(xyz, features, main.cuda_stream, q)
-                main.wait_event(e_nbr)
-                consume(s, self.outputs(slot=q, idx_slot=q))
-                ev = torch.cuda.Event()
-                ev.record(main)
-                done[q] = ev
-        cur.wait_stream(main)
+        for s in range(steps):
+            xyz, normals, features = batch(s)
+            self._check_inputs(xyz, normals, features)
+            q = s & 1
+            e_nbr = self.enqueue_neighbors(xyz, normals, q, after=done[q])
+            self.enqueue_voxels(xyz, features, cur.cuda_stream, q)
+            cur.wait_event(e_nbr)
+            consume(s, self.outputs(slot=q, idx_slot=q))
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            done[q] = ev
         cur.wait_stream(self.s_nbr)
 
     def outputs(self, slot=0, idx_slot=0):
