@@ -195,6 +195,11 @@ __global__ __launch_bounds__(NT) void knn_sort_kernel(const float* __restrict__ 
   // order (keys are compared lexicographically), only its speed does.
   int* hist = (int*)keys;     // [4096]
   int* order = hist + 4096;   // [n]
+  // the coordinates in sorted order, written by the scatter from the
+  // registers that already hold them: the block pass reads them from LDS
+  // instead of gathering P[order[p]] from global memory (a dependent round
+  // trip, microseconds under the grid stream's writes)
+  float* sxyz = (float*)(order + n);  // [3][n]
   __shared__ int scan_b[NT / kWave + 1];
   for (int c = tid; c < 4096; c += NT) hist[c] = 0;
   __syncthreads();
@@ -233,7 +238,13 @@ __global__ __launch_bounds__(NT) void knn_sort_kernel(const float* __restrict__ 
   __syncthreads();
 #pragma unroll
   for (int e = 0; e < kMaxE; e++)
-    if (cell[e] >= 0) order[hist[cell[e]] + slot[e]] = e * NT + tid;
+    if (cell[e] >= 0) {
+      const int pos = hist[cell[e]] + slot[e];
+      order[pos] = e * NT + tid;
+      sxyz[pos] = px[e];
+      sxyz[n + pos] = py[e];
+      sxyz[2 * n + pos] = pz[e];
+    }
   __syncthreads();
   // sorted SoA + per-block boxes (one wave per block)
   const size_t base = (size_t)b * s.npad;
@@ -244,9 +255,9 @@ __global__ __launch_bounds__(NT) void knn_sort_kernel(const float* __restrict__ 
     int j = -1;
     if (p < n) {
       j = order[p];
-      x = P[j];
-      y = P[n + j];
-      z = P[2 * n + j];
+      x = sxyz[p];
+      y = sxyz[n + p];
+      z = sxyz[2 * n + p];
       if (s.inv) s.inv[(size_t)b * n + j] = p;
     }
     s.x[base + p] = x;
@@ -1804,7 +1815,7 @@ static void launch_sort(const float* pts, int b, int n, const KnnSet& s, hipStre
   }
   // clouds of <= 1024 points: 256 threads (four points each), so the sort
   // fits on a CU beside the other stream's grid kernel
-  const size_t smem = 4096 * 4 + (size_t)n * 4;
+  const size_t smem = 4096 * 4 + (size_t)n * 16;  // hist | order | sorted x y z
   if (n <= kSmallSortN) {
     const int npad_sort = next_pow2i(n < kSmallSortThreads ? kSmallSortThreads : n);
     allow_big_lds(knn_sort_kernel<kSmallSortThreads>, smem);
