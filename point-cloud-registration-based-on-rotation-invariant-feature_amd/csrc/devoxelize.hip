@@ -594,9 +594,12 @@ __global__ __launch_bounds__(kBwdThreads) void devox_bwd_kernel(
       start++;
     }
     const int nv = (r3 - start) >> 2;
-    float4* v4 = (float4*)(row + start);
-    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int t = tid; t < nv; t += kBwdThreads) v4[t] = z;
+    // nontemporal zero stream: the dense gradient grid is written once and
+    // not read back here (c3 step 1.97 -> 1.90 ms with the PPF / emit ones)
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    f4v* w4 = (f4v*)(row + start);
+    const f4v z4 = {0.f, 0.f, 0.f, 0.f};
+    for (int t = tid; t < nv; t += kBwdThreads) __builtin_nontemporal_store(z4, &w4[t]);
     for (int t = start + nv * 4 + tid; t < r3; t += kBwdThreads) row[t] = 0.0f;
   }
   // 3. rare out-of-window corners (cube grids): global atomics after this
@@ -618,7 +621,8 @@ __global__ __launch_bounds__(kBwdThreads) void devox_bwd_kernel(
   __syncthreads();
   // 3. store the window
   for (int g = 0; g < gcount; g++)
-    for (int t = tid; t < hw; t += kBwdThreads) gx[(size_t)g * r3 + t] = acc_s[g * hw + t];
+    for (int t = tid; t < hw; t += kBwdThreads)
+      __builtin_nontemporal_store(acc_s[g * hw + t], &gx[(size_t)g * r3 + t]);
 }
 
 __global__ __launch_bounds__(256) void center_gather_kernel(const float* __restrict__ features,

@@ -1721,14 +1721,17 @@ __global__ __launch_bounds__(256) void knn_emit_kernel(KnnSet qs, int k, int nqb
       if (g + t >= ns) break;
       const int sl = s0 + g + t;
       const size_t o = ((size_t)b * k + sl) * n + qj;
-      if (idx) idx[o] = key_idx(key[g + t]);
-      if (dist) dist[o] = key_dist(key[g + t]);
+      // streamed outputs (far larger than the L2 / MALL): nontemporal stores
+      // (c5 KNN + PPF 2.20 -> 2.12 ms)
+#define PCR_EST(p, v) __builtin_nontemporal_store((v), &(p))
+      if (idx) PCR_EST(idx[o], key_idx(key[g + t]));
+      if (dist) PCR_EST(dist[o], key_dist(key[g + t]));
       if (PPF) {
         float f[4];
         pcr_local_ppf(ox, oy, oz, cnx, cny, cnz, nbr[t][0], nbr[t][1], nbr[t][2], nbr[t][3],
                       nbr[t][4], nbr[t][5], relative, f);
 #pragma unroll
-        for (int ch = 0; ch < 4; ch++) ppf[(((size_t)b * 4 + ch) * k + sl) * n + qj] = f[ch];
+        for (int ch = 0; ch < 4; ch++) PCR_EST(ppf[(((size_t)b * 4 + ch) * k + sl) * n + qj], f[ch]);
       }
     }
   }

@@ -337,8 +337,10 @@ __global__ __launch_bounds__(NT) void local_ppf_self_kernel(const float* __restr
       float o[4];
       pcr_local_ppf(cx, cy, cz, cnx, cny, cnz, cl_s[si], cl_s[n + si], cl_s[2 * n + si],
                     cl_s[3 * n + si], cl_s[4 * n + si], cl_s[5 * n + si], relative, o);
+      // nontemporal: the PPF rows are streamed out (c3 KNN + PPF 0.91 -> 0.85 ms)
 #pragma unroll
-      for (int ch = 0; ch < 4; ch++) O[((size_t)ch * k + q) * n + j] = o[ch];
+      for (int ch = 0; ch < 4; ch++)
+        __builtin_nontemporal_store(o[ch], &O[((size_t)ch * k + q) * n + j]);
     }
   }
 }
