@@ -1564,12 +1564,8 @@ __global__ __launch_bounds__(256) void vox_gather_big_t_kernel(
     }
 #pragma unroll
     for (int q = 0; q < CH; q++)
-      if (c0 + q < c)
-#ifdef PCR_BIG_NT
-        __builtin_nontemporal_store(acc[q], &O[(size_t)(c0 + q) * r3]);
-#else
-        O[(size_t)(c0 + q) * r3] = acc[q];
-#endif
+      // nontemporal: the 537 MB grid at c5 is written once (c5 step -2%)
+      if (c0 + q < c) __builtin_nontemporal_store(acc[q], &O[(size_t)(c0 + q) * r3]);
   }
 }
 
@@ -1946,13 +1942,7 @@ extern "C" pcr_status pcr_extractor_voxel_stream(int b, int c, int n, int r, int
                        dim3((NSV + 1) * 64), smem, as_stream(stream), c, n, r3, ws, grid, cnt, \
                        ngrp, wpc, per, dbg);                                                  \
   } while (0)
-#ifndef PCR_WIDE_AUX
-#define PCR_WIDE_AUX 16
-#endif
-#ifndef PCR_NARROW_AUX
-#define PCR_NARROW_AUX 16
-#endif
-  if (wide) PCR_LAUNCH_STREAM(4, kStreamNB, 2, PCR_WIDE_AUX, kStreamG, 17);
+  if (wide) PCR_LAUNCH_STREAM(4, kStreamNB, 2, 16, kStreamG, 17);
   else
 #ifdef PCR_DIAG
   if (G == 4 && NB == 3) PCR_LAUNCH_STREAM(4, 3, 2, 16, 4, 17);
@@ -1964,7 +1954,7 @@ extern "C" pcr_status pcr_extractor_voxel_stream(int b, int c, int n, int r, int
   else if (nsk == 8) PCR_LAUNCH_STREAM(8, 3, 2, 16, 2, 9);
   else
 #endif
-    PCR_LAUNCH_STREAM(4, kStreamNB, 2, PCR_NARROW_AUX, kStreamG, kStreamNG);
+    PCR_LAUNCH_STREAM(4, kStreamNB, 2, 16, kStreamG, kStreamNG);
 #undef PCR_LAUNCH_STREAM
   return launch_status(name);
 }
