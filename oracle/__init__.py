@@ -49,6 +49,7 @@ _SIGS = {
     "orc_atanf_v": [_i, _f32p, _f32p],
     "orc_acos_d_v": [_i, _f64p, _f64p],
     "orc_sph_index_v": [_i, _f32p, _i, _i, _i32p],
+    "orc_sph_index_ulp": [_i, _f32p, _i, _i, _i, _i32p],
     "orc_mutual_nn": [_i, _i, _i, _i, _f32p, _f32p, _i32p, _i32p, _i32p, _i32p, _i32p],
     "orc_lrf": [_i, _i, _f32p, _f32p, _f32p, _i32p, _i32p],
     "orc_gather": [_i, _i, _i, _i, _f32p, _i32p, _f32p],
@@ -287,6 +288,17 @@ def sph_index(xyz, r, use_fma=True):
     n = xyz.shape[1]
     ind = np.empty(n, np.int32)
     lib().orc_sph_index_v(n, xyz, r, int(bool(use_fma)), ind)
+    return ind
+
+
+def sph_index_ulp(xyz, r, dacos, datan):
+    """sph_index with the float acos / atan results moved dacos / datan fp32
+    ulps from the correctly rounded values (CUDA's float acosf / atanf are
+    accurate to <= 2 ulp; spherical_vox.cu:46,54)."""
+    xyz = _f32(xyz)
+    n = xyz.shape[1]
+    ind = np.empty(n, np.int32)
+    lib().orc_sph_index_ulp(n, xyz, r, int(dacos), int(datan), ind)
     return ind
 
 

@@ -21,6 +21,7 @@
  * bit for bit, the scatter backwards are compared within a tolerance.
  * Compile with -ffp-contract=off (see include/pcr_math.h).
  */
+#include <math.h>
 #include <stdlib.h>
 #include <string.h>
 #include <stdint.h>
@@ -497,6 +498,53 @@ void orc_acos_d_v(int n, const double *x, double *y) {
 void orc_sph_index_v(int n, const float *xyz, int r, int use_fma, int *ind) {
   int i;
   for (i = 0; i < n; i++) ind[i] = pcr_sph_index_v(xyz[i], xyz[i + n], xyz[i + 2 * n], r, use_fma);
+}
+/* The spherical voxel index of pcr_sph_index_v (use_fma = 1) with the
+ * float acos / atan results moved `dacos` / `datan` fp32 ulps (nextafterf
+ * steps) from the correctly rounded values the oracle and the kernels use:
+ * CUDA's float acosf / atanf, which the reference calls
+ * (spherical_vox.cu:46,54), are accurate to <= 2 ulp, so an sm_61 result may
+ * sit there.  Line for line pcr_sph_coords + pcr_sph_index_v otherwise;
+ * (0, 0) reproduces orc_sph_index_v (tests/test_edges_cpu.py checks it). */
+static float step_ulps(float v, int d) {
+  for (; d > 0; d--) v = nextafterf(v, __builtin_inff());
+  for (; d < 0; d++) v = nextafterf(v, -__builtin_inff());
+  return v;
+}
+void orc_sph_index_ulp(int n, const float *xyz, int r, int dacos, int datan, int *ind) {
+  int i;
+  for (i = 0; i < n; i++) {
+    float x = xyz[i], y = xyz[i + n], z = xyz[i + 2 * n];
+    float g2 = pcr_sumsq3f(x, y, z);
+    float gama = __builtin_sqrtf(g2);
+    float beta, alpha;
+    int gx, gy, gz;
+    if ((gama == 0.0f) || (gama >= 1.0f) || ((z / gama) > 1.0f) || ((z / gama) < -1.0f)) {
+      ind[i] = -1;
+      continue;
+    }
+    beta = step_ulps(pcr_acosf(z / gama), dacos);
+    if ((double)beta >= PCR_PI) {
+      ind[i] = -1;
+      continue;
+    }
+    if (x == 0.0f && y != 0.0f)
+      alpha = (float)((double)(y / __builtin_fabsf(y)) * PCR_PI * 0.5);
+    else if (x == 0.0f && y == 0.0f)
+      alpha = 0.0f;
+    else
+      alpha = (float)((double)step_ulps(pcr_atanf(y / x), datan) +
+                      PCR_PI * (double)(1.0f - (x / __builtin_fabsf(x))) / 2.0);
+    alpha = (float)((double)alpha + PCR_PI / (double)r);
+    if (alpha < 0.0f) alpha = (float)((double)alpha + 2.0 * PCR_PI);
+    gx = pcr_f2i(__builtin_floorf(gama * (float)r));
+    gy = pcr_d2i(__builtin_floor((double)((alpha * (float)r) / 2.0f) / PCR_PI));
+    gz = pcr_d2i(__builtin_floor((double)(beta * (float)r) / PCR_PI));
+    if (gx >= r) gx = r - 1;
+    if (gy >= r) gy = r - 1;
+    if (gz >= r) gz = r - 1;
+    ind[i] = gx * r * r + gy * r + gz;
+  }
 }
 /* feature-space mutual nearest neighbours of p registration pairs
  * (datasets/deepgmr_mn40.py:232-244): f1 [p][n1][c], f2 [p][n2][c];

@@ -153,10 +153,15 @@ __device__ inline void lds_barrier() {
 // (s_waitcnt lgkmcnt(0); s_barrier; vmcnt and expcnt at their maxima, gfx9
 // encoding): outstanding global loads, stores and LDS-DMA transfers stay in
 // flight.  Only for data exchanged through LDS; an LDS-DMA target must be
-// waited for with vmcnt by the issuing wave before the barrier.
+// waited for with vmcnt by the issuing wave before the barrier.  The two
+// builtins are IntrNoMem in LLVM, so on their own they do not stop IR passes
+// from moving or forwarding LDS accesses across them: the signal fences are
+// compiler-only barriers (they emit no instruction and no vmcnt wait).
 __device__ inline void lds_only_barrier() {
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
   __builtin_amdgcn_s_waitcnt(0xC07F);
   __builtin_amdgcn_s_barrier();
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
 
 // Inclusive block-wide scan of one int per thread (blockDim.x threads,

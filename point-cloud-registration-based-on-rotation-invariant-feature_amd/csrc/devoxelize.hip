@@ -401,7 +401,7 @@ constexpr int kBwdMaxG = 4;
 
 __global__ __launch_bounds__(kBwdThreads) void devox_bwd_kernel(
     const float* __restrict__ grad_y, const int* __restrict__ inds, const float* __restrict__ wgts,
-    int c, int n, int r, int G, int hw, int skip_neg, float* __restrict__ grad_x, int dbg,
+    int c, int n, int r, int G, int hw, int skip_neg, float* __restrict__ grad_x,
     const int* __restrict__ order) {
   extern __shared__ __align__(16) float acc_s[];  // [G][hw]
   // spherical grads: each wave's segment sums for the 80 corner voxels
@@ -428,7 +428,7 @@ __global__ __launch_bounds__(kBwdThreads) void devox_bwd_kernel(
   float* gx = grad_x + ((size_t)b * c + c0) * r3;
   // 1. accumulate the hot window in LDS; note whether any corner falls outside
   int outside = 0;
-  if (skip_neg && !(dbg & 1)) {
+  if (skip_neg) {
     // Spherical grads: the 64 points of a wave mostly share a handful of
     // corner sets (the integer-division quirk pins gamma_lo = 0, so every
     // corner set is one of ~28 (alpha_lo, beta_lo) cells plus three "hi"
@@ -566,7 +566,7 @@ __global__ __launch_bounds__(kBwdThreads) void devox_bwd_kernel(
       }
     }
   }
-  if (!skip_neg && !(dbg & 1))
+  if (!skip_neg)
   for (int i = tid; i < n; i += kBwdThreads) {
     if (skip_neg && I[i] == -1) continue;
     int ci[8];
@@ -1108,7 +1108,7 @@ static pcr_status devox_backward(const float* grad_y, const int* inds, const flo
   allow_big_lds(devox_bwd_kernel, (size_t)G * hw * 4);
   hipLaunchKernelGGL(devox_bwd_kernel, dim3(ceil_div(c, G), b), dim3(kBwdThreads),
                      (size_t)G * hw * 4, as_stream(stream), grad_y, inds, wgts, c, n, r, G, hw,
-                     skip_neg, grad_x, PCR_KNOB("PCR_DEVOX_BWD_DBG", 0), order);
+                     skip_neg, grad_x, order);
   return launch_status("devoxelize_backward");
 }
 

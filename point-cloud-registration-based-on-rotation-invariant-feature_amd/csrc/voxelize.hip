@@ -897,8 +897,7 @@ template <int NS, int NB, int U, int AUX, int G = kStreamG, int NG = kStreamNG>
 __global__ __launch_bounds__((NS + 1) * 64) void vox_stream_kernel(int c, int n, int r3, VoxWs ws,
                                                                   float* __restrict__ out,
                                                                   int* __restrict__ cnt_out,
-                                                                  int ngrp, int wpc, int per,
-                                                                  int dbg) {
+                                                                  int ngrp, int wpc, int per) {
   constexpr int D = NB - 1;     // prefetch distance in items
   constexpr int NTS = NS * 64;  // streamer threads
   constexpr int BUFB = NG * 1024;
@@ -923,7 +922,6 @@ __global__ __launch_bounds__((NS + 1) * 64) void vox_stream_kernel(int c, int n,
     // item j (channel pair) of this cloud into means buffer `buf`: NG whole
     // 1 KB pieces (the two rows are adjacent; the tail past them is unused)
     auto issue = [&](int j, int buf) {
-      if (dbg & 2) return;
       const char* src = (const char*)(ws.means + ((size_t)b * c + (size_t)j * G) * ms);
       char* dst = (char*)smem_raw + buf * BUFB;
 #pragma unroll
@@ -936,7 +934,7 @@ __global__ __launch_bounds__((NS + 1) * 64) void vox_stream_kernel(int c, int n,
 #pragma unroll
     for (int q = 0; q < D; q++)
       if (q < nit) issue(j0 + q, q);
-    if (!(dbg & 2)) {
+    {
       // bitmap and segment counts by LDS-DMA too (4-byte pieces: 256 B per
       // wave instruction), so the loader holds no staging registers
       const char* gbm = (const char*)(ws.bitmap + (size_t)b * W);
@@ -988,18 +986,6 @@ __global__ __launch_bounds__((NS + 1) * 64) void vox_stream_kernel(int c, int n,
   // counts, slot n = 0 for empty cells) is issued before any is waited on;
   // one 16-byte store per channel (+ cnt) and group
   auto stream_u = [&](int base0, float* ob, int g_lo, int gcount, const float* ms0, int* cb) {
-    if (dbg & 1) {  // diagnostic: zeros only, no LDS reads
-      const float4 z = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-      for (int u = 0; u < U; u++) {
-        const int base = base0 + u * NTS * 4;
-        if (base < r3)
-#pragma unroll
-          for (int g = 0; g < G; g++)
-            if (g >= g_lo && g < gcount) *(float4*)(ob + (size_t)g * r3 + base) = z;
-      }
-      return;
-    }
     unsigned word[U];
     int pw[U];
 #pragma unroll
@@ -1058,7 +1044,7 @@ __global__ __launch_bounds__((NS + 1) * 64) void vox_stream_kernel(int c, int n,
   // the sweep starts at a workgroup-dependent step of the item and wraps, so
   // the workgroups do not all hit the same HBM channels at once
   const int nstep = (r3 + NTS * 4 * U - 1) / (NTS * 4 * U);
-  const int rot = (dbg & 4) ? 0 : (int)(blockIdx.x % nstep);
+  const int rot = (int)(blockIdx.x % nstep);
   for (int it = 0; it < nit; it++) {
     const int j = j0 + it;
     const int c0 = j * G;
@@ -1066,18 +1052,9 @@ __global__ __launch_bounds__((NS + 1) * 64) void vox_stream_kernel(int c, int n,
     float* ob = out + ((size_t)b * c + c0) * r3;
     int* cb = (cnt_out && j == 0) ? cnt_out + (size_t)b * r3 : nullptr;
     const float* ms0 = mean_s + (size_t)(it % NB) * (BUFB / 4);
-    if (dbg & 8) {
-      // one row at a time: the item's two rows are one contiguous 2 r^3 sweep
-      for (int g = 0; g < gcount; g++)
-        for (int st = 0; st < nstep; st++) {
-          const int sp = st + rot < nstep ? st + rot : st + rot - nstep;
-          stream_u(sp * NTS * 4 * U + tid * 4, ob, g, g + 1, ms0, g == 0 ? cb : nullptr);
-        }
-    } else {
-      for (int st = 0; st < nstep; st++) {
-        const int sp = st + rot < nstep ? st + rot : st + rot - nstep;
-        stream_u(sp * NTS * 4 * U + tid * 4, ob, 0, gcount, ms0, cb);
-      }
+    for (int st = 0; st < nstep; st++) {
+      const int sp = st + rot < nstep ? st + rot : st + rot - nstep;
+      stream_u(sp * NTS * 4 * U + tid * 4, ob, 0, gcount, ms0, cb);
     }
     if (it < 4) PCR_STAMP(2 + it);
     lds_only_barrier();
@@ -1227,10 +1204,13 @@ __global__ __launch_bounds__(kGradSortThreads) void avg_vox_grad_sorted_kernel(
     for (int u = 0; u < PT; u++) {
       const int s2 = u * kGradSortThreads + tid;
       if (s2 < n) {
+        // iv == 0 marks a dropped point: +0 as the reference leaves it
+        // (spherical_vox.cu:153-156), not grad_y[voxel 0] * 0 (-0 / NaN)
         const float iv = sinv_s[s2];
         const int i = sidx_s[s2];
 #pragma unroll
-        for (int q = 0; q < kGradSortU; q++) out_s[q * kGradSortMaxN + i] = v[u][q] * iv;
+        for (int q = 0; q < kGradSortU; q++)
+          out_s[q * kGradSortMaxN + i] = iv != 0.0f ? v[u][q] * iv : 0.0f;
       }
     }
     lds_only_barrier();
@@ -1927,7 +1907,6 @@ extern "C" pcr_status pcr_extractor_voxel_stream(int b, int c, int n, int r, int
   if (wpc < 1) wpc = 1;
   if (wpc > ngrp) wpc = ngrp;
   const int per = ceil_div(ngrp, wpc);
-  static const int dbg = PCR_KNOB("PCR_STREAM_DBG", 0);
   PCR_REQUIRE(ws.W % 64 == 0, "%s: r^3 %% 2048 != 0 unsupported", name);
   const size_t smem = (size_t)NB * NGP * 1024 + (size_t)ws.W * 6 +
                       ((size_t)ws.ms * 2 + 255) / 256 * 256;
@@ -1940,7 +1919,7 @@ extern "C" pcr_status pcr_extractor_voxel_stream(int b, int c, int n, int r, int
     allow_big_lds(vox_stream_kernel<NSV, NBV, UV, AV, GV, NGV>, smem);                        \
     hipLaunchKernelGGL((vox_stream_kernel<NSV, NBV, UV, AV, GV, NGV>), dim3(b * wpc),         \
                        dim3((NSV + 1) * 64), smem, as_stream(stream), c, n, r3, ws, grid, cnt, \
-                       ngrp, wpc, per, dbg);                                                  \
+                       ngrp, wpc, per);                                                       \
   } while (0)
   if (wide) PCR_LAUNCH_STREAM(4, kStreamNB, 2, 16, kStreamG, 17);
   else

@@ -328,7 +328,16 @@ class SphExtractor:
         voxelize backwards).  Index sets alternate; batch s+2's neighbours
         wait until step s's consume is done with set s % 2.  batch(s)
         returns (xyz, normals, features) of step s; nothing is skipped:
-        every step's neighbours, voxels and consume run once."""
+        every step's neighbours, voxels and consume run once.
+
+        batch(s) may make its tensors on the caller's stream (an H2D copy as
+        in train.py:140, an augmentation, the LRF change_coords): batch(s+1)
+        is called after step s's voxel side is enqueued and before its
+        consume, and s_nbr waits for an event recorded on the caller's
+        stream right after it, so batch s+1's neighbours are ordered after
+        its producers but not after consume(s) -- the overlap stays.  xyz and
+        normals are record_stream'ed to s_nbr, so the caching allocator does
+        not hand their blocks out while s_nbr still reads them."""
         cur = torch.cuda.current_stream(self.device)
         # set 1's buffers are made here, before s_nbr forks from the caller's
         # stream.  Made lazily inside the loop they could reuse a block the
@@ -339,13 +348,26 @@ class SphExtractor:
         self._set(1)
         self._ppf(1)
         self.s_nbr.wait_stream(cur)
+
+        def fetch(s):
+            t = batch(s)
+            self._check_inputs(*t)
+            ev = torch.cuda.Event()
+            ev.record(cur)  # after whatever batch(s) enqueued on the caller's stream
+            return t, ev
+
         done = [None, None]
+        nxt = fetch(0) if steps > 0 else None
         for s in range(steps):
-            xyz, normals, features = batch(s)
-            self._check_inputs(xyz, normals, features)
+            (xyz, normals, features), e_in = nxt
             q = s & 1
+            self.s_nbr.wait_event(e_in)
+            xyz.record_stream(self.s_nbr)
+            normals.record_stream(self.s_nbr)
             e_nbr = self.enqueue_neighbors(xyz, normals, q, after=done[q])
             self.enqueue_voxels(xyz, features, cur.cuda_stream, q)
+            # the next batch is produced ahead of this step's consume
+            nxt = fetch(s + 1) if s + 1 < steps else None
             cur.wait_event(e_nbr)
             consume(s, self.outputs(slot=q, idx_slot=q))
             ev = torch.cuda.Event()

@@ -40,8 +40,6 @@ for step in "$@"; do
           run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 5 --warmup 5 --steps-per-launch 5 --kernel-iters 5 --no-cpu-baseline
           run pmc_json 60 python3 scripts/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc_traffic.json 32 1024 32 32 64 ;;
     large) run pytest_large 600 python -m pytest tests/test_gpu_large.py -q -m gpu -p no:cacheprovider ;;
-    knnb) run knn_bench 300 python scripts/knn_bench.py ;;
-    overlap) run overlap 300 python scripts/overlap_probe.py ;;
     c5) run c5_time 300 python scripts/c5_time.py ;;
     cube) run cube_time 300 python scripts/cube_time.py ;;
     cubebwd) run cube_bwd 300 python scripts/cube_bwd_time.py

@@ -63,3 +63,54 @@ def test_c2_normalisation_sensitive_indices_are_bin_edges():
     print("c2 normalisation-sensitive voxel indices (fixed-order fp64 vs torch-CPU fp32): "
           "%d of %d points; max |norm_coords diff| %.3g" % (total, 3 * B * N, worst_nc))
     assert worst_nc <= 1e-6
+
+
+def _ulp_exposure(b, n, r, seeds):
+    """Points whose voxel index changes when the float acos / atan of the
+    voxelisation (spherical_vox.cu:46,54) return a value 1 or 2 ulps from the
+    correctly rounded one (include/pcr_math.h pcr_acosf / pcr_atanf), in
+    either direction, alone or both at once: (changed, explained by a bin
+    edge, points)."""
+    changed = explained = 0
+    for seed in seeds:
+        xyz, _, _ = gaussian_clouds(b, n, seed=seed)
+        nc = oracle.normalize_sph(xyz)
+        for i in range(b):
+            base = oracle.sph_index(nc[i], r)
+            assert np.array_equal(oracle.sph_index_ulp(nc[i], r, 0, 0), base)
+            moved = np.zeros(n, bool)
+            alt = base.copy()
+            for da in range(-2, 3):
+                for dt in range(-2, 3):
+                    if da == 0 and dt == 0:
+                        continue
+                    v = oracle.sph_index_ulp(nc[i], r, da, dt)
+                    new = (v != base) & ~moved
+                    alt[new] = v[new]
+                    moved |= v != base
+            d, e, worst = edges.explain(nc[i], nc[i], base, alt, r)
+            assert d == int(moved.sum())
+            assert d == e, "cloud %d: %d indices move under +-2 ulp acos/atan, %d on a bin " \
+                "edge (worst %.3g)" % (i, d, e, worst)
+            changed += d
+            explained += e
+    return changed, explained, b * n * len(seeds)
+
+
+def test_c2_acos_atan_ulp_exposure_is_bin_edges():
+    """The 'bit-exact voxel index' claim against a real sm_61 run rests on the
+    correctly rounded acos / atan here; CUDA's float overloads may be 2 ulps
+    off.  At full c2 size every point whose index that could change sits on
+    a bin edge; the count is the unpinned exposure."""
+    d, e, pts = _ulp_exposure(B, N, R, (0, 1))
+    print("c2 acos/atan +-2 ulp exposure: %d of %d points move voxel, all on bin edges"
+          % (d, pts))
+    assert d <= pts // 1000
+
+
+def test_c5_acos_atan_ulp_exposure_is_bin_edges():
+    """The same at BASELINE c5 size (8 x 65,536 points, r = 64)."""
+    d, e, pts = _ulp_exposure(8, 65536, 64, (0,))
+    print("c5 acos/atan +-2 ulp exposure: %d of %d points move voxel, all on bin edges"
+          % (d, pts))
+    assert d <= pts // 1000

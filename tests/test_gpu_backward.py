@@ -160,6 +160,26 @@ def test_sph_avg_vox_backward_c3_shape(dev):
     assert (N(gx)[np.broadcast_to((gind == -1)[:, None, :], gx.shape)] == 0).all()
 
 
+@pytest.mark.parametrize("v0", [-1.5, float("nan"), float("-inf")])
+def test_sph_avg_vox_backward_dropped_points_positive_zero(dev, v0):
+    """Points the voxelisation drops (ind = -1) keep the +0 the reference's
+    zero-initialised grad_x holds (spherical_vox.cu:153-156), whatever
+    grad_y[voxel 0] is: the sorted gather must not write grad_y[0] * 0 there
+    (-0 for a negative value, NaN for inf / NaN)."""
+    from pcr_amd import ops
+    b, n, c, r = 2, 2048, 20, 32
+    nc, _, _, gind, cnt = _sph_setup(b, n, c, r, seed=36)
+    gind = gind.copy()
+    gind[:, ::7] = -1  # about 1 in 7 points dropped
+    gy = np.random.default_rng(37).standard_normal((b, c, r ** 3)).astype(np.float32)
+    gy[:, :, 0] = v0
+    gx = N(ops.spherical_avg_voxelize_backward(T(gy, dev), T(gind, dev), T(cnt, dev)))
+    exp = oracle.avg_voxelize_backward(gy, gind, cnt)
+    drop = np.broadcast_to((gind == -1)[:, None, :], gx.shape)
+    assert (gx[drop] == 0).all() and not np.signbit(gx[drop]).any()
+    assert np.array_equal(gx[~drop], exp[~drop], equal_nan=True)
+
+
 def test_cube_avg_vox_backward_c3_shape(dev):
     from pcr_amd import ops
     b, n, c, r = 4, 2048, 64, 32

@@ -255,3 +255,71 @@ def test_extractor_pipelined_steps(dev, b, n, c, k, r):
         ref = ops.spherical_trilinear_devoxelize_backward(gy, T(exp["dinds"], dev),
                                                           T(exp["dwgts"], dev), r)
         assert torch.equal(gg, ref), s
+
+
+def _check_steps(got, batches, k, r):
+    assert len(got) == len(batches)
+    for s, out in enumerate(got):
+        exp = expected_step(*batches[s], k, r)
+        for key in ("knn_idx", "ind", "cnt", "dinds", "grid", "devox", "desc"):
+            assert np.array_equal(N(out[key]), exp[key]), (s, key)
+        assert np.array_equal(N(out["local_ppf"]), exp["local_ppf"], equal_nan=True), s
+
+
+def test_extractor_pipelined_batches_made_in_loop(dev):
+    """pipelined_steps with batch(s) making its tensors on the caller's stream
+    inside the loop, as train.py:140 does (inputs.to(device)): each batch is
+    uploaded after a GPU-side delay on the current stream, into fresh
+    buffers, and then scaled in place (x * 2 / 2, exact), so a neighbour
+    stream that is not ordered after the producer reads unwritten memory.
+    Every step against the oracle."""
+    from pcr_amd.extractor import SphExtractor
+    b, n, c, k, r, steps = 4, 1024, 16, 32, 32, 5
+    batches = [gaussian_clouds(b, n, seed=60 + s, c=c) for s in range(steps)]
+    staged = [[T(a * np.float32(2.0), dev) for a in bt] for bt in batches]
+    ex = SphExtractor(b, n, c, k, r, device=dev)
+    got = []
+
+    def batch(s):
+        torch.cuda._sleep(2_000_000)  # the producer lags behind the host
+        out = []
+        for src in staged[s]:
+            t = torch.empty_like(src)
+            t.copy_(src)  # device to device: asynchronous on the current stream
+            t.div_(2.0)
+            out.append(t)
+        return tuple(out)
+
+    ex.pipelined_steps(steps, batch, lambda s, out: got.append(
+        {kk: v.clone() for kk, v in out.items()}))
+    torch.cuda.synchronize()
+    _check_steps(got, batches, k, r)
+
+
+def test_extractor_pipelined_after_serial_forward(dev):
+    """The sequence behind the round-3 illegal-address fault: a serial
+    forward whose consume allocates and frees a large gradient on the
+    caller's stream, then pipelined_steps on the same extractor (index set 1
+    made on the first pipelined call, not pre-made by poison()).  Every
+    pipelined step against the oracle."""
+    from pcr_amd import ops
+    from pcr_amd.extractor import SphExtractor
+    b, n, c, k, r, steps = 8, 2048, 64, 32, 32, 4
+    batches = [gaussian_clouds(b, n, seed=70 + s, c=c) for s in range(steps)]
+    tb = [tuple(T(a, dev) for a in bt) for bt in batches]
+    gy = torch.randn((b, c, n), generator=torch.Generator().manual_seed(6)).to(dev)
+    ex = SphExtractor(b, n, c, k, r, device=dev)
+    out = ex.forward(*tb[0])
+    gg = ops.spherical_trilinear_devoxelize_backward(gy, out["dinds"], out["dwgts"], r)
+    gx = ops.spherical_avg_voxelize_backward(gg, out["ind"], out["cnt"])
+    del gg, gx  # freed with their kernels possibly still pending
+    got = []
+
+    def consume(s, o):
+        g2 = ops.spherical_trilinear_devoxelize_backward(gy, o["dinds"], o["dwgts"], r)
+        ops.spherical_avg_voxelize_backward(g2, o["ind"], o["cnt"])
+        got.append({kk: v.clone() for kk, v in o.items()})
+
+    ex.pipelined_steps(steps, lambda s: tb[s], consume)
+    torch.cuda.synchronize()
+    _check_steps(got, batches, k, r)
