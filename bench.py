@@ -78,10 +78,10 @@ def parse(argv=None):
     ap.add_argument("--kernel-iters", type=int, default=50, help="(kept for old command lines)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--schedule", type=int, choices=(0, 1, 2), default=1,
+    ap.add_argument("--schedule", type=int, choices=(1, 2), default=1,
                     help="pcr_extractor_run schedule (include/pcr_amd.h): 1 = three streams "
                          "(sort+select+PPF / prep+means+devox / dense-grid stream), 2 = as 1 "
-                         "with the Morton sort on the prep stream, 0 = two streams")
+                         "with the Morton sort on the prep stream")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="diagnostic: no timing events around the dominant kernel")
     ap.add_argument("--no-verify", action="store_true",
@@ -94,6 +94,10 @@ def parse(argv=None):
     ap.add_argument("--steps-per-launch", type=int, default=40,
                     help="most pipelined steps per native runner call (extract / pairs); "
                          "--steps and --warmup are split into calls of at most this many")
+    ap.add_argument("--batches", type=int, default=None,
+                    help="extract / pairs: distinct input batches cycled through the timed "
+                         "steps (the runner's batch ring; each batch has its own output set; "
+                         "default 20 extract, 8 pairs)")
     args = ap.parse_args(argv)
     b, n, k, r, c = DEFAULTS[args.workload]
     args.batch = b if args.batch is None else args.batch
@@ -106,6 +110,10 @@ def parse(argv=None):
         args.steps = {"c3": 20, "c5": 10}.get(args.workload, 200)
     if args.warmup is None:
         args.warmup = 3 if heavy else 40
+    if args.batches is None:
+        args.batches = 8 if args.workload == "pairs" else 20
+    if args.batches < 1:
+        ap.error("--batches must be >= 1")
     if args.workload == "pairs" and args.batch % 2:
         ap.error("--workload pairs needs an even --batch (source + target clouds)")
     if args.gpus < 1:
@@ -268,8 +276,11 @@ def cpu_baseline(args):
 # ------------------------------------------------------------ workloads
 class ExtractWorkload:
     """BASELINE c2 (extract) / c4 (pairs): the native runner enqueues up to
-    S pipelined steps per call; each call's descriptors are all-gathered
-    across ranks by the product pipeline (pcr_amd.distributed)."""
+    S pipelined steps per call over a ring of R distinct synthetic batches
+    (step s reads batch (s mod R) and writes that batch's own output set, as
+    the reference's loaders hand a fresh batch to every iteration:
+    datasets/deepgmr_mn40.py:71-97); each call's descriptors are
+    all-gathered across ranks by the product pipeline (pcr_amd.distributed)."""
 
     def __init__(self, args, dev, rank, world):
         from pcr_amd.extractor import SphExtractor, algorithmic_bytes_per_cloud, \
@@ -277,22 +288,16 @@ class ExtractWorkload:
         self.args, self.dev, self.world = args, dev, world
         b, n, c, k, r = args.batch, args.points, args.channels, args.k, args.res
         self.b, self.c = b, c
-        xyz, nrm, feat = synthetic_inputs(b, n, c, dev, seed=1234 + rank)
+        self.R = args.batches
+        self.batches = [self._make_batch(args, dev, 1234 + 7919 * rank + i)
+                        for i in range(self.R)]
         if args.workload == "pairs":
-            # targets = sources rotated by a fixed rotation and permuted
-            rot = torch.linalg.qr(torch.randn(3, 3, generator=torch.Generator().manual_seed(7)))[0]
-            rot = rot.to(dev)
-            perm = torch.randperm(n, generator=torch.Generator().manual_seed(8)).to(dev)
-            p = b // 2
-            xyz[p:] = torch.einsum("ij,bjn->bin", rot, xyz[:p])[:, :, perm]
-            nrm[p:] = torch.einsum("ij,bjn->bin", rot, nrm[:p])[:, :, perm]
-            feat[p:] = feat[:p][:, :, perm]
             from pcr_amd.registration import PairExtractor
             self.ex = PairExtractor(b // 2, n, c, k, r, device=dev)
         else:
             self.ex = SphExtractor(b, n, c, k, r, device=dev)
-        self.inputs = (xyz, nrm, feat)
         self.S = max(1, args.steps_per_launch)
+        self.next_set = 0
         self.desc_steps = {}
         self.pipe = None
         if world > 1:
@@ -306,27 +311,50 @@ class ExtractWorkload:
         self.kernel_bytes = stream_kernel_bytes_per_cloud(r, c) * b
         self.KTIMED = 10
 
+    @staticmethod
+    def _make_batch(args, dev, seed):
+        b, n, c = args.batch, args.points, args.channels
+        xyz, nrm, feat = synthetic_inputs(b, n, c, dev, seed=seed)
+        if args.workload == "pairs":
+            # targets = sources rotated by a fixed rotation and permuted
+            g = torch.Generator().manual_seed(seed)
+            rot = torch.linalg.qr(torch.randn(3, 3, generator=g))[0].to(dev)
+            perm = torch.randperm(n, generator=g).to(dev)
+            p = b // 2
+            xyz[p:] = torch.einsum("ij,bjn->bin", rot, xyz[:p])[:, :, perm]
+            nrm[p:] = torch.einsum("ij,bjn->bin", rot, nrm[:p])[:, :, perm]
+            feat[p:] = feat[:p][:, :, perm]
+        return xyz.contiguous(), nrm.contiguous(), feat.contiguous()
+
     def chunks(self, total):
         from pcr_amd.distributed import step_chunks
         return step_chunks(total, self.S)
 
     def verify(self):
-        """Two native-runner steps with the bench's schedule vs one forward():
-        knn_idx, local_ppf, ind, cnt, grid and devox must be identical (every
-        runner output poisoned first)."""
+        """One runner call of R steps over the ring, every ring output
+        poisoned first; then each step's outputs (knn_idx, local_ppf, ind,
+        cnt, grid, devox, desc, and the pair matching) must equal one
+        forward() of that step's batch."""
         args = self.args
-        sx = self.ex.ex if args.workload == "pairs" else self.ex
-        xyz, nrm, feat = self.inputs
-        ref = {kk: v.clone() for kk, v in sx.forward(xyz, nrm, feat).items()}
-        for t in list(sx.outputs(0).values()) + list(sx.outputs(1).values()):
-            t.view(-1).view(torch.uint8).fill_(0xFF)
-        out = sx.run_native(xyz, nrm, feat, 2, None, schedule=args.schedule)
+        pairs = args.workload == "pairs"
+        sx = self.ex.ex if pairs else self.ex
+        ring = sx.ring_outputs(self.R, self.ex.pairs if pairs else 0)
+        for o in ring:
+            for t in o.values():
+                t.view(-1).view(torch.uint8).fill_(0xFF)
+        self.ex.run_ring(self.batches, self.R, 0, None, schedule=args.schedule)
         torch.cuda.synchronize(self.dev)
-        for key in ("knn_idx", "local_ppf", "ind", "cnt", "grid", "devox"):
-            if not torch.equal(out[key], ref[key]) and not torch.allclose(
-                    out[key], ref[key], equal_nan=True):
-                raise SystemExit("bench: runner output %s differs from the single-step path"
-                                 % key)
+        keys = ("knn_idx", "local_ppf", "ind", "cnt", "grid", "devox", "desc")
+        if pairs:
+            keys += ("corr12", "corr21", "idx1", "idx2", "count")
+        for i, (xyz, nrm, feat) in enumerate(self.batches):
+            ref = self.ex.forward(xyz, nrm, feat)
+            for key in keys:
+                got = ring[i][key]
+                if not torch.equal(got, ref[key]) and not torch.allclose(
+                        got, ref[key], equal_nan=True):
+                    raise SystemExit("bench: runner output %s of batch %d differs from the "
+                                     "single-step path" % (key, i))
         return True
 
     def prepare_timing(self):
@@ -336,10 +364,10 @@ class ExtractWorkload:
             self.ex.reserve_timing(self.KTIMED)
 
     def run(self, steps, timed):
-        """`steps` steps; timed: the last call brackets the grid kernel of its
-        last KTIMED steps with HIP events on its stream (in-step durations)."""
+        """`steps` steps over the batch ring, continuing the cycle across
+        calls; timed: the last call brackets the grid kernel of its last
+        KTIMED steps with HIP events on its stream (in-step durations)."""
         from pcr_amd.distributed import run_pipelined
-        xyz, nrm, feat = self.inputs
         ncalls = len(self.chunks(steps))
 
         def launch(i, m):
@@ -347,8 +375,9 @@ class ExtractWorkload:
                 self.desc_steps[m] = torch.empty((m, self.b, self.c), device=self.dev)
             tk = self.KTIMED if (timed and i == ncalls - 1 and
                                  not self.args.no_kernel_timing) else False
-            self.ex.run_native(xyz, nrm, feat, m, self.desc_steps[m],
-                               schedule=self.args.schedule, timed=tk)
+            self.ex.run_ring(self.batches, m, self.next_set, self.desc_steps[m],
+                             schedule=self.args.schedule, timed=tk)
+            self.next_set = (self.next_set + m) % self.R
             return self.desc_steps[m]
 
         return run_pipelined(steps, self.S, launch, self.pipe)
@@ -392,7 +421,8 @@ class ExtractWorkload:
                 "parallelism": "dp%d (clouds sharded, descriptor all-gather)" % self.world,
                 "schedule": a.schedule,
                 "runner_calls": [len(self.chunks(a.warmup)), len(self.chunks(a.steps))],
-                "steps_per_launch": self.S}
+                "steps_per_launch": self.S,
+                "distinct_batches": self.R}
 
 
 class C3Workload:

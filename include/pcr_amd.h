@@ -389,7 +389,19 @@ pcr_status pcr_read_xyzn_txt(const char *path, float *out, long long rows, int c
  * last min(steps, timed_steps) steps of each run (pipeline full; fewer after
  * pcr_runner_set_timed) with timing events on its stream;
  * pcr_runner_grid_times waits for them and returns the per-step durations
- * (ms) of the last run -- the dominant kernel's in-step duration. */
+ * (ms) of the last run -- the dominant kernel's in-step duration.
+ *
+ * Batch ring (nsets > 0, schedules 1 / 2): step s of a call reads its clouds
+ * from, and writes every output into, sets[(set0 + s) % nsets] -- a fresh
+ * batch per step, as the reference's loaders hand one over per iteration
+ * (datasets/deepgmr_mn40.py:71-97, train.py:138-153) -- and the single-set
+ * input / output pointers of pcr_extractor_args are ignored (the workspaces
+ * stay the alternating scratch pair).  With steps <= nsets every step of a
+ * call writes its own set, so after the call (all streams joined back into
+ * `origin`) the outputs of every step are readable on `origin`; the next
+ * call forks from `origin` after whatever the caller enqueued there, so a
+ * consumer enqueued between calls never races the next call's writes.  More
+ * steps than sets in one call overwrite set q with step s + nsets. */
 typedef struct pcr_runner pcr_runner;
 pcr_status pcr_runner_create(int timed_steps, pcr_runner **out);
 void pcr_runner_destroy(pcr_runner *runner);
@@ -397,6 +409,18 @@ pcr_status pcr_runner_grid_times(pcr_runner *runner, float *ms, int cap, int *co
 /* steps timed by each later run (0..timed_steps of pcr_runner_create; the
  * default is all of them) */
 pcr_status pcr_runner_set_timed(pcr_runner *runner, int timed_steps);
+typedef struct pcr_extractor_set {
+  const float *xyz, *normals, *features;  /* [b,3,n], [b,3,n], [b,c,n] */
+  int *knn_idx;                           /* [b,k,n] */
+  float *knn_dist;                        /* [b,k,n] or NULL */
+  float *local_ppf;                       /* [b,4,k,n] */
+  float *norm_coords;                     /* [b,3,n] */
+  int *ind, *cnt;                         /* [b,n], [b,r^3] */
+  float *grid, *devox, *desc;             /* [b,c,r^3], [b,c,n], [b,c] */
+  int *dinds;                             /* [b,8,n] */
+  float *dwgts;                           /* [b,8,n] */
+  int *corr12, *corr21, *idx1, *idx2, *match_count; /* match_pairs > 0: [P,n] / [P] */
+} pcr_extractor_set;
 typedef struct pcr_extractor_args {
   int b, n, c, k, r, relative;
   const float *xyz, *normals, *features;  /* [b,3,n], [b,3,n], [b,c,n] */
@@ -421,6 +445,10 @@ typedef struct pcr_extractor_args {
   int *corr12, *corr21, *idx1, *idx2, *match_count;
   void *match_ws;                         /* pcr_mutual_nn_workspace_size(P, n, n) */
   size_t match_ws_bytes;
+  /* batch ring (see above): nsets sets, step s of the call uses set
+   * (set0 + s) % nsets; nsets = 0: the single set above */
+  int nsets, set0;
+  const pcr_extractor_set *sets;
 } pcr_extractor_args;
 pcr_status pcr_extractor_run(pcr_runner *runner, const pcr_extractor_args *args, int steps,
                              int schedule, float *desc_steps, void *origin, void *s_nbr,

@@ -291,6 +291,67 @@ PCR_HD int pcr_sph_corners(float x, float y, float z, int pos, int r, int idx[8]
   return 1;
 }
 
+/* voxel index (pcr_sph_index) and spherical corners (pcr_sph_corners of that
+ * index) of one point from ONE evaluation of its spherical coordinates: both
+ * functions recompute pcr_sph_coords from the same (x, y, z), so this is
+ * bit-identical to calling them in turn, at half the fp64 trig.  Returns the
+ * index (-1 when dropped); *corners_ok = pcr_sph_corners' return value (0
+ * for a dropped point). */
+PCR_HD int pcr_sph_index_corners(float x, float y, float z, int r, int idx[8], float w[8],
+                                 int *corners_ok) {
+  float gama, alpha, beta;
+  int gx, gy, gz, pos, r2 = r * r;
+  int gg, ga, gb, glo, alo, blo, ghi, ahi, bhi;
+  float glo_f, alo_f, blo_f, gd1, ad1, bd1, gd0, ad0, bd0;
+  *corners_ok = 0;
+  if (!pcr_sph_coords(x, y, z, r, 1, &gama, &alpha, &beta)) return -1;
+  /* pcr_sph_index_v */
+  gx = pcr_f2i(__builtin_floorf(gama * (float)r));
+  gy = pcr_d2i(__builtin_floor((double)((alpha * (float)r) / 2.0f) / PCR_PI));
+  gz = pcr_d2i(__builtin_floor((double)(beta * (float)r) / PCR_PI));
+  if (gx >= r) gx = r - 1;
+  if (gy >= r) gy = r - 1;
+  if (gz >= r) gz = r - 1;
+  pos = gx * r * r + gy * r + gz;
+  /* pcr_sph_corners(x, y, z, pos, r) after its pcr_sph_coords */
+  gg = pos / r2;
+  ga = (pos - gg * r2) / r;
+  gb = pos - gg * r2 - ga * r;
+  glo_f = (float)(gg / r);
+  alo_f = (float)(PCR_PI * 2.0 * (double)ga / (double)r);
+  blo_f = (float)(PCR_PI * (double)gb / (double)r);
+  gd1 = gama - glo_f;
+  ad1 = alpha - alo_f;
+  bd1 = beta - blo_f;
+  gd0 = 1.0f - gd1;
+  ad0 = 1.0f - ad1;
+  bd0 = 1.0f - bd1;
+  w[0] = gd0 * ad0 * bd0;
+  w[1] = gd0 * ad0 * bd1;
+  w[2] = gd0 * ad1 * bd0;
+  w[3] = gd0 * ad1 * bd1;
+  w[4] = gd1 * ad0 * bd0;
+  w[5] = gd1 * ad0 * bd1;
+  w[6] = gd1 * ad1 * bd0;
+  w[7] = gd1 * ad1 * bd1;
+  glo = pcr_f2i(glo_f);
+  alo = pcr_f2i(alo_f);
+  blo = pcr_f2i(blo_f);
+  ghi = (gd1 > 0.0f) ? -1 : 0;
+  ahi = (ad1 > 0.0f) ? -1 : 0;
+  bhi = (bd1 > 0.0f) ? 1 : 0;
+  idx[0] = glo * r2 + alo * r + blo;
+  idx[1] = idx[0] + bhi;
+  idx[2] = idx[0] + (ahi & r);
+  idx[3] = idx[2] + bhi;
+  idx[4] = idx[0] + (ghi & r2);
+  idx[5] = idx[4] + bhi;
+  idx[6] = idx[4] + (ahi & r);
+  idx[7] = idx[6] + bhi;
+  *corners_ok = 1;
+  return pos;
+}
+
 /* ---- cube trilinear corners (trilinear_devox.cu:45-80) on continuous
  * voxel coordinates already clamped to [0, r-1] ---- */
 PCR_HD void pcr_cube_corners(float x, float y, float z, int r, int idx[8], float w[8]) {

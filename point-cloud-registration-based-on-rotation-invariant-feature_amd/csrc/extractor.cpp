@@ -56,40 +56,70 @@ namespace {
     }                                                                            \
   } while (0)
 
+// The inputs and outputs of one step: the single set of pcr_extractor_args
+// (nsets = 0, devox corners alternating with the scratch slot) or the batch
+// ring's set (set0 + s) % nsets
+struct StepIO {
+  const float *xyz, *normals, *features;
+  int* knn_idx;
+  float *knn_dist, *local_ppf, *norm_coords;
+  int *ind, *cnt;
+  float *grid, *devox, *desc;
+  int* dinds;
+  float* dwgts;
+  int *corr12, *corr21, *idx1, *idx2, *match_count;
+};
+
+StepIO step_io(const pcr_extractor_args* a, int s, int slot) {
+  if (a->nsets > 0) {
+    const pcr_extractor_set& t = a->sets[(a->set0 + s) % a->nsets];
+    return StepIO{t.xyz,  t.normals,     t.features, t.knn_idx, t.knn_dist, t.local_ppf,
+                  t.norm_coords, t.ind,  t.cnt,      t.grid,    t.devox,    t.desc,
+                  t.dinds, t.dwgts,      t.corr12,   t.corr21,  t.idx1,     t.idx2,
+                  t.match_count};
+  }
+  return StepIO{a->xyz,  a->normals,     a->features,     a->knn_idx, a->knn_dist, a->local_ppf,
+                a->norm_coords, a->ind,  a->cnt,          a->grid,    a->devox,    a->desc,
+                a->dinds[slot], a->dwgts[slot], a->corr12, a->corr21, a->idx1,     a->idx2,
+                a->match_count};
+}
+
 // Morton sort of the cloud into KNN workspace q; false when the sorted path
 // does not apply (nothing launched; the selection then runs unsorted)
-pcr_status knn_sort(const pcr_extractor_args* a, int q, hipStream_t st, bool* sorted) {
-  const pcr_status rc = pcr_knn_prepare(a->xyz, a->b, a->n, a->knn_ws[q], a->knn_ws_bytes, st);
+pcr_status knn_sort(const pcr_extractor_args* a, const StepIO& io, int q, hipStream_t st,
+                    bool* sorted) {
+  const pcr_status rc = pcr_knn_prepare(io.xyz, a->b, a->n, a->knn_ws[q], a->knn_ws_bytes, st);
   *sorted = rc == PCR_OK;
   return rc == PCR_ERR_UNSUPPORTED ? PCR_OK : rc;
 }
 
 // selection (from KNN workspace q) + local PPF of one step on `st`
-pcr_status knn_select_ppf(const pcr_extractor_args* a, int q, bool sorted, hipStream_t st) {
+pcr_status knn_select_ppf(const pcr_extractor_args* a, const StepIO& io, int q, bool sorted,
+                          hipStream_t st) {
   if (!sorted)  // no sorted path: the one-call selection + PPF
-    return pcr_knn_local_ppf(a->xyz, a->normals, a->b, a->n, a->k, a->relative, a->knn_idx,
-                             a->knn_dist, a->local_ppf, a->knn_ws[q], a->knn_ws_bytes, st);
-  if (a->knn_dist) {  // distances requested: the selection writes in original order
-    PCR_TRY(pcr_knn_local_ppf_prepared(a->xyz, a->normals, a->b, a->n, a->k, a->relative,
-                                         a->knn_idx, a->knn_dist, nullptr, a->knn_ws[q],
+    return pcr_knn_local_ppf(io.xyz, io.normals, a->b, a->n, a->k, a->relative, io.knn_idx,
+                             io.knn_dist, io.local_ppf, a->knn_ws[q], a->knn_ws_bytes, st);
+  if (io.knn_dist) {  // distances requested: the selection writes in original order
+    PCR_TRY(pcr_knn_local_ppf_prepared(io.xyz, io.normals, a->b, a->n, a->k, a->relative,
+                                         io.knn_idx, io.knn_dist, nullptr, a->knn_ws[q],
                                          a->knn_ws_bytes, st));
-    return pcr_local_ppf_forward(a->xyz, a->normals, a->xyz, a->normals, a->knn_idx, a->b, a->n,
-                                 a->n, a->k, 1, a->relative, a->local_ppf, st);
+    return pcr_local_ppf_forward(io.xyz, io.normals, io.xyz, io.normals, io.knn_idx, a->b, a->n,
+                                 a->n, a->k, 1, a->relative, io.local_ppf, st);
   }
   // selection in sorted query order, the PPF launch writes knn_idx + PPF
-  return pcr_knn_select_ppf(a->xyz, a->normals, a->b, a->n, a->k, a->relative, a->knn_idx,
-                            a->local_ppf, a->knn_ws[q], a->knn_ws_bytes, st);
+  return pcr_knn_select_ppf(io.xyz, io.normals, a->b, a->n, a->k, a->relative, io.knn_idx,
+                            io.local_ppf, a->knn_ws[q], a->knn_ws_bytes, st);
 }
 
 // the step's registration matching (source clouds [0, P) against targets
 // [P, 2P)) on the devox features the step just wrote
-pcr_status match_pairs(const pcr_extractor_args* a, hipStream_t st) {
+pcr_status match_pairs(const pcr_extractor_args* a, const StepIO& io, hipStream_t st) {
   if (a->match_pairs <= 0) return PCR_OK;
   const int P = a->match_pairs;
-  const float* src = a->devox;
-  const float* tgt = a->devox + (size_t)P * a->c * a->n;
-  return pcr_mutual_nn_match_cm(src, tgt, P, a->n, a->n, a->c, a->corr12, a->corr21, a->idx1,
-                                a->idx2, a->match_count, a->match_ws, a->match_ws_bytes, st);
+  const float* src = io.devox;
+  const float* tgt = io.devox + (size_t)P * a->c * a->n;
+  return pcr_mutual_nn_match_cm(src, tgt, P, a->n, a->n, a->c, io.corr12, io.corr21, io.idx1,
+                                io.idx2, io.match_count, a->match_ws, a->match_ws_bytes, st);
 }
 
 }  // namespace
@@ -161,9 +191,17 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
   const hipStream_t org = as_stream(origin), sn = as_stream(s_nbr_p), sp = as_stream(s_pre_p),
                     sv = as_stream(s_vox_p);
   const int nslots = schedule >= 1 ? 2 : 1;
+  PCR_REQUIRE(a->nsets >= 0 && (a->nsets == 0 || (a->sets && schedule >= 1 && a->set0 >= 0)),
+              "extractor_run: a batch ring needs sets, set0 >= 0 and schedule 1 or 2");
   for (int q = 0; q < nslots; q++)
-    PCR_REQUIRE(a->vox_ws[q] && a->dinds[q] && a->dwgts[q] && a->knn_ws[schedule == 2 ? q : 0],
+    PCR_REQUIRE(a->vox_ws[q] && a->knn_ws[schedule == 2 ? q : 0] &&
+                    (a->nsets > 0 || (a->dinds[q] && a->dwgts[q])),
                 "extractor_run: buffer set %d missing", q);
+  for (int t = 0; t < a->nsets; t++)
+    PCR_REQUIRE(a->sets[t].xyz && a->sets[t].normals && a->sets[t].features &&
+                    a->sets[t].knn_idx && a->sets[t].local_ppf && a->sets[t].grid &&
+                    a->sets[t].devox && a->sets[t].dinds && a->sets[t].dwgts,
+                "extractor_run: ring set %d incomplete", t);
   // no runner: a transient one (events created and destroyed in this call;
   // hipEventDestroy of a pending event is deferred until it completes)
   pcr_runner* tmp = nullptr;
@@ -187,44 +225,44 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
   for (hipStream_t st : {sn, sp, sv}) PCR_HIP(hipStreamWaitEvent(st, fork, 0), "fork wait");
   const size_t dstride = (size_t)a->b * a->c;
   for (int s = 0; s < steps; s++) {
-    float* desc = desc_steps ? desc_steps + (size_t)s * dstride : a->desc;
+    const int q = schedule >= 1 ? (s & 1) : 0;  // scratch slot
+    const StepIO io = step_io(a, s, q);
+    float* desc = desc_steps ? desc_steps + (size_t)s * dstride : io.desc;
     bool sorted = false;
     if (schedule == 0) {
-      PCR_TRY(knn_sort(a, 0, sn, &sorted));
-      PCR_TRY(knn_select_ppf(a, 0, sorted, sn));
-      PCR_TRY(pcr_extractor_voxel_stage(a->xyz, a->features, a->b, a->c, a->n, a->r,
-                                        a->norm_coords, a->ind, a->cnt, a->grid, a->devox,
-                                        a->dinds[0], a->dwgts[0], desc, a->vox_ws[0],
+      PCR_TRY(knn_sort(a, io, 0, sn, &sorted));
+      PCR_TRY(knn_select_ppf(a, io, 0, sorted, sn));
+      PCR_TRY(pcr_extractor_voxel_stage(io.xyz, io.features, a->b, a->c, a->n, a->r,
+                                        io.norm_coords, io.ind, io.cnt, io.grid, io.devox,
+                                        io.dinds, io.dwgts, desc, a->vox_ws[0],
                                         a->vox_ws_bytes, sv));
-      PCR_TRY(match_pairs(a, sv));
+      PCR_TRY(match_pairs(a, io, sv));
       continue;
     }
-    const int q = s & 1;
     if (schedule == 2) {
       if (s >= 2) PCR_HIP(hipStreamWaitEvent(sp, sel_done[q], 0), "knn slot wait");
-      PCR_TRY(knn_sort(a, q, sp, &sorted));
+      PCR_TRY(knn_sort(a, io, q, sp, &sorted));
       PCR_HIP(hipEventRecord(sort_done[q], sp), "sort record");
     }
     if (s >= 2) PCR_HIP(hipStreamWaitEvent(sp, stream_done[q], 0), "slot wait");
-    PCR_TRY(pcr_extractor_voxel_prep(a->xyz, a->b, a->n, a->r, a->norm_coords, a->ind,
-                                       a->dinds[q], a->dwgts[q], a->vox_ws[q], a->vox_ws_bytes,
-                                       sp));
-    PCR_TRY(pcr_extractor_voxel_means_devox(a->features, a->b, a->c, a->n, a->r, a->devox,
-                                            a->dinds[q], a->dwgts[q], desc, a->vox_ws[q],
+    PCR_TRY(pcr_extractor_voxel_prep(io.xyz, a->b, a->n, a->r, io.norm_coords, io.ind, io.dinds,
+                                       io.dwgts, a->vox_ws[q], a->vox_ws_bytes, sp));
+    PCR_TRY(pcr_extractor_voxel_means_devox(io.features, a->b, a->c, a->n, a->r, io.devox,
+                                            io.dinds, io.dwgts, desc, a->vox_ws[q],
                                             a->vox_ws_bytes, sp));
     PCR_HIP(hipEventRecord(means_done[q], sp), "means record");
-    PCR_TRY(match_pairs(a, sp));
+    PCR_TRY(match_pairs(a, io, sp));
     PCR_HIP(hipStreamWaitEvent(sv, means_done[q], 0), "means wait");
     const bool timed = s >= t_first;
     if (timed) PCR_HIP(hipEventRecord(rn->t0[s - t_first], sv), "timing record");
-    PCR_TRY(pcr_extractor_voxel_stream(a->b, a->c, a->n, a->r, a->cnt, a->grid, a->vox_ws[q],
+    PCR_TRY(pcr_extractor_voxel_stream(a->b, a->c, a->n, a->r, io.cnt, io.grid, a->vox_ws[q],
                                        a->vox_ws_bytes, sv));
     if (timed) PCR_HIP(hipEventRecord(rn->t1[s - t_first], sv), "timing record");
     PCR_HIP(hipEventRecord(stream_done[q], sv), "stream record");
     if (schedule == 2) {
       PCR_HIP(hipStreamWaitEvent(sn, sort_done[q], 0), "sort wait");
       // (the PPF launch reads the workspace too: the slot is free after it)
-      PCR_TRY(knn_select_ppf(a, q, sorted, sn));
+      PCR_TRY(knn_select_ppf(a, io, q, sorted, sn));
       PCR_HIP(hipEventRecord(sel_done[q], sn), "select record");
     } else {
       // the first step's neighbour stream starts after that step's voxel
@@ -232,8 +270,8 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
       // the grid stream starts ~1/3 sooner (a 20-step call: 289k -> 298k
       // clouds/s; long runs unchanged)
       if (s == 0) PCR_HIP(hipStreamWaitEvent(sn, means_done[q], 0), "head wait");
-      PCR_TRY(knn_sort(a, 0, sn, &sorted));
-      PCR_TRY(knn_select_ppf(a, 0, sorted, sn));
+      PCR_TRY(knn_sort(a, io, 0, sn, &sorted));
+      PCR_TRY(knn_select_ppf(a, io, 0, sorted, sn));
     }
   }
   int i = 0;

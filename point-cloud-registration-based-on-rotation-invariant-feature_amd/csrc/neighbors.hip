@@ -345,6 +345,80 @@ __global__ __launch_bounds__(NT) void local_ppf_self_kernel(const float* __restr
   }
 }
 
+// The same local PPF from the selection's sorted-order id rows
+// (pcr_knn_select_ppf), one workgroup per (cloud, SL slots) covering every
+// point of the cloud: the cloud's coordinates + normals and the SL id rows
+// (sorted query order, KnnSet::sidx) are staged in LDS by coalesced loads,
+// each exactly once per workgroup, and every neighbour / id lookup is an LDS
+// read.  The per-256-point workgroups of local_ppf_self_kernel gathered the
+// id rows through the sort's inverse permutation from global memory, each
+// 4-byte gather on its own line, and the four workgroups of a (cloud, slot
+// group) sat on different XCDs, so every XCD's L2 fetched the rows again:
+// 44.6 MB of HBM traffic per c2 launch against 21.8 MB algorithmic
+// (profiles/r03_pmc_traffic.json).  XCD-aware: the dispatcher deals
+// workgroups round-robin over the 8 XCDs, so unit (id % 8) * (U / 8) + id / 8
+// puts a cloud's slot groups on one XCD (its cloud is fetched into one L2).
+template <int SL, int NT = 512>
+__global__ __launch_bounds__(NT) void local_ppf_cloud_kernel(const float* __restrict__ xyz,
+                                                              const float* __restrict__ nrm, int n,
+                                                              int k, int relative,
+                                                              float* __restrict__ out,
+                                                              const int* __restrict__ sidx,
+                                                              const int* __restrict__ inv,
+                                                              int npad, int* __restrict__ idx_out) {
+  extern __shared__ __align__(16) float cl_s[];  // [6][n] x y z nx ny nz, then [SL][npad] ids
+  int* id_s = (int*)(cl_s + 6 * n);
+  constexpr int PT = kPpfSelfMaxN / NT;  // points per thread at most
+  const int G = (k + SL - 1) / SL;
+  const int U = gridDim.x;
+  const int id = blockIdx.x;
+  const int u = (U % 8 == 0) ? (id % 8) * (U / 8) + id / 8 : id;
+  const int b = u / G;
+  const int q0 = (u - b * G) * SL;
+  const int sl = min(SL, k - q0);
+  const int tid = threadIdx.x;
+  // this thread's points' rows in sorted order, loaded before the staging
+  int p[PT];
+#pragma unroll
+  for (int e = 0; e < PT; e++) {
+    const int j = e * NT + tid;
+    p[e] = j < n ? inv[(size_t)b * n + j] : 0;
+  }
+  const float* P = xyz + (size_t)b * 3 * n;
+  const float* Nn = nrm + (size_t)b * 3 * n;
+  for (int i = tid; i < 3 * n; i += NT) {
+    cl_s[i] = P[i];
+    cl_s[3 * n + i] = Nn[i];
+  }
+  const int* rows = sidx + ((size_t)b * kKnnSortedK + q0) * npad;
+  for (int i = tid; i < sl * npad; i += NT) id_s[i] = rows[i];
+  __syncthreads();
+  float* O = out + (size_t)b * 4 * k * n;
+  int* I = idx_out + (size_t)b * k * n;
+#pragma unroll
+  for (int e = 0; e < PT; e++) {
+    const int j = e * NT + tid;
+    if (j >= n) break;
+    const float cx = cl_s[j], cy = cl_s[n + j], cz = cl_s[2 * n + j];
+    const float cnx = cl_s[3 * n + j], cny = cl_s[4 * n + j], cnz = cl_s[5 * n + j];
+#pragma unroll
+    for (int s = 0; s < SL; s++) {
+      if (s >= sl) break;
+      const int q = q0 + s;
+      const int jd = id_s[s * npad + p[e]];
+      I[(size_t)q * n + j] = jd;
+      const unsigned si = (jd < 0 || jd >= n) ? 0u : (unsigned)jd;
+      float o[4];
+      pcr_local_ppf(cx, cy, cz, cnx, cny, cnz, cl_s[si], cl_s[n + si], cl_s[2 * n + si],
+                    cl_s[3 * n + si], cl_s[4 * n + si], cl_s[5 * n + si], relative, o);
+      // nontemporal: the PPF rows are streamed out
+#pragma unroll
+      for (int ch = 0; ch < 4; ch++)
+        __builtin_nontemporal_store(o[ch], &O[((size_t)ch * k + q) * n + j]);
+    }
+  }
+}
+
 // ball_query.cu:30-49: points staged through LDS tiles; per-centre early exit
 constexpr int kBqTile = 1024;
 __global__ __launch_bounds__(256) void ball_query_kernel(const float* __restrict__ centers,
@@ -705,10 +779,11 @@ extern "C" pcr_status pcr_knn_select_ppf(const float* xyz, const float* normals,
       knn_spatial(xyz, xyz, b, n, n, k, nullptr, idx, nullptr, nullptr, nullptr, nullptr, 0,
                   nullptr, const_cast<void*>(workspace), workspace_bytes, true, st, 2 | 4) ==
           PCR_OK) {
-    constexpr int SL = 8;
-    hipLaunchKernelGGL((local_ppf_self_kernel<SL>), dim3(ceil_div(n, 256), ceil_div(k, SL), b),
-                       dim3(256), (size_t)6 * n * 4, st, xyz, normals, nullptr, n, k, relative,
-                       ppf, sidx, inv, npad, idx);
+    constexpr int SL = 4;
+    const size_t lds = ((size_t)6 * n + (size_t)SL * npad) * 4;
+    allow_big_lds(local_ppf_cloud_kernel<SL>, lds);
+    hipLaunchKernelGGL((local_ppf_cloud_kernel<SL>), dim3(b * ceil_div(k, SL)), dim3(512), lds,
+                       st, xyz, normals, n, k, relative, ppf, sidx, inv, npad, idx);
     return launch_status("knn_select_ppf");
   }
   const pcr_status rc = pcr_knn_local_ppf_prepared(xyz, normals, b, n, k, relative, idx, nullptr,

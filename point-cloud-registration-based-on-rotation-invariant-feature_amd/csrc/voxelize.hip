@@ -265,14 +265,17 @@ __global__ __launch_bounds__(NT) void vox_prep_kernel(
           o[i + n] = py[e];
           o[i + 2 * n] = pz[e];
         }
-        v = pcr_sph_index(px[e], py[e], pz[e], r);
-        valid = v >= 0;
         if (MODE == kSphNormalize && dinds) {
+          // index and corners from one evaluation of the spherical
+          // coordinates (bit-identical to pcr_sph_index + pcr_sph_corners)
           int cidx[8];
           float cw[8];
+          int okc;
+          v = pcr_sph_index_corners(px[e], py[e], pz[e], r, cidx, cw, &okc);
+          valid = v >= 0;
           int* I = dinds + (size_t)b * 8 * n;
           float* Wt = dwgts + (size_t)b * 8 * n;
-          const bool ok = valid && pcr_sph_corners(px[e], py[e], pz[e], v, r, cidx, cw);
+          const bool ok = valid && okc;
           corner_ok[e] = ok;
 #pragma unroll
           for (int q = 0; q < 8; q++) corner_cell[MODE == kSphNormalize ? e : 0][q] = cidx[q];
@@ -281,6 +284,9 @@ __global__ __launch_bounds__(NT) void vox_prep_kernel(
             I[i + (size_t)q * n] = ok ? cidx[q] : ((q == 0 && !valid) ? -1 : 0);
             Wt[i + (size_t)q * n] = ok ? cw[q] : 0.0f;
           }
+        } else {
+          v = pcr_sph_index(px[e], py[e], pz[e], r);
+          valid = v >= 0;
         }
       }
       ind[(size_t)b * n + i] = v;

@@ -81,6 +81,14 @@ SIGNATURES = {
 
 
 
+class ExtractorSet(ctypes.Structure):
+    """struct pcr_extractor_set of include/pcr_amd.h (one batch-ring set)"""
+    _fields_ = [("xyz", P), ("normals", P), ("features", P), ("knn_idx", P), ("knn_dist", P),
+                ("local_ppf", P), ("norm_coords", P), ("ind", P), ("cnt", P), ("grid", P),
+                ("devox", P), ("desc", P), ("dinds", P), ("dwgts", P), ("corr12", P),
+                ("corr21", P), ("idx1", P), ("idx2", P), ("match_count", P)]
+
+
 class ExtractorArgs(ctypes.Structure):
     """struct pcr_extractor_args of include/pcr_amd.h"""
     _fields_ = [("b", I), ("n", I), ("c", I), ("k", I), ("r", I), ("relative", I),
@@ -89,7 +97,8 @@ class ExtractorArgs(ctypes.Structure):
                 ("devox", P), ("desc", P), ("dinds", P * 2), ("dwgts", P * 2), ("knn_ws", P * 2),
                 ("knn_ws_bytes", SZ), ("vox_ws", P * 2), ("vox_ws_bytes", SZ),
                 ("match_pairs", I), ("corr12", P), ("corr21", P), ("idx1", P), ("idx2", P),
-                ("match_count", P), ("match_ws", P), ("match_ws_bytes", SZ)]
+                ("match_count", P), ("match_ws", P), ("match_ws_bytes", SZ),
+                ("nsets", I), ("set0", I), ("sets", ctypes.POINTER(ExtractorSet))]
 
 
 _lib = None

@@ -492,6 +492,84 @@ class SphExtractor:
         last = (steps - 1) & 1 if schedule >= 1 else 0
         return self.outputs(slot=last)
 
+    # ------------------------------------------------------------ batch ring
+    def ring_outputs(self, nsets, match_pairs=0):
+        """The output sets of run_ring: one dict of output tensors per batch
+        slot (knn_idx, local_ppf, norm_coords, ind, cnt, grid, devox, desc,
+        dinds, dwgts; the matching outputs when match_pairs > 0), made once
+        per ring size on the caller's stream."""
+        ring = getattr(self, "_ring", None)
+        if ring is not None and len(ring) == nsets and self._ring_match == match_pairs:
+            return ring
+        b, n, c, k, r3 = self.b, self.n, self.c, self.k, self.r ** 3
+        e, dev = torch.empty, self.device
+        i32, f32 = dict(dtype=torch.int32, device=dev), dict(dtype=torch.float32, device=dev)
+        ring = []
+        for _ in range(nsets):
+            o = {"knn_idx": e((b, k, n), **i32), "local_ppf": e((b, 4, k, n), **f32),
+                 "norm_coords": e((b, 3, n), **f32), "ind": e((b, n), **i32),
+                 "cnt": e((b, r3), **i32), "grid": e((b, c, r3), **f32),
+                 "devox": e((b, c, n), **f32), "desc": e((b, c), **f32),
+                 "dinds": e((b, 8, n), **i32), "dwgts": e((b, 8, n), **f32)}
+            if self.knn_dist is not None:
+                o["knn_dist"] = e((b, k, n), **f32)
+            if match_pairs:
+                for key in ("corr12", "corr21", "idx1", "idx2"):
+                    o[key] = e((match_pairs, n), **i32)
+                o["count"] = e((match_pairs,), **i32)
+            ring.append(o)
+        self._ring, self._ring_match = ring, match_pairs
+        self._order_new_buffers()
+        return ring
+
+    def run_ring(self, batches, steps, set0=0, desc_steps=None, schedule=1, timed=False,
+                 match=None):
+        """`steps` pipelined steps of the native runner over a batch ring
+        (pcr_extractor_run with nsets = len(batches)): step s reads the
+        clouds of batches[(set0 + s) % R] = (xyz, normals, features) and
+        writes every output into ring_outputs(R)[(set0 + s) % R], so with
+        steps <= R each step's outputs survive the call and are readable on
+        the current stream after it.  match: a
+        registration.PairMatch (its workspace; the matching outputs go to
+        the ring sets).  Returns the ring's output sets."""
+        if schedule not in (1, 2):
+            raise RuntimeError("run_ring needs schedule 1 or 2")
+        R = len(batches)
+        if R < 1:
+            raise RuntimeError("run_ring needs at least one batch")
+        for t in batches:
+            self._check_inputs(*t)
+        mp = match.pairs if match is not None else 0
+        ring = self.ring_outputs(R, mp)
+        ntimed = min(steps, (steps if timed is True else int(timed)) if timed else 0)
+        runner = self._get_runner(ntimed)
+        if self._runner_cap:
+            _lib.check(_lib.load().pcr_runner_set_timed(runner, ntimed), "runner_set_timed")
+        key = ("ring", tuple(tuple(x.data_ptr() for x in t) for t in batches), match)
+        if self._args_key != key:
+            a = self._make_args(*batches[0], match)
+            sets = (_lib.ExtractorSet * R)()
+            for i, ((xyz, nrm, feat), o) in enumerate(zip(batches, ring)):
+                st = sets[i]
+                st.xyz, st.normals, st.features = _ptr(xyz), _ptr(nrm), _ptr(feat)
+                for f in ("knn_idx", "local_ppf", "norm_coords", "ind", "cnt", "grid", "devox",
+                          "desc", "dinds", "dwgts", "corr12", "corr21", "idx1", "idx2"):
+                    setattr(st, f, _ptr(o[f]) if f in o else None)
+                st.knn_dist = _ptr(o["knn_dist"]) if "knn_dist" in o else None
+                st.match_count = _ptr(o["count"]) if "count" in o else None
+            a.nsets, a.sets = R, sets
+            self._args, self._args_key, self._ring_sets = a, key, sets
+        a = self._args
+        a.set0 = int(set0) % R
+        if desc_steps is not None and tuple(desc_steps.shape) != (steps, self.b, self.c):
+            raise RuntimeError("desc_steps must be [steps, B, C]")
+        cur = torch.cuda.current_stream(self.device)
+        _lib.check(_lib.load().pcr_extractor_run(
+            runner, ctypes.byref(a), steps, schedule, _ptr(desc_steps), cur.cuda_stream,
+            self.s_nbr.cuda_stream, self.s_pre.cuda_stream, self.s_vox.cuda_stream),
+            "extractor_run")
+        return ring
+
     def capture(self, xyz, normals, features):
         """Capture one step over these input tensors into a hipGraph."""
         self._check_inputs(xyz, normals, features)

@@ -80,6 +80,14 @@ class PairExtractor:
         out.update(self.match.outputs())
         return out
 
+    def run_ring(self, batches, steps, set0=0, desc_steps=None, schedule=1, timed=False):
+        """`steps` pipelined steps of extraction + matching over a batch ring
+        of packed [2P, ...] batches (SphExtractor.run_ring): step s matches
+        the pairs of batches[(set0 + s) % R] into that ring set's corr12 /
+        corr21 / idx1 / idx2 / count."""
+        return self.ex.run_ring(batches, steps, set0, desc_steps, schedule=schedule,
+                                timed=timed, match=self.match)
+
     def grid_kernel_times(self):
         return self.ex.grid_kernel_times()
 

@@ -83,3 +83,31 @@ def test_workspace_size_query():
     lib = _lib.load()
     assert lib.pcr_voxelize_workspace_size(32, 1024, 32) > 32 * 1024 * 4 * 3
     assert lib.pcr_voxelize_workspace_size(0, 0, 0) == 256
+
+
+def test_extractor_structs_match_header(tmp_path):
+    """The ctypes mirrors of pcr_extractor_args / pcr_extractor_set
+    (pcr_amd/_lib.py) have the header's size and field offsets (gcc on the
+    header; a mismatch would hand the runner garbage pointers)."""
+    import ctypes
+    import subprocess
+    from pcr_amd import _lib
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "pcr_amd.h"',
+             'int main(void) {']
+    for cname, cls in (("pcr_extractor_args", _lib.ExtractorArgs),
+                       ("pcr_extractor_set", _lib.ExtractorSet)):
+        lines.append('printf("%s size %%zu\\n", sizeof(%s));' % (cname, cname))
+        for f in cls._fields_:
+            lines.append('printf("%s %s %%zu\\n", offsetof(%s, %s));' % (cname, f[0], cname, f[0]))
+    lines += ['return 0;', '}']
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
+    got = subprocess.check_output([str(exe)]).decode().split("\n")
+    want = []
+    for cname, cls in (("pcr_extractor_args", _lib.ExtractorArgs),
+                       ("pcr_extractor_set", _lib.ExtractorSet)):
+        want.append("%s size %d" % (cname, ctypes.sizeof(cls)))
+        want += ["%s %s %d" % (cname, f[0], getattr(cls, f[0]).offset) for f in cls._fields_]
+    assert [g for g in got if g] == want

@@ -103,6 +103,40 @@ def test_extractor_native_runner(dev, schedule):
             assert all(0 < t < 100 for t in ms)
 
 
+@pytest.mark.parametrize("schedule", [1, 2])
+def test_extractor_runner_batch_ring(dev, schedule):
+    """pcr_extractor_run over a batch ring of 3 distinct batches (each with
+    its own output set): one call of 3 steps, then a call of 5 steps that
+    continues the cycle at set0 = 3 % 3 and wraps (sets 0 and 1 written
+    twice, by batches 0 and 1 again).  After each call every set holds the
+    oracle's outputs of its batch; desc_steps holds every step's
+    descriptor."""
+    from pcr_amd.extractor import SphExtractor
+    b, n, c, k, r = 4, 1024, 16, 32, 32
+    batches = [gaussian_clouds(b, n, seed=80 + i, c=c) for i in range(3)]
+    tb = [tuple(T(a, dev) for a in bt) for bt in batches]
+    exp = [expected_step(*bt, k, r) for bt in batches]
+    ex = SphExtractor(b, n, c, k, r, device=dev)
+    set0 = 0
+    for steps in (3, 5):
+        ring = ex.ring_outputs(3)
+        for o in ring:
+            for t in o.values():
+                t.view(-1).view(torch.uint8).fill_(0xFF)
+        desc_steps = torch.full((steps, b, c), float("nan"), device=dev)
+        ex.run_ring(tb, steps, set0, desc_steps, schedule=schedule)
+        torch.cuda.synchronize()
+        for i in range(3):
+            for key in ("knn_idx", "ind", "cnt", "dinds", "dwgts", "norm_coords", "grid",
+                        "devox"):
+                assert np.array_equal(N(ring[i][key]), exp[i][key]), (steps, i, key)
+            assert np.array_equal(N(ring[i]["local_ppf"]), exp[i]["local_ppf"],
+                                  equal_nan=True), (steps, i)
+        for s in range(steps):
+            assert np.array_equal(N(desc_steps[s]), exp[(set0 + s) % 3]["desc"]), (steps, s)
+        set0 = (set0 + steps) % 3
+
+
 def test_extractor_full_size_properties(dev):
     """BASELINE c2 shape: 32 x 1024, k=32, r=32, C=64 -- size-independent
     properties: ind consistent with cnt, grid empty where cnt == 0, the grid

@@ -82,3 +82,39 @@ def test_pair_runner_rejects_odd_batch(dev):
     with pytest.raises(RuntimeError):
         ex.run_native(T(xyz, dev), T(nrm, dev), T(feat, dev), 1,
                       match=PairMatch(1, 256, dev))
+
+
+def _pair_batch(p, n, c, seed):
+    xyz, nrm, feat = gaussian_clouds(2 * p, n, seed=seed, c=c)
+    rng = np.random.default_rng(seed)
+    q, _ = np.linalg.qr(rng.standard_normal((3, 3)))
+    for i in range(p):
+        perm = rng.permutation(n)
+        xyz[p + i] = (q @ xyz[i])[:, perm]
+        nrm[p + i] = (q @ nrm[i])[:, perm]
+        feat[p + i] = feat[i][:, perm]
+    return xyz.astype(np.float32), nrm.astype(np.float32), feat
+
+
+def test_pair_runner_batch_ring(dev):
+    """BASELINE c4 over distinct pair batches (datasets/deepgmr_mn40.py:71-97,
+    a new pair per item): the native runner's batch ring, 3 batches of 2
+    pairs, 3 steps; every ring set's extractor outputs and matching against
+    the oracle of its batch."""
+    from pcr_amd.registration import PairExtractor
+    p, n, c, k, r = 2, 1024, 32, 32, 32
+    batches = [_pair_batch(p, n, c, 90 + i) for i in range(3)]
+    tb = [tuple(T(a, dev) for a in bt) for bt in batches]
+    pe = PairExtractor(p, n, c, k, r, device=dev)
+    ring = pe.ex.ring_outputs(3, p)
+    for o in ring:
+        for t in o.values():
+            t.view(-1).view(torch.uint8).fill_(0xFF)
+    pe.run_ring(tb, 3)
+    torch.cuda.synchronize()
+    for i, bt in enumerate(batches):
+        exp = oracle_pair_step(*bt, k, r, p)
+        for key in ("knn_idx", "ind", "cnt", "grid", "devox", "desc"):
+            assert np.array_equal(N(ring[i][key]), exp[key]), (i, key)
+        for name, e in zip(("corr12", "corr21", "idx1", "idx2", "count"), exp["match"]):
+            assert np.array_equal(N(ring[i][name]), e), (i, name)
