@@ -62,6 +62,16 @@ pcr_status pcr_knn_backward(const float *xyz1, const float *xyz2, const float *g
                             const float *graddist2, const int *idx1, const int *idx2, int b,
                             int c, int n, int m, int k, float *gradxyz1, float *gradxyz2,
                             void *stream);
+/* The same without atomics (bit-repeatable): each direction's (query, slot)
+ * pairs counting-sorted by neighbour in `workspace`
+ * (pcr_knn_backward_workspace_size bytes), then one gather per point of its
+ * own terms and of the pairs naming it.  Clouds of more than 16384 points
+ * take pcr_knn_backward. */
+size_t pcr_knn_backward_workspace_size(int b, int n, int m, int k);
+pcr_status pcr_knn_backward_ws(const float *xyz1, const float *xyz2, const float *graddist1,
+                               const float *graddist2, const int *idx1, const int *idx2, int b,
+                               int c, int n, int m, int k, float *gradxyz1, float *gradxyz2,
+                               void *workspace, size_t workspace_bytes, void *stream);
 
 /* ---------------------------------------------------------------- PPF ----
  * spherical_ppf_forward (modules/functional/src/spherical_ppf/ppf.cpp:17-36,

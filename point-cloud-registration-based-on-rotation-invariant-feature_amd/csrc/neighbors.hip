@@ -208,6 +208,156 @@ __global__ __launch_bounds__(256) void knn_grad_kernel(const float* __restrict__
   }
 }
 
+// KNN backward without atomics (contract knn.cu:52-78, both launches of
+// knn.cu:88-98): every output element is a gather of its own terms in a
+// fixed order, so the gradient is bit-repeatable.  Point i of cloud A gets
+//   sum_q  g(q,i) (xA[i] - xB[idxA(q,i)])                    own slots
+//   - sum over the pairs (q, i') of cloud B's direction with idxB(q,i') = i
+//         of g(q,i') (xB[i'] - xA[i])                         as a neighbour
+// with g = 2 graddist skipped at >= 20000, every term the reference's own
+// product.  The second sum needs, per target point, the list of pairs that
+// name it: knn_bwd_sort_kernel counting-sorts each direction's pairs by
+// target (one workgroup per (cloud, direction), LDS counters), then orders
+// each target's segment by pair id (the arrival order of the placement is
+// not deterministic), and knn_bwd_gather_kernel sums, one thread per point.
+constexpr int kKnnBwdThreads = 1024;
+constexpr int kKnnBwdMaxT = 16384;  // targets per cloud the LDS counters hold
+
+struct KnnBwdWs {
+  int* start[2];  // [b][T_d + 1] segment starts of direction d (by target)
+  int* list[2];   // [b][k N_d] pair ids (q N_d + i) by target, ascending within a target
+  int* tmp[2];    // [b][k N_d] the same in arrival order
+};
+
+static size_t knn_bwd_ws_layout(int b, int n, int m, int k, KnnBwdWs* w, char* base) {
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    char* q = base ? base + off : nullptr;
+    off = (off + bytes + 255) / 256 * 256;
+    return (int*)q;
+  };
+  const int N[2] = {n, m}, T[2] = {m, n};
+  for (int d = 0; d < 2; d++) {
+    int* s = take((size_t)b * (T[d] + 1) * 4);
+    int* l = take((size_t)b * k * N[d] * 4);
+    int* t = take((size_t)b * k * N[d] * 4);
+    if (w) {
+      w->start[d] = s;
+      w->list[d] = l;
+      w->tmp[d] = t;
+    }
+  }
+  return off;
+}
+
+__global__ __launch_bounds__(kKnnBwdThreads) void knn_bwd_sort_kernel(
+    const float* __restrict__ gd0, const int* __restrict__ idx0, const float* __restrict__ gd1,
+    const int* __restrict__ idx1, int n, int m, int k, KnnBwdWs ws) {
+  extern __shared__ int cnt_s[];  // [T]
+  __shared__ int scan_s[kKnnBwdThreads / kWave + 1];
+  const int b = blockIdx.x, d = blockIdx.y, tid = threadIdx.x;
+  const int N = d ? m : n, T = d ? n : m;
+  const size_t P = (size_t)k * N;
+  const float* gd = (d ? gd1 : gd0) + (size_t)b * P;
+  const int* idx = (d ? idx1 : idx0) + (size_t)b * P;
+  int* start = ws.start[d] + (size_t)b * (T + 1);
+  int* list = ws.list[d] + (size_t)b * P;
+  int* tmp = ws.tmp[d] + (size_t)b * P;
+  auto target = [&](size_t p) {
+    const float g = gd[p] * 2.0f;
+    const int j = idx[p];
+    return (!(g >= 20000.0f) && j >= 0 && j < T) ? j : -1;  // knn.cu:68: NaN is not skipped
+  };
+  for (int t = tid; t < T; t += kKnnBwdThreads) cnt_s[t] = 0;
+  __syncthreads();
+  for (size_t p = tid; p < P; p += kKnnBwdThreads) {
+    const int j = target(p);
+    if (j >= 0) atomicAdd(&cnt_s[j], 1);
+  }
+  __syncthreads();
+  {
+    const int chunk = (T + kKnnBwdThreads - 1) / kKnnBwdThreads;
+    const int t0 = min(T, tid * chunk), t1 = min(T, t0 + chunk);
+    int sum = 0;
+    for (int t = t0; t < t1; t++) sum += cnt_s[t];
+    const int incl = block_inclusive_scan(sum, scan_s);
+    int run = incl - sum;
+    for (int t = t0; t < t1; t++) {
+      const int c = cnt_s[t];
+      start[t] = run;
+      cnt_s[t] = run;  // placement cursor
+      run += c;
+    }
+    if (tid == kKnnBwdThreads - 1) start[T] = incl;
+  }
+  __syncthreads();
+  for (size_t p = tid; p < P; p += kKnnBwdThreads) {
+    const int j = target(p);
+    if (j >= 0) tmp[atomicAdd(&cnt_s[j], 1)] = (int)p;
+  }
+  __threadfence_block();
+  __syncthreads();
+  // every pair's final place: its rank by pair id within its target's segment
+  const int total = start[T];
+  for (int e = tid; e < total; e += kKnnBwdThreads) {
+    const int p = tmp[e];
+    const int j = idx[p];
+    const int s0 = start[j], s1 = start[j + 1];
+    int rank = 0;
+    for (int x = s0; x < s1; x++) rank += tmp[x] < p ? 1 : 0;
+    list[s0 + rank] = p;
+  }
+}
+
+template <int CG>
+__global__ __launch_bounds__(256) void knn_bwd_gather_kernel(
+    const float* __restrict__ x1, const float* __restrict__ x2, const float* __restrict__ gd0,
+    const int* __restrict__ idx0, const float* __restrict__ gd1, const int* __restrict__ idx1,
+    int c, int n, int m, int k, KnnBwdWs ws, float* __restrict__ g1, float* __restrict__ g2) {
+  const int b = blockIdx.y;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n + m) return;
+  const int side = t < n ? 0 : 1;  // cloud A of this point: 0 = xyz1, 1 = xyz2
+  const int i = side ? t - n : t;
+  const int Na = side ? m : n, Nb = side ? n : m;
+  const float* xa = (side ? x2 : x1) + (size_t)b * c * Na;
+  const float* xb = (side ? x1 : x2) + (size_t)b * c * Nb;
+  const float* gdo = (side ? gd1 : gd0) + (size_t)b * k * Na;  // own direction
+  const int* ido = (side ? idx1 : idx0) + (size_t)b * k * Na;
+  const float* gdt = (side ? gd0 : gd1) + (size_t)b * k * Nb;  // cloud B's direction
+  const int* lst = ws.list[1 - side] + (size_t)b * k * Nb;
+  const int* st = ws.start[1 - side] + (size_t)b * (Na + 1);
+  float* out = (side ? g2 : g1) + (size_t)b * c * Na;
+  const int s0 = st[i], s1 = st[i + 1];
+  for (int c0 = 0; c0 < c; c0 += CG) {
+    float acc[CG], xi[CG];
+#pragma unroll
+    for (int p = 0; p < CG; p++) {
+      acc[p] = 0.0f;
+      xi[p] = c0 + p < c ? xa[(size_t)(c0 + p) * Na + i] : 0.0f;
+    }
+    for (int q = 0; q < k; q++) {
+      const float g = gdo[(size_t)q * Na + i] * 2.0f;
+      const int j = ido[(size_t)q * Na + i];
+      if (g >= 20000.0f || j < 0 || j >= Nb) continue;
+#pragma unroll
+      for (int p = 0; p < CG; p++)
+        if (c0 + p < c) acc[p] += g * (xi[p] - xb[(size_t)(c0 + p) * Nb + j]);
+    }
+    for (int e = s0; e < s1; e++) {
+      const int pp = lst[e];
+      const int i2 = pp % Nb;
+      const float g = gdt[pp] * 2.0f;
+#pragma unroll
+      for (int p = 0; p < CG; p++)
+        if (c0 + p < c) acc[p] += -(g * (xb[(size_t)(c0 + p) * Nb + i2] - xi[p]));
+    }
+#pragma unroll
+    for (int p = 0; p < CG; p++)
+      if (c0 + p < c) out[(size_t)(c0 + p) * Na + i] = acc[p];
+  }
+}
+
 // ppf.cu:28-90
 __global__ __launch_bounds__(256) void global_ppf_kernel(const float* __restrict__ coords,
                                                          const float* __restrict__ center,
@@ -707,6 +857,44 @@ extern "C" pcr_status pcr_knn_backward(const float* xyz1, const float* xyz2,
     hipLaunchKernelGGL(knn_grad_kernel, dim3(ceil_div(m, 256), b), dim3(256), 0, st, xyz2, xyz1,
                        c, m, n, k, graddist2, idx2, gradxyz2, gradxyz1);
   return launch_status("knn_backward");
+}
+
+extern "C" size_t pcr_knn_backward_workspace_size(int b, int n, int m, int k) {
+  if (b <= 0 || n < 0 || m < 0 || k <= 0) return 256;
+  return knn_bwd_ws_layout(b, n, m, k, nullptr, nullptr);
+}
+
+extern "C" pcr_status pcr_knn_backward_ws(const float* xyz1, const float* xyz2,
+                                          const float* graddist1, const float* graddist2,
+                                          const int* idx1, const int* idx2, int b, int c, int n,
+                                          int m, int k, float* gradxyz1, float* gradxyz2,
+                                          void* workspace, size_t workspace_bytes,
+                                          void* stream) {
+  PCR_REQUIRE(b >= 0 && c >= 1 && n >= 0 && m >= 0 && k >= 1,
+              "knn_backward_ws: invalid sizes");
+  if (b == 0) return PCR_OK;
+  // clouds past the LDS counters: the atomic kernel (same contract)
+  if (n > kKnnBwdMaxT || m > kKnnBwdMaxT || n == 0 || m == 0 ||
+      (size_t)k * (n > m ? n : m) >= (1u << 31))
+    return pcr_knn_backward(xyz1, xyz2, graddist1, graddist2, idx1, idx2, b, c, n, m, k,
+                            gradxyz1, gradxyz2, stream);
+  KnnBwdWs ws;
+  const size_t need = knn_bwd_ws_layout(b, n, m, k, &ws, (char*)workspace);
+  PCR_REQUIRE(workspace != nullptr && workspace_bytes >= need,
+              "knn_backward_ws: workspace too small (%zu < %zu)", workspace_bytes, need);
+  hipStream_t st = as_stream(stream);
+  const size_t lds = (size_t)(n > m ? n : m) * 4;
+  allow_big_lds(knn_bwd_sort_kernel, lds);
+  hipLaunchKernelGGL(knn_bwd_sort_kernel, dim3(b, 2), dim3(kKnnBwdThreads), lds, st, graddist1,
+                     idx1, graddist2, idx2, n, m, k, ws);
+  const dim3 grid(ceil_div(n + m, 256), b);
+  if (c <= 3)
+    hipLaunchKernelGGL((knn_bwd_gather_kernel<3>), grid, dim3(256), 0, st, xyz1, xyz2, graddist1,
+                       idx1, graddist2, idx2, c, n, m, k, ws, gradxyz1, gradxyz2);
+  else
+    hipLaunchKernelGGL((knn_bwd_gather_kernel<4>), grid, dim3(256), 0, st, xyz1, xyz2, graddist1,
+                       idx1, graddist2, idx2, c, n, m, k, ws, gradxyz1, gradxyz2);
+  return launch_status("knn_backward_ws");
 }
 
 extern "C" pcr_status pcr_knn_local_ppf(const float* xyz, const float* normals, int b, int n,

@@ -26,7 +26,6 @@
 //      per-cloud max-pooled descriptor.
 #include "common.hpp"
 
-#include <hipcub/hipcub.hpp>
 
 namespace pcr {
 
@@ -1288,40 +1287,35 @@ __global__ __launch_bounds__(kPrepThreads) void sph_normalize_kernel(
 }
 
 // ------------------------------------------------- clouds of > 4096 points
-// Sort-based, like the small path, at any size: (1) per-point voxel index,
-// count atomics and a 64-bit key (cloud | voxel | point); (2) a device radix
-// sort of the keys (hipCUB), so every voxel's points are contiguous and in
-// ascending point order; (3) an exclusive scan of the counts locates each
-// voxel's segment; (4) one thread per voxel sums its segment in that order
-// and writes all C channels, so the dense grid is written once, coalesced,
-// zeros included.  The reference scatters C fp32 atomics per point into a
-// memset grid (spherical_vox.cu:103-123); here the order is the oracle's
-// ascending point order, bit-exact.  Dropped points (ind = -1) get the
-// voxel field r^3 and sort after every voxel of their cloud.
+// A stable counting sort by voxel, hand-written, at any size: (1) per-point
+// voxel index and count atomics, whose return value is the point's arrival
+// slot in its voxel; (2) a per-cloud exclusive scan of the counts (tile sums,
+// then each tile scans itself after the sum of the tiles before it) locates
+// every voxel's segment; (3) each point lands at start + slot (arrival
+// order); (4) each point of a segment of m > 1 takes its rank by point id
+// among the segment (m reads), so every voxel's points end up in ascending
+// point order -- the order the oracle sums in; (5) one thread per voxel sums
+// its segment in that order and writes all C channels, so the dense grid is
+// written once, coalesced, zeros included.  The reference scatters C fp32
+// atomics per point (spherical_vox.cu:103-123, one cache line each).
 struct BigVoxWs {
-  unsigned long long *keys_in, *keys_out;
-  int* scan;
-  float* featT;  // [b][n][c] point-major copy of the features (nullptr: c == 0)
-  void* temp;
-  size_t temp_bytes;
-  int pb, vb, end_bit;
+  int* slot;      // [b][n] arrival slot of each point in its voxel
+  int* perm_u;    // [b][n] points by voxel, arrival order within a voxel
+  int* perm;      // [b][n] points by voxel, ascending within a voxel
+  int* start;     // [b][r3] segment start of each voxel (relative to its cloud)
+  int* tsum;      // [b][ntile] counts per scan tile
+  float* featT;   // [b][n][c] point-major copy of the features (nullptr: c == 0)
+  int ntile;
 };
 
-static int bits_for(uint64_t v) {  // bits needed to hold 0..v
-  int nb = 1;
-  while (nb < 64 && (v >> nb) != 0) nb++;
-  return nb;
-}
+constexpr int kBigScanThreads = 256;
+constexpr int kBigScanPer = 16;
+constexpr int kBigScanTile = kBigScanThreads * kBigScanPer;
 
 static size_t big_ws_layout(int b, int n, int r, BigVoxWs* ws, void* base, int c = 0) {
   const int64_t r3 = (int64_t)r * r * r;
   const size_t nk = (size_t)b * n, nr = (size_t)b * r3;
-  const int pb = bits_for((uint64_t)(n - 1)), vb = bits_for((uint64_t)r3),
-            cb = bits_for((uint64_t)(b > 1 ? b - 1 : 1));
-  size_t s1 = 0, s2 = 0;
-  (void)hipcub::DeviceRadixSort::SortKeys(nullptr, s1, (unsigned long long*)nullptr,
-                                          (unsigned long long*)nullptr, (int)nk, 0, pb + vb + cb);
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, s2, (int*)nullptr, (int*)nullptr, (int)nr);
+  const int ntile = (int)((r3 + kBigScanTile - 1) / kBigScanTile);
   size_t off = 0;
   char* p = (char*)base;
   auto take = [&](size_t bytes) {
@@ -1329,22 +1323,20 @@ static size_t big_ws_layout(int b, int n, int r, BigVoxWs* ws, void* base, int c
     off = align_up(off + bytes, 256);
     return q;
   };
-  auto* ki = (unsigned long long*)take(nk * 8);
-  auto* ko = (unsigned long long*)take(nk * 8);
-  int* scan = (int*)take(nr * 4);
-  const size_t tb = s1 > s2 ? s1 : s2;
-  void* temp = take(tb);
+  int* slot = (int*)take(nk * 4);
+  int* perm_u = (int*)take(nk * 4);
+  int* perm = (int*)take(nk * 4);
+  int* start = (int*)take(nr * 4);
+  int* tsum = (int*)take((size_t)b * ntile * 4);
   float* ft = c > 0 ? (float*)take(nk * (size_t)c * 4) : nullptr;
   if (ws) {
+    ws->slot = slot;
+    ws->perm_u = perm_u;
+    ws->perm = perm;
+    ws->start = start;
+    ws->tsum = tsum;
     ws->featT = ft;
-    ws->keys_in = ki;
-    ws->keys_out = ko;
-    ws->scan = scan;
-    ws->temp = temp;
-    ws->temp_bytes = tb;
-    ws->pb = pb;
-    ws->vb = vb;
-    ws->end_bit = pb + vb + cb;
+    ws->ntile = ntile;
   }
   return off;
 }
@@ -1352,10 +1344,9 @@ static size_t big_ws_layout(int b, int n, int r, BigVoxWs* ws, void* base, int c
 template <int MODE>
 __global__ __launch_bounds__(256) void vox_key_big_kernel(const float* __restrict__ coords_f,
                                                           const int* __restrict__ coords_i, int n,
-                                                          int r, int pb, int vb,
-                                                          int* __restrict__ ind,
+                                                          int r, int* __restrict__ ind,
                                                           int* __restrict__ cnt,
-                                                          unsigned long long* __restrict__ keys) {
+                                                          int* __restrict__ slot) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   const int b = blockIdx.y;
   if (i >= n) return;
@@ -1372,24 +1363,112 @@ __global__ __launch_bounds__(256) void vox_key_big_kernel(const float* __restric
     valid = v >= 0;
   }
   ind[(size_t)b * n + i] = v;
-  if (valid) atomicAdd(&cnt[(size_t)b * r3 + v], 1);
-  const unsigned long long vv = (unsigned long long)(valid ? v : r3);
-  keys[(size_t)b * n + i] = ((unsigned long long)b << (pb + vb)) | (vv << pb) | (unsigned)i;
+  slot[(size_t)b * n + i] = valid ? atomicAdd(&cnt[(size_t)b * r3 + v], 1) : -1;
 }
 
-// one thread per voxel: its segment of the sorted keys, summed per channel
+// per-cloud exclusive scan of the voxel counts, pass 1: each tile's total
+__global__ __launch_bounds__(kBigScanThreads) void vox_scan_tiles_kernel(
+    const int* __restrict__ cnt, int r3, int ntile, int* __restrict__ tsum) {
+  __shared__ int red[kBigScanThreads / kWave];
+  const int t = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int* C = cnt + (size_t)b * r3 + (size_t)t * kBigScanTile;
+  const int lim = min(kBigScanTile, r3 - t * kBigScanTile);
+  int s = 0;
+#pragma unroll
+  for (int e = 0; e < kBigScanPer; e++) {
+    const int v = e * kBigScanThreads + tid;
+    s += v < lim ? C[v] : 0;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, kWave);
+  if ((tid & 63) == 0) red[tid >> 6] = s;
+  __syncthreads();
+  if (tid == 0) {
+    int tot = 0;
+    for (int w = 0; w < kBigScanThreads / kWave; w++) tot += red[w];
+    tsum[(size_t)b * ntile + t] = tot;
+  }
+}
+
+// pass 2: each tile adds the totals of the tiles before it (in order) and
+// scans its counts; thread t owns kBigScanPer consecutive voxels
+__global__ __launch_bounds__(kBigScanThreads) void vox_scan_apply_kernel(
+    const int* __restrict__ cnt, int r3, int ntile, const int* __restrict__ tsum,
+    int* __restrict__ start) {
+  __shared__ int scan_s[kBigScanThreads / kWave + 1];
+  __shared__ int base_s;
+  const int t = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  if (tid < 64) {
+    int s = 0;
+    for (int q = tid; q < t; q += 64) s += tsum[(size_t)b * ntile + q];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, kWave);
+    if (tid == 0) base_s = s;
+  }
+  const int v0 = t * kBigScanTile + tid * kBigScanPer;
+  const int* C = cnt + (size_t)b * r3;
+  int c[kBigScanPer], sum = 0;
+#pragma unroll
+  for (int e = 0; e < kBigScanPer; e++) {
+    c[e] = v0 + e < r3 ? C[v0 + e] : 0;
+    sum += c[e];
+  }
+  const int incl = block_inclusive_scan(sum, scan_s);  // its barriers also publish base_s
+  int run = base_s + incl - sum;
+  int* S = start + (size_t)b * r3;
+#pragma unroll
+  for (int e = 0; e < kBigScanPer; e++) {
+    if (v0 + e < r3) S[v0 + e] = run;
+    run += c[e];
+  }
+}
+
+// every point at its voxel's start + arrival slot
+__global__ __launch_bounds__(256) void vox_place_big_kernel(const int* __restrict__ ind,
+                                                            const int* __restrict__ slot, int n,
+                                                            int r3, const int* __restrict__ start,
+                                                            int* __restrict__ perm_u) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (i >= n) return;
+  const int sl = slot[(size_t)b * n + i];
+  if (sl < 0) return;
+  const int v = ind[(size_t)b * n + i];
+  perm_u[(size_t)b * n + start[(size_t)b * r3 + v] + sl] = i;
+}
+
+// every point's final place: its rank by point id within its voxel's segment
+// (m reads for a voxel of m points; one-point voxels copy)
+__global__ __launch_bounds__(256) void vox_rank_big_kernel(const int* __restrict__ ind,
+                                                           const int* __restrict__ slot, int n,
+                                                           int r3, const int* __restrict__ cnt,
+                                                           const int* __restrict__ start,
+                                                           const int* __restrict__ perm_u,
+                                                           int* __restrict__ perm) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (i >= n) return;
+  if (slot[(size_t)b * n + i] < 0) return;
+  const int v = ind[(size_t)b * n + i];
+  const size_t vi = (size_t)b * r3 + v;
+  const int m = cnt[vi];
+  const int* seg = perm_u + (size_t)b * n + start[vi];
+  int rank = 0;
+  for (int x = 0; x < m; x++) rank += seg[x] < i ? 1 : 0;
+  perm[(size_t)b * n + start[vi] + rank] = i;
+}
+
+// one thread per voxel: its segment of the sorted points, summed per channel
 // in ascending point order (acc += f * inv, the product rounded first)
 __global__ __launch_bounds__(256) void vox_gather_big_kernel(
-    const float* __restrict__ feat, const int* __restrict__ cnt, const int* __restrict__ scan,
-    const unsigned long long* __restrict__ keys, int c, int n, int r3, int pb,
-    float* __restrict__ out) {
+    const float* __restrict__ feat, const int* __restrict__ cnt, const int* __restrict__ start,
+    const int* __restrict__ perm, int c, int n, int r3, float* __restrict__ out) {
   const int v = blockIdx.x * blockDim.x + threadIdx.x;
   const int b = blockIdx.y;
   if (v >= r3) return;
   const size_t vi = (size_t)b * r3 + v;
   const int m = cnt[vi];
-  const size_t start = (size_t)b * n + (size_t)(scan[vi] - scan[(size_t)b * r3]);
-  const unsigned long long pmask = (1ull << pb) - 1;
+  const int* P = perm + (size_t)b * n + start[vi];
   const float* F = feat + (size_t)b * c * n;
   float* O = out + (size_t)b * c * r3 + v;
   if (m == 0) {
@@ -1400,14 +1479,14 @@ __global__ __launch_bounds__(256) void vox_gather_big_kernel(
   constexpr int kHold = 8;
   int pts[kHold];
 #pragma unroll
-  for (int s = 0; s < kHold; s++) pts[s] = s < m ? (int)(keys[start + s] & pmask) : 0;
+  for (int s = 0; s < kHold; s++) pts[s] = s < m ? P[s] : 0;
   for (int ch = 0; ch < c; ch++) {
     const float* f = F + (size_t)ch * n;
     float acc = 0.0f;
 #pragma unroll
     for (int s = 0; s < kHold; s++)
       if (s < m) acc += f[pts[s]] * inv;
-    for (int s = kHold; s < m; s++) acc += f[(int)(keys[start + s] & pmask)] * inv;
+    for (int s = kHold; s < m; s++) acc += f[P[s]] * inv;
     O[(size_t)ch * r3] = acc;
   }
 }
@@ -1491,23 +1570,21 @@ __global__ __launch_bounds__(256) void feat_transpose_kernel(const float* __rest
 // consecutive channels (64 B) at a time instead of 16 scattered lines
 template <int CH>
 __global__ __launch_bounds__(256) void vox_gather_big_t_kernel(
-    const float* __restrict__ featT, const int* __restrict__ cnt, const int* __restrict__ scan,
-    const unsigned long long* __restrict__ keys, int c, int n, int r3, int pb,
-    float* __restrict__ out) {
+    const float* __restrict__ featT, const int* __restrict__ cnt, const int* __restrict__ start,
+    const int* __restrict__ perm, int c, int n, int r3, float* __restrict__ out) {
   const int v = blockIdx.x * blockDim.x + threadIdx.x;
   const int b = blockIdx.y;
   if (v >= r3) return;
   const size_t vi = (size_t)b * r3 + v;
   const int m = cnt[vi];
   float* O = out + (size_t)b * c * r3 + v;
-  const size_t start = (size_t)b * n + (size_t)(m > 0 ? scan[vi] - scan[(size_t)b * r3] : 0);
-  const unsigned long long pmask = (1ull << pb) - 1;
+  const int* P = perm + (size_t)b * n + (m > 0 ? start[vi] : 0);
   const float* FT = featT + (size_t)b * n * c;
   const float inv = m > 0 ? pcr_inv_count(m) : 0.0f;
   constexpr int kHold = 4;  // the first points' rows, read once for every chunk
   const float* rows[kHold];
 #pragma unroll
-  for (int s = 0; s < kHold; s++) rows[s] = s < m ? FT + (size_t)(keys[start + s] & pmask) * c : FT;
+  for (int s = 0; s < kHold; s++) rows[s] = s < m ? FT + (size_t)P[s] * c : FT;
   const bool vec = (c & 3) == 0;
   // every lane runs the same chunk loop and stores (empty voxels add nothing
   // and store zeros), so the stores stay whole-wave and coalesced
@@ -1530,7 +1607,7 @@ __global__ __launch_bounds__(256) void vox_gather_big_t_kernel(
         }
       }
       for (int s = kHold; s < m; s++) {
-        const float* row = FT + (size_t)(keys[start + s] & pmask) * c + c0;
+        const float* row = FT + (size_t)P[s] * c + c0;
 #pragma unroll
         for (int q = 0; q < CH; q += 4) {
           const float4 x = *reinterpret_cast<const float4*>(row + q);
@@ -1542,7 +1619,7 @@ __global__ __launch_bounds__(256) void vox_gather_big_t_kernel(
       }
     } else {
       for (int s = 0; s < m; s++) {
-        const float* row = FT + (size_t)(keys[start + s] & pmask) * c + c0;
+        const float* row = FT + (size_t)P[s] * c + c0;
 #pragma unroll
         for (int q = 0; q < CH; q++)
           if (c0 + q < c) acc[q] += row[q] * inv;
@@ -1569,36 +1646,33 @@ static pcr_status run_voxelize_big(const float* features, const float* coords_f,
   // else the direct one (same results)
   size_t need = big_ws_layout(b, n, r, &ws, workspace, c);
   if (workspace == nullptr || ws_bytes < need) need = big_ws_layout(b, n, r, &ws, workspace, 0);
-  PCR_REQUIRE(ws.end_bit <= 64, "%s: key does not fit 64 bits", name);
   PCR_REQUIRE(workspace != nullptr && ws_bytes >= need, "%s: workspace too small (%zu < %zu)",
               name, ws_bytes, need);
   if (hipMemsetAsync(cnt, 0, (size_t)b * r3 * sizeof(int), stream) != hipSuccess) {
     set_error("%s: memset failed", name);
     return PCR_ERR_LAUNCH;
   }
-  hipLaunchKernelGGL(vox_key_big_kernel<MODE>, dim3(ceil_div(n, 256), b), dim3(256), 0, stream,
-                     coords_f, coords_i, n, r, ws.pb, ws.vb, ind, cnt, ws.keys_in);
+  const dim3 pts(ceil_div(n, 256), b);
+  hipLaunchKernelGGL(vox_key_big_kernel<MODE>, pts, dim3(256), 0, stream, coords_f, coords_i, n,
+                     r, ind, cnt, ws.slot);
   if (c > 0 && out) {
-    size_t tb = ws.temp_bytes;
-    if (hipcub::DeviceRadixSort::SortKeys(ws.temp, tb, ws.keys_in, ws.keys_out, b * n, 0,
-                                          ws.end_bit, stream) != hipSuccess) {
-      set_error("%s: radix sort failed", name);
-      return PCR_ERR_LAUNCH;
-    }
-    tb = ws.temp_bytes;
-    if (hipcub::DeviceScan::ExclusiveSum(ws.temp, tb, cnt, ws.scan, b * r3, stream) !=
-        hipSuccess) {
-      set_error("%s: count scan failed", name);
-      return PCR_ERR_LAUNCH;
-    }
+    const dim3 tiles(ws.ntile, b);
+    hipLaunchKernelGGL(vox_scan_tiles_kernel, tiles, dim3(kBigScanThreads), 0, stream, cnt, r3,
+                       ws.ntile, ws.tsum);
+    hipLaunchKernelGGL(vox_scan_apply_kernel, tiles, dim3(kBigScanThreads), 0, stream, cnt, r3,
+                       ws.ntile, ws.tsum, ws.start);
+    hipLaunchKernelGGL(vox_place_big_kernel, pts, dim3(256), 0, stream, ind, ws.slot, n, r3,
+                       ws.start, ws.perm_u);
+    hipLaunchKernelGGL(vox_rank_big_kernel, pts, dim3(256), 0, stream, ind, ws.slot, n, r3, cnt,
+                       ws.start, ws.perm_u, ws.perm);
     if (ws.featT) {
       hipLaunchKernelGGL(feat_transpose_kernel, dim3(ceil_div(n, 64), ceil_div(c, 64), b),
                          dim3(256), 0, stream, features, c, n, ws.featT);
       hipLaunchKernelGGL(vox_gather_big_t_kernel<32>, dim3(ceil_div(r3, 256), b), dim3(256), 0,
-                         stream, ws.featT, cnt, ws.scan, ws.keys_out, c, n, r3, ws.pb, out);
+                         stream, ws.featT, cnt, ws.start, ws.perm, c, n, r3, out);
     } else {
       hipLaunchKernelGGL(vox_gather_big_kernel, dim3(ceil_div(r3, 256), b), dim3(256), 0, stream,
-                         features, cnt, ws.scan, ws.keys_out, c, n, r3, ws.pb, out);
+                         features, cnt, ws.start, ws.perm, c, n, r3, out);
     }
   }
   return launch_status(name);

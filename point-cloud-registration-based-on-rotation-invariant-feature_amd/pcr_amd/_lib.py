@@ -25,6 +25,8 @@ SIGNATURES = {
     "pcr_knn_forward": (ST, [P, P, I, I, I, I, I, P, P, P, P, P, SZ, P]),
     "pcr_knn_workspace_size": (SZ, [I, I, I]),
     "pcr_knn_backward": (ST, [P, P, P, P, P, P, I, I, I, I, I, P, P, P]),
+    "pcr_knn_backward_workspace_size": (SZ, [I, I, I, I]),
+    "pcr_knn_backward_ws": (ST, [P, P, P, P, P, P, I, I, I, I, I, P, P, P, SZ, P]),
     "pcr_spherical_ppf_forward": (ST, [P, P, P, P, I, I, P, P]),
     "pcr_local_ppf_forward": (ST, [P, P, P, P, P, I, I, I, I, I, I, P, P]),
     "pcr_knn_local_ppf": (ST, [P, P, I, I, I, I, P, P, P, P, SZ, P]),

@@ -90,9 +90,15 @@ def knn_backward_cuda(xyz1, xyz2, graddist1, graddist2, idx1, idx2):
     k = idx1.shape[1]
     g1 = torch.empty((b, c, n), dtype=torch.float32, device=xyz1.device)
     g2 = torch.empty((b, c, m), dtype=torch.float32, device=xyz1.device)
-    _lib.check(_lib.load().pcr_knn_backward(
+    # the atomics-free path: (query, slot) pairs counting-sorted by neighbour
+    # in a workspace, then one gather per point (bit-repeatable)
+    lib = _lib.load()
+    ws = torch.empty(lib.pcr_knn_backward_workspace_size(b, n, m, k), dtype=torch.uint8,
+                     device=xyz1.device)
+    _lib.check(lib.pcr_knn_backward_ws(
         _ptr(xyz1), _ptr(xyz2), _ptr(graddist1), _ptr(graddist2), _ptr(idx1), _ptr(idx2),
-        b, c, n, m, k, _ptr(g1), _ptr(g2), _stream()), "knn_backward_cuda")
+        b, c, n, m, k, _ptr(g1), _ptr(g2), _ptr(ws), ws.numel(), _stream()),
+        "knn_backward_cuda")
     return [g1, g2]
 
 

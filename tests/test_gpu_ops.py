@@ -227,6 +227,38 @@ def test_knn_backward_c2_shape(dev, self_knn):
     assert_within_sum_order(N(g2), e2, b2)
 
 
+def test_knn_backward_gather_repeatable_and_entry_points(dev):
+    """The atomics-free KNN backward (pcr_knn_backward_ws: pairs counting-
+    sorted by neighbour, one gather per point) is bit-identical run to run,
+    and both it and the atomic entry point (pcr_knn_backward) stay within the
+    sum-order bound at the c2 shape, with unequal clouds (n != m) and the
+    reference's 2 gd >= 20000 skip."""
+    from pcr_amd import _lib, ops
+    from pcr_amd.ops import _ptr, _stream
+    b, n, m, k = 4, 1024, 900, 32
+    x1, _, _ = gaussian_clouds(b, n, seed=24)
+    x2, _, _ = gaussian_clouds(b, m, seed=25)
+    _, _, i1, i2 = oracle.knn_forward(x1, x2, k)
+    rng = np.random.default_rng(26)
+    gd1 = rng.standard_normal((b, k, n)).astype(np.float32)
+    gd2 = rng.standard_normal((b, k, m)).astype(np.float32)
+    gd1[:, 7, ::3] = 10000.0
+    args = [T(a, dev) for a in (x1, x2, gd1, gd2, i1, i2)]
+    runs = [ops.knn_backward_cuda(*args) for _ in range(3)]
+    for g in runs[1:]:
+        assert torch.equal(g[0], runs[0][0]) and torch.equal(g[1], runs[0][1])
+    e1, e2 = oracle.knn_backward(x1, x2, gd1, gd2, i1, i2)
+    b1, b2 = knn_backward_bound(x1, x2, gd1, gd2, i1, i2)
+    assert_within_sum_order(N(runs[0][0]), e1, b1)
+    assert_within_sum_order(N(runs[0][1]), e2, b2)
+    g1 = torch.full((b, 3, n), float("nan"), device=dev)
+    g2 = torch.full((b, 3, m), float("nan"), device=dev)
+    _lib.check(_lib.load().pcr_knn_backward(*[_ptr(a) for a in args], b, 3, n, m, k, _ptr(g1),
+                                            _ptr(g2), _stream()), "knn_backward")
+    assert_within_sum_order(N(g1), e1, b1)
+    assert_within_sum_order(N(g2), e2, b2)
+
+
 # ------------------------------------------------ ball query / grouping / PPF
 def test_ball_query_grouping(dev):
     from pcr_amd import ops
