@@ -479,7 +479,8 @@ class C3Workload:
             res = self._backward(out, self.ev[s] if timed else None)
             if keep is not None:
                 keep.append(({kk: v.clone() for kk, v in out.items()}, res))
-        self.ex.pipelined_steps(steps, lambda s: self.inputs, consume)
+        self.ex.pipelined_steps(steps, lambda s: self.inputs, consume,
+                                select_events=self.sev if timed else None)
 
     def verify(self):
         """Three pipelined steps vs the serial forward + backwards: every
@@ -511,6 +512,9 @@ class C3Workload:
     def prepare_timing(self):
         self.ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                    for _ in range(self.args.steps)]
+        # the KNN selection launch of every step, on the neighbour stream
+        self.sev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                    for _ in range(self.args.steps)]
 
     def run(self, steps, timed):
         # the extractor's stage kernels from Python (pipelined: the split
@@ -525,17 +529,41 @@ class C3Workload:
         return steps
 
     def kernel_report(self):
-        ms = [a.elapsed_time(b) for a, b in self.ev[:self.timed_steps]] \
-            if not self.args.no_kernel_timing else []
+        """The step's dominant kernel by in-step duration (HIP events on the
+        stream each runs on): the KNN selection (VALU, priced at the
+        brute-force-equivalent 9 N^2 fp32 operations per cloud, SURVEY.md
+        8d) or the spherical devox backward (HBM); the other one is listed
+        beside it."""
+        a = self.args
+        if a.no_kernel_timing:
+            return None, None
+        ms = [x.elapsed_time(y) for x, y in self.ev[:self.timed_steps]]
         avg = sum(ms) / len(ms) if ms else float("nan")
         gbs = self.devox_bwd_bytes / (avg * 1e-3) / 1e9
-        return None, {
+        devox = {
             "name": "spherical devoxelize backward (pcr_devoxelize_backward_ws: corner-set "
                     "order + gather, dense gradient grid written once)",
             "bound": "hbm", "avg_ms_in_step": round(avg, 5), "launches_timed": len(ms),
             "bytes_per_launch": self.devox_bwd_bytes, "achieved": round(gbs, 1),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
             "traffic": None}
+        sms = [x.elapsed_time(y) for x, y in self.sev[:self.timed_steps]]
+        if c3_selection_timed(sms):
+            savg = sum(sms) / len(sms)
+            ops = 9.0 * a.points * a.points * a.batch
+            tf = ops / (savg * 1e-3) / 1e12
+            sel = {"name": "knn_select_kernel (threshold selection, k=%d, %d-point LDS-cached "
+                           "candidates; pcr_knn_select_sorted)" % (a.k, a.points),
+                   "bound": "valu", "avg_ms_in_step": round(savg, 5),
+                   "launches_timed": len(sms), "fp32_ops_per_launch": ops,
+                   "ops_model": "brute-force-equivalent 9 N^2 per cloud (SURVEY.md 8d)",
+                   "achieved": round(tf, 3), "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                   "frac": round(tf / VALU_PEAK_TFLOPS, 4), "traffic": None}
+            if savg >= avg:
+                sel["other_kernels"] = [devox]
+                return None, sel
+            devox["other_kernels"] = [sel]
+        return None, devox
 
     def config(self):
         a = self.args
@@ -548,6 +576,12 @@ class C3Workload:
                 "global_batch": a.batch * self.world,
                 "parallelism": "dp%d (clouds sharded, no collective)" % self.world,
                 "schedule": a.c3_schedule}
+
+
+def c3_selection_timed(ms):
+    """True when the selection events of the timed steps were recorded (the
+    sorted-rows path ran; other shapes fall back without them)."""
+    return bool(ms) and all(t > 0 for t in ms)
 
 
 class C5Workload:

@@ -127,6 +127,15 @@ pcr_status pcr_knn_local_ppf_prepared(const float *xyz, const float *normals, in
 pcr_status pcr_knn_select_ppf(const float *xyz, const float *normals, int b, int n, int k,
                               int relative, int *idx, float *ppf, const void *workspace,
                               size_t workspace_bytes, void *stream);
+/* The two launches of pcr_knn_select_ppf separately: the selection into the
+ * workspace's sorted-order rows (PCR_ERR_UNSUPPORTED, nothing launched, when
+ * that path does not apply), then the PPF launch that writes knn_idx and
+ * ppf from them (k <= 32, n <= 2048). */
+pcr_status pcr_knn_select_sorted(const float *xyz, int b, int n, int k, const void *workspace,
+                                 size_t workspace_bytes, void *stream);
+pcr_status pcr_knn_ppf_sorted(const float *xyz, const float *normals, int b, int n, int k,
+                              int relative, int *idx, float *ppf, const void *workspace,
+                              size_t workspace_bytes, void *stream);
 
 /* ------------------------------------------------ ball query / grouping --
  * ball_query (ball_query/ball_query.cpp:6-30, kernel ball_query.cu:19-50):

@@ -949,6 +949,55 @@ extern "C" pcr_status pcr_knn_local_ppf_prepared(const float* xyz, const float* 
 // order together with the PPF [b,4,k,n].  Shapes outside that path (k > 32,
 // clouds of more than 2048 points, no sorted views) take the two calls it
 // replaces, with the same outputs.
+// The two launches of pcr_knn_select_ppf as entry points of their own (the
+// c3 bench times the selection in step between them).  select_sorted returns
+// PCR_ERR_UNSUPPORTED, launching nothing, when the sorted-rows path does not
+// apply (k > 32, clouds of more than 2048 points, no sorted views).
+extern "C" pcr_status pcr_knn_select_sorted(const float* xyz, int b, int n, int k,
+                                            const void* workspace, size_t workspace_bytes,
+                                            void* stream) {
+  PCR_REQUIRE(b >= 0 && n >= 1 && k >= 1 && k <= 128, "knn_select_sorted: invalid sizes");
+  if (b == 0) return PCR_OK;
+  const int* sidx = nullptr;
+  const int* inv = nullptr;
+  int npad = 0;
+  if (workspace == nullptr || n > kPpfSelfMaxN ||
+      !knn_sorted_views(const_cast<void*>(workspace), b, n, &sidx, &inv, &npad))
+    return PCR_ERR_UNSUPPORTED;
+  return knn_spatial(xyz, xyz, b, n, n, k, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                     0, nullptr, const_cast<void*>(workspace), workspace_bytes, true,
+                     as_stream(stream), 2 | 4);
+}
+
+extern "C" pcr_status pcr_knn_ppf_sorted(const float* xyz, const float* normals, int b, int n,
+                                         int k, int relative, int* idx, float* ppf,
+                                         const void* workspace, size_t workspace_bytes,
+                                         void* stream) {
+  PCR_REQUIRE(b >= 0 && n >= 1 && k >= 1 && k <= kKnnSortedK && n <= kPpfSelfMaxN,
+              "knn_ppf_sorted: invalid sizes (k <= 32, n <= 2048)");
+  PCR_REQUIRE(idx != nullptr && ppf != nullptr, "knn_ppf_sorted: idx and ppf required");
+  if (b == 0) return PCR_OK;
+  const int* sidx = nullptr;
+  const int* inv = nullptr;
+  int npad = 0;
+  PCR_REQUIRE(workspace != nullptr && workspace_bytes >= pcr_knn_workspace_size(b, n, n) &&
+                  knn_sorted_views(const_cast<void*>(workspace), b, n, &sidx, &inv, &npad),
+              "knn_ppf_sorted: workspace without sorted neighbour rows");
+  constexpr int SL = 4;
+  const size_t lds = ((size_t)6 * n + (size_t)SL * npad) * 4;
+  allow_big_lds(local_ppf_cloud_kernel<SL>, lds);
+  hipLaunchKernelGGL((local_ppf_cloud_kernel<SL>), dim3(b * ceil_div(k, SL)), dim3(512), lds,
+                     as_stream(stream), xyz, normals, n, k, relative, ppf, sidx, inv, npad, idx);
+  return launch_status("knn_ppf_sorted");
+}
+
+// Selection + local PPF of a prepared (sorted) workspace with the neighbour
+// ids passed in sorted query order (knn_spatial stage 4): the selection
+// writes whole rows of the workspace, the PPF kernel reads them back through
+// the sort's inverse permutation and writes knn_idx [b,k,n] in original
+// order together with the PPF [b,4,k,n].  Shapes outside that path (k > 32,
+// clouds of more than 2048 points, no sorted views) take the two calls it
+// replaces, with the same outputs.
 extern "C" pcr_status pcr_knn_select_ppf(const float* xyz, const float* normals, int b, int n,
                                          int k, int relative, int* idx, float* ppf,
                                          const void* workspace, size_t workspace_bytes,
@@ -956,24 +1005,10 @@ extern "C" pcr_status pcr_knn_select_ppf(const float* xyz, const float* normals,
   PCR_REQUIRE(b >= 0 && n >= 1 && k >= 1 && k <= 128, "knn_select_ppf: invalid sizes (k<=128)");
   PCR_REQUIRE(idx != nullptr && ppf != nullptr, "knn_select_ppf: idx and ppf required");
   if (b == 0) return PCR_OK;
-  hipStream_t st = as_stream(stream);
-  const int* sidx = nullptr;
-  const int* inv = nullptr;
-  int npad = 0;
-  // (knn_spatial checks the workspace size before launching anything)
-  const bool views = workspace != nullptr &&
-                     knn_sorted_views(const_cast<void*>(workspace), b, n, &sidx, &inv, &npad);
-  if (views && n <= kPpfSelfMaxN &&
-      knn_spatial(xyz, xyz, b, n, n, k, nullptr, idx, nullptr, nullptr, nullptr, nullptr, 0,
-                  nullptr, const_cast<void*>(workspace), workspace_bytes, true, st, 2 | 4) ==
-          PCR_OK) {
-    constexpr int SL = 4;
-    const size_t lds = ((size_t)6 * n + (size_t)SL * npad) * 4;
-    allow_big_lds(local_ppf_cloud_kernel<SL>, lds);
-    hipLaunchKernelGGL((local_ppf_cloud_kernel<SL>), dim3(b * ceil_div(k, SL)), dim3(512), lds,
-                       st, xyz, normals, n, k, relative, ppf, sidx, inv, npad, idx);
-    return launch_status("knn_select_ppf");
-  }
+  const pcr_status rs = pcr_knn_select_sorted(xyz, b, n, k, workspace, workspace_bytes, stream);
+  if (rs == PCR_OK)
+    return pcr_knn_ppf_sorted(xyz, normals, b, n, k, relative, idx, ppf, workspace,
+                              workspace_bytes, stream);
   const pcr_status rc = pcr_knn_local_ppf_prepared(xyz, normals, b, n, k, relative, idx, nullptr,
                                                    nullptr, workspace, workspace_bytes, stream);
   if (rc != PCR_OK) return rc;

@@ -33,6 +33,8 @@ SIGNATURES = {
     "pcr_knn_prepare": (ST, [P, I, I, P, SZ, P]),
     "pcr_knn_local_ppf_prepared": (ST, [P, P, I, I, I, I, P, P, P, P, SZ, P]),
     "pcr_knn_select_ppf": (ST, [P, P, I, I, I, I, P, P, P, SZ, P]),
+    "pcr_knn_select_sorted": (ST, [P, I, I, I, P, SZ, P]),
+    "pcr_knn_ppf_sorted": (ST, [P, P, I, I, I, I, P, P, P, SZ, P]),
     "pcr_ball_query": (ST, [P, P, I, I, I, F, I, P, P]),
     "pcr_grouping_forward": (ST, [P, P, I, I, I, I, I, P, P]),
     "pcr_grouping_backward": (ST, [P, P, I, I, I, I, I, P, P]),

@@ -119,10 +119,17 @@ class SphExtractor:
         _lib.check(rc, "knn_prepare")
         return True
 
-    def knn_select(self, xyz, normals, stream, slot=0, sorted_ok=True, ppf=True):
-        """Selection (+ local PPF unless ppf=False) into index set `slot`."""
+    def knn_select(self, xyz, normals, stream, slot=0, sorted_ok=True, ppf=True, events=None):
+        """Selection (+ local PPF unless ppf=False) into index set `slot`.
+        events: (ev0, ev1) torch.cuda.Events recorded on `stream` (a
+        torch.cuda.Stream) around the selection launch alone."""
         kws, idx = self._set(slot)[0], self._set(slot)[4]
         ppf_out = self._ppf(slot)
+        torch_stream = stream if isinstance(stream, torch.cuda.Stream) else None
+        if torch_stream is not None:
+            stream = torch_stream.cuda_stream
+        if torch_stream is None:
+            events = None  # events are recorded on a torch.cuda.Stream
         if not sorted_ok:
             _lib.check(_lib.load().pcr_knn_local_ppf(
                 _ptr(xyz), _ptr(normals), self.b, self.n, self.k, int(self.relative),
@@ -130,6 +137,21 @@ class SphExtractor:
                 kws.numel(), stream), "knn_local_ppf")
             return
         lib = _lib.load()
+        if self.split_ppf and ppf and self.knn_dist is None and events is not None:
+            # the same two launches with timing events around the selection
+            ev0, ev1 = events
+            ev0.record(torch_stream)
+            rs = lib.pcr_knn_select_sorted(_ptr(xyz), self.b, self.n, self.k, _ptr(kws),
+                                           kws.numel(), stream)
+            ev1.record(torch_stream)
+            if rs == 0:
+                _lib.check(lib.pcr_knn_ppf_sorted(
+                    _ptr(xyz), _ptr(normals), self.b, self.n, self.k, int(self.relative),
+                    _ptr(idx), _ptr(ppf_out), _ptr(kws), kws.numel(), stream),
+                    "knn_ppf_sorted")
+                return
+            if rs != -3:  # PCR_ERR_UNSUPPORTED: nothing launched
+                _lib.check(rs, "knn_select_sorted")
         if self.split_ppf and ppf and self.knn_dist is None:
             # selection in sorted query order + the PPF launch that writes
             # knn_idx and the PPF (pcr_knn_select_ppf)
@@ -280,15 +302,17 @@ class SphExtractor:
         return self.outputs()
 
     # ------------------------------------------------- train-step pipeline
-    def enqueue_neighbors(self, xyz, normals, slot, after=None):
+    def enqueue_neighbors(self, xyz, normals, slot, after=None, events=None):
         """Self-KNN (Morton sort + selection) + local PPF of one batch on
         s_nbr into index set `slot` (its knn_idx / local_ppf).  `after`: an
         event recorded once the set's previous consumer is done with it.
-        Returns the event this batch's consumer waits on."""
+        events: (ev0, ev1) around the selection launch.  Returns the event
+        this batch's consumer waits on."""
         if after is not None:
             self.s_nbr.wait_event(after)
         sorted_ok = self.knn_sort(xyz, self.s_nbr.cuda_stream, slot)
-        self.knn_select(xyz, normals, self.s_nbr.cuda_stream, slot, sorted_ok)
+        self.knn_select(xyz, normals, self.s_nbr if events is not None else
+                        self.s_nbr.cuda_stream, slot, sorted_ok, events=events)
         ev = torch.cuda.Event()
         ev.record(self.s_nbr)
         return ev
@@ -314,7 +338,7 @@ class SphExtractor:
         else:
             self.voxel_devox(features, stream, desc, slot)
 
-    def pipelined_steps(self, steps, batch, consume):
+    def pipelined_steps(self, steps, batch, consume, select_events=None):
         """`steps` train steps whose neighbour side runs one batch ahead.
 
         A batch's self-KNN + local PPF depend on its coordinates and normals
@@ -337,7 +361,9 @@ class SphExtractor:
         stream right after it, so batch s+1's neighbours are ordered after
         its producers but not after consume(s) -- the overlap stays.  xyz and
         normals are record_stream'ed to s_nbr, so the caching allocator does
-        not hand their blocks out while s_nbr still reads them."""
+        not hand their blocks out while s_nbr still reads them.
+        select_events: optional list of (ev0, ev1) per step, recorded on s_nbr
+        around that step's selection launch (its in-step duration)."""
         cur = torch.cuda.current_stream(self.device)
         # set 1's buffers are made here, before s_nbr forks from the caller's
         # stream.  Made lazily inside the loop they could reuse a block the
@@ -364,7 +390,9 @@ class SphExtractor:
             self.s_nbr.wait_event(e_in)
             xyz.record_stream(self.s_nbr)
             normals.record_stream(self.s_nbr)
-            e_nbr = self.enqueue_neighbors(xyz, normals, q, after=done[q])
+            e_nbr = self.enqueue_neighbors(
+                xyz, normals, q, after=done[q],
+                events=select_events[s] if select_events is not None else None)
             self.enqueue_voxels(xyz, features, cur.cuda_stream, q)
             # the next batch is produced ahead of this step's consume
             nxt = fetch(s + 1) if s + 1 < steps else None

@@ -9,3 +9,5 @@ rc=$?; tail -4 gpurun_out/pt_b.log
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 timeout -k 10 300 python bench.py --workload c5 --no-cpu-baseline > gpurun_out/bench_c5.log 2>&1 || exit $?
 tail -1 gpurun_out/bench_c5.log
+timeout -k 10 400 python bench.py --workload c3 --no-cpu-baseline > gpurun_out/bench_c3.log 2>&1 || exit $?
+tail -1 gpurun_out/bench_c3.log
