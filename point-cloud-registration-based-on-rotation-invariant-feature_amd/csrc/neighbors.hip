@@ -495,6 +495,40 @@ __global__ __launch_bounds__(NT) void local_ppf_self_kernel(const float* __restr
   }
 }
 
+// Local PPF on the hardware's approximate reciprocal square root / square
+// root (v_rsq_f32, v_sqrt_f32, ~1 ulp) instead of IEEE divisions and
+// correctly rounded square roots: experiment build KNN_EXP == 21 only (the
+// product keeps pcr_local_ppf, bit-identical to the oracle)
+__device__ inline float acosf_hw(float x) {
+  const float pio2_hi = 1.57079637e+00f, pio2_lo = -4.37113883e-08f;
+  const float pi_hi = 3.14159274e+00f, pi_lo = -8.74227766e-08f;
+  const float ax = __builtin_fabsf(x);
+  const bool mid = ax <= 0.5f;
+  const float s = mid ? x : __builtin_amdgcn_sqrtf((1.0f - ax) * 0.5f);
+  const float p = pcr_asinf_core(s);
+  return mid ? pio2_hi - (p - pio2_lo) : (x > 0.0f ? 2.0f * p : pi_hi - (2.0f * p - pi_lo));
+}
+__device__ inline void local_ppf_hw(float cx, float cy, float cz, float cnx, float cny,
+                                    float cnz, float px, float py, float pz, float pnx,
+                                    float pny, float pnz, int relative, float out[4]) {
+  const float gx = relative ? px - cx : px;
+  const float gy = relative ? py - cy : py;
+  const float gz = relative ? pz - cz : pz;
+  const float dx = cx - gx, dy = cy - gy, dz = cz - gz;
+  const float d2 = pcr_sumsq3f(dx, dy, dz);
+  const float rn = __builtin_amdgcn_rsqf(d2);
+  const float ux = dx * rn, uy = dy * rn, uz = dz * rn;
+  out[0] = acosf_hw(pcr_clamp1f(pcr_dot3f(pnx, pny, pnz, ux, uy, uz)));
+  out[1] = acosf_hw(pcr_clamp1f(pcr_dot3f(cnx, cny, cnz, ux, uy, uz)));
+  out[2] = acosf_hw(pcr_clamp1f(pcr_dot3f(pnx, pny, pnz, cnx, cny, cnz)));
+  out[3] = __builtin_amdgcn_sqrtf(d2);
+}
+#if defined(KNN_EXP) && KNN_EXP == 21
+#define PCR_LOCAL_PPF_CLOUD local_ppf_hw
+#else
+#define PCR_LOCAL_PPF_CLOUD pcr_local_ppf
+#endif
+
 // The same local PPF from the selection's sorted-order id rows
 // (pcr_knn_select_ppf), one workgroup per (cloud, SL slots) covering every
 // point of the cloud: the cloud's coordinates + normals and the SL id rows
@@ -559,8 +593,8 @@ __global__ __launch_bounds__(NT) void local_ppf_cloud_kernel(const float* __rest
       I[(size_t)q * n + j] = jd;
       const unsigned si = (jd < 0 || jd >= n) ? 0u : (unsigned)jd;
       float o[4];
-      pcr_local_ppf(cx, cy, cz, cnx, cny, cnz, cl_s[si], cl_s[n + si], cl_s[2 * n + si],
-                    cl_s[3 * n + si], cl_s[4 * n + si], cl_s[5 * n + si], relative, o);
+      PCR_LOCAL_PPF_CLOUD(cx, cy, cz, cnx, cny, cnz, cl_s[si], cl_s[n + si], cl_s[2 * n + si],
+                          cl_s[3 * n + si], cl_s[4 * n + si], cl_s[5 * n + si], relative, o);
       // nontemporal: the PPF rows are streamed out
 #pragma unroll
       for (int ch = 0; ch < 4; ch++)
@@ -983,11 +1017,25 @@ extern "C" pcr_status pcr_knn_ppf_sorted(const float* xyz, const float* normals,
   PCR_REQUIRE(workspace != nullptr && workspace_bytes >= pcr_knn_workspace_size(b, n, n) &&
                   knn_sorted_views(const_cast<void*>(workspace), b, n, &sidx, &inv, &npad),
               "knn_ppf_sorted: workspace without sorted neighbour rows");
+#if defined(KNN_EXP) && KNN_EXP == 22
+  // A/B build: the per-256-point workgroups of local_ppf_self_kernel
+  hipLaunchKernelGGL((local_ppf_self_kernel<8>), dim3(ceil_div(n, 256), ceil_div(k, 8), b),
+                     dim3(256), (size_t)6 * n * 4, as_stream(stream), xyz, normals, nullptr, n, k,
+                     relative, ppf, sidx, inv, npad, idx);
+#elif defined(KNN_EXP) && KNN_EXP == 23
+  // A/B build: two slots per workgroup (LDS 64 KB at 2048 points)
+  constexpr int SL = 2;
+  const size_t lds = ((size_t)6 * n + (size_t)SL * npad) * 4;
+  allow_big_lds(local_ppf_cloud_kernel<SL>, lds);
+  hipLaunchKernelGGL((local_ppf_cloud_kernel<SL>), dim3(b * ceil_div(k, SL)), dim3(512), lds,
+                     as_stream(stream), xyz, normals, n, k, relative, ppf, sidx, inv, npad, idx);
+#else
   constexpr int SL = 4;
   const size_t lds = ((size_t)6 * n + (size_t)SL * npad) * 4;
   allow_big_lds(local_ppf_cloud_kernel<SL>, lds);
   hipLaunchKernelGGL((local_ppf_cloud_kernel<SL>), dim3(b * ceil_div(k, SL)), dim3(512), lds,
                      as_stream(stream), xyz, normals, n, k, relative, ppf, sidx, inv, npad, idx);
+#endif
   return launch_status("knn_ppf_sorted");
 }
 
