@@ -894,7 +894,9 @@ typedef __attribute__((address_space(1))) void* gbl_void_p;
 template <int N>
 __device__ inline void wait_vmcnt() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);  // compiler-only (the builtin is IntrNoMem)
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
 
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
