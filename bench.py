@@ -91,6 +91,9 @@ def parse(argv=None):
                          "batch ahead, overlapping the previous step's backwards "
                          "(SphExtractor.pipelined_steps); serial = forward (joined), then "
                          "the backwards")
+    ap.add_argument("--c3-cu-split", type=float, default=0.0,
+                    help="c3 diagnostic: run the neighbour stream on this fraction of the CUs "
+                         "and the caller's chain on the rest (CU-masked HIP streams); 0 = off")
     ap.add_argument("--steps-per-launch", type=int, default=40,
                     help="most pipelined steps per native runner call (extract / pairs); "
                          "--steps and --warmup are split into calls of at most this many")
@@ -443,6 +446,11 @@ class C3Workload:
         g = torch.Generator(device=dev).manual_seed(99 + rank)
         self.gy = torch.randn((b, c, n), generator=g, device=dev)
         self.ex = SphExtractor(b, n, c, k, r, device=dev)
+        self.main_stream = None
+        if args.c3_cu_split > 0:
+            nbr, main = cu_masked_streams(args.c3_cu_split, dev)
+            self.ex.s_nbr = nbr
+            self.main_stream = main
         fwd = algorithmic_bytes_per_cloud(n, k, r, c)["total"]
         # devox backward: upstream gradient 4CN + corner inds / wgts 64N in,
         # the dense gradient grid 4C r^3 out (written once); vox backward:
@@ -521,7 +529,15 @@ class C3Workload:
         # voxel stage -- means + devox, then the dense-grid stream -- on the
         # caller's stream, KNN + PPF one batch ahead on s_nbr)
         t = timed and not self.args.no_kernel_timing
-        if self.args.c3_schedule == "serial":
+        if self.main_stream is not None:
+            self.main_stream.wait_stream(torch.cuda.current_stream(self.dev))
+            with torch.cuda.stream(self.main_stream):
+                if self.args.c3_schedule == "serial":
+                    self._serial(steps, t)
+                else:
+                    self._pipelined(steps, t)
+            torch.cuda.current_stream(self.dev).wait_stream(self.main_stream)
+        elif self.args.c3_schedule == "serial":
             self._serial(steps, t)
         else:
             self._pipelined(steps, t)
@@ -575,13 +591,40 @@ class C3Workload:
                 "resolution": a.res, "channels": a.channels,
                 "global_batch": a.batch * self.world,
                 "parallelism": "dp%d (clouds sharded, no collective)" % self.world,
-                "schedule": a.c3_schedule}
+                "schedule": a.c3_schedule,
+                "cu_split": a.c3_cu_split or None}
 
 
 def c3_selection_timed(ms):
     """True when the selection events of the timed steps were recorded (the
     sorted-rows path ran; other shapes fall back without them)."""
     return bool(ms) and all(t > 0 for t in ms)
+
+
+def cu_masked_streams(frac, dev):
+    """Two HIP streams on complementary CU masks (hipExtStreamCreateWithCUMask
+    of the runtime torch loaded): `frac` of every 8 consecutive CU bits for
+    the first.  Returns torch ExternalStreams (diagnostic)."""
+    import ctypes
+    hip = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"))
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    words = (ncu + 31) // 32
+    take = max(1, min(7, int(round(frac * 8))))
+    a = (ctypes.c_uint32 * words)()
+    bm = (ctypes.c_uint32 * words)()
+    for cu in range(ncu):
+        if cu % 8 < take:
+            a[cu // 32] |= 1 << (cu % 32)
+        else:
+            bm[cu // 32] |= 1 << (cu % 32)
+    out = []
+    for mask in (a, bm):
+        st = ctypes.c_void_p()
+        rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(st), ctypes.c_uint32(words), mask)
+        if rc != 0:
+            raise SystemExit("bench: hipExtStreamCreateWithCUMask failed (%d)" % rc)
+        out.append(torch.cuda.ExternalStream(st.value, device=dev))
+    return out
 
 
 class C5Workload:
