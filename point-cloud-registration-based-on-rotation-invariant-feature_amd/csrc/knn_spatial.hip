@@ -429,6 +429,12 @@ __device__ inline kkey make_key(float d, int j) {
   return __longlong_as_double((long long)(((unsigned long long)(__float_as_uint(d) & 0x7FFFFFFFu)
                                            << 32) | (unsigned)j));
 }
+// a taken key (d below a finite cut: never NaN, and a sum of squares is
+// never negative) needs no sign clearing
+__device__ inline kkey make_key_finite(float d, int j) {
+  return __longlong_as_double(
+      (long long)(((unsigned long long)__float_as_uint(d) << 32) | (unsigned)j));
+}
 __device__ inline float key_dist(kkey k) {
   return __uint_as_float((unsigned)((unsigned long long)__double_as_longlong(k) >> 32));
 }
@@ -1400,7 +1406,7 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
           // exec-masked: only the taking lanes store (few lanes of a wave)
           if (take[h] && !(dbg & 16)) {
             const bool lo = __float_as_uint(d[h]) < ulo;
-            buf_s[(lo ? slot_lo : slot_cut) * kBlk + lane] = make_key(d[h], j4[h]);
+            buf_s[(lo ? slot_lo : slot_cut) * kBlk + lane] = make_key_finite(d[h], j4[h]);
             slot_lo += lo ? 1 : 0;
             slot_cut += lo ? 0 : 1;
           }
