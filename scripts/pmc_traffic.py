@@ -9,6 +9,7 @@ the bytes of a wide coalesced streaming read, so it is doubled; WRITE_SIZE is
 exact for 16-B-per-lane streaming stores (the grid kernel's float4 stores).
 Both counters are in KiB.
   usage: scripts/pmc_traffic.py <fetch_dir> <write_dir> <out.json> B N K R C
+                                [<rdreq_dir> <wrreq_dir>]
 """
 import csv
 import glob
@@ -21,11 +22,11 @@ KERNEL = os.environ.get("PCR_PMC_KERNEL", "vox_stream_kernel")
 
 
 # the kernels of one bench step (schedule 1): one launch each per step
-STEP_KERNELS = ("knn_sort_kernel", "knn_select_kernel", "local_ppf_self_kernel",
+STEP_KERNELS = ("knn_sort_kernel", "knn_select_kernel", "local_ppf_cloud_kernel",
                 "vox_prep_kernel", "vox_means_kernel", "vox_stream_kernel")
 
 
-def per_dispatch(d, counter, kernel=None):
+def per_dispatch(d, counter, kernel=None, missing_ok=False):
     kernel = kernel or KERNEL
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     if not files:
@@ -39,6 +40,8 @@ def per_dispatch(d, counter, kernel=None):
                 continue
             acc[row["Dispatch_Id"]] += float(row["Counter_Value"])
     if not acc:
+        if missing_ok:
+            return None
         raise SystemExit(f"no {counter} rows for {kernel} under {d}")
     return list(acc.values())
 
@@ -63,6 +66,20 @@ def main():
         kb = 2.0 * sum(kf) / len(kf) * 1024.0 + sum(kw) / len(kw) * 1024.0
         res["step_kernels"][kname] = kb
         res["step_hbm_bytes"] += kb
+    # optional request-count passes (TCC_EA0_RDREQ / _32B, TCC_EA0_WRREQ /
+    # _64B): per kernel and launch, the raw fabric request counts, which do
+    # not depend on the FETCH_SIZE width calibration
+    if len(sys.argv) > 10:
+        rd, wr = sys.argv[9], sys.argv[10]
+        reqs = {}
+        for kname in STEP_KERNELS:
+            row = {}
+            for d, cn in ((rd, "TCC_EA0_RDREQ_sum"), (rd, "TCC_EA0_RDREQ_32B_sum"),
+                          (wr, "TCC_EA0_WRREQ_sum"), (wr, "TCC_EA0_WRREQ_64B_sum")):
+                v = per_dispatch(d, cn, kname, missing_ok=True)
+                row[cn] = (sum(v) / len(v)) if v else None
+            reqs[kname] = row
+        res["ea_requests_per_launch"] = reqs
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps(res))
