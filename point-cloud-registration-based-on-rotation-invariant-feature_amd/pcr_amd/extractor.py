@@ -356,10 +356,11 @@ class SphExtractor:
 
         batch(s) may make its tensors on the caller's stream (an H2D copy as
         in train.py:140, an augmentation, the LRF change_coords): batch(s+1)
-        is called after step s's voxel side is enqueued and before its
-        consume, and s_nbr waits for an event recorded on the caller's
-        stream right after it, so batch s+1's neighbours are ordered after
-        its producers but not after consume(s) -- the overlap stays.  xyz and
+        is called right after step s's neighbours are enqueued, before step
+        s's voxel side and consume, and s_nbr waits for an event recorded on
+        the caller's stream right after it, so batch s+1's neighbours are
+        ordered after its producers but neither after step s's voxel side
+        nor after consume(s) -- the overlap stays.  xyz and
         normals are record_stream'ed to s_nbr, so the caching allocator does
         not hand their blocks out while s_nbr still reads them.
         select_events: optional list of (ev0, ev1) per step, recorded on s_nbr
@@ -393,9 +394,10 @@ class SphExtractor:
             e_nbr = self.enqueue_neighbors(
                 xyz, normals, q, after=done[q],
                 events=select_events[s] if select_events is not None else None)
-            self.enqueue_voxels(xyz, features, cur.cuda_stream, q)
-            # the next batch is produced ahead of this step's consume
+            # the next batch is produced ahead of this step's voxel side and
+            # consume (its neighbours wait for its producers only)
             nxt = fetch(s + 1) if s + 1 < steps else None
+            self.enqueue_voxels(xyz, features, cur.cuda_stream, q)
             cur.wait_event(e_nbr)
             consume(s, self.outputs(slot=q, idx_slot=q))
             ev = torch.cuda.Event()
