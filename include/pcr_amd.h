@@ -398,6 +398,10 @@ pcr_status pcr_read_xyzn_txt(const char *path, float *out, long long rows, int c
  *   schedule 2: as 1, with the Morton sort moved to s_pre (ahead of prep, into
  *               KNN workspace s % 2 after the selection of step s-2 read it),
  *               so s_nbr only selects and computes the local PPF.
+ *   schedule 3: as 1, with the local PPF of step s on `origin` (a fourth
+ *               stream) after the selection of step s, beside the sort +
+ *               selection of step s+1 on s_nbr (KNN workspace s % 2, reused
+ *               by step s+2 after that PPF read it).
  * Buffers with two entries are the alternating sets (schedule 0 uses set 0).
  * desc_steps: [steps][b][c] per-step descriptors, or NULL (then desc).
  *

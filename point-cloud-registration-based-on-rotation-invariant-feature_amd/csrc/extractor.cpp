@@ -15,7 +15,7 @@ namespace {
 // every pcr_extractor_run call.  A wait captures the event's most recent
 // record at the time it is enqueued, so re-recording across steps and calls
 // keeps the same ordering as fresh events.
-constexpr int kSyncEvents = 12;
+constexpr int kSyncEvents = 14;
 }  // namespace
 }  // namespace pcr
 
@@ -180,7 +180,7 @@ extern "C" pcr_status pcr_runner_grid_times(pcr_runner* rn, float* ms, int cap, 
 extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_args* a,
                                         int steps, int schedule, float* desc_steps, void* origin,
                                         void* s_nbr_p, void* s_pre_p, void* s_vox_p) {
-  PCR_REQUIRE(a != nullptr && steps >= 0 && schedule >= 0 && schedule <= 2,
+  PCR_REQUIRE(a != nullptr && steps >= 0 && schedule >= 0 && schedule <= 3,
               "extractor_run: invalid arguments");
   PCR_REQUIRE(a->b >= 0 && a->n >= 1 && a->c >= 1 && a->k >= 1 && a->r >= 1,
               "extractor_run: invalid sizes");
@@ -194,7 +194,7 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
   PCR_REQUIRE(a->nsets >= 0 && (a->nsets == 0 || (a->sets && schedule >= 1 && a->set0 >= 0)),
               "extractor_run: a batch ring needs sets, set0 >= 0 and schedule 1 or 2");
   for (int q = 0; q < nslots; q++)
-    PCR_REQUIRE(a->vox_ws[q] && a->knn_ws[schedule == 2 ? q : 0] &&
+    PCR_REQUIRE(a->vox_ws[q] && a->knn_ws[schedule >= 2 ? q : 0] &&
                     (a->nsets > 0 || (a->dinds[q] && a->dwgts[q])),
                 "extractor_run: buffer set %d missing", q);
   for (int t = 0; t < a->nsets; t++)
@@ -220,7 +220,7 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
   hipEvent_t* e = rn->sync;
   hipEvent_t fork = e[0], means_done[2] = {e[1], e[2]}, stream_done[2] = {e[3], e[4]},
              join[3] = {e[5], e[6], e[7]}, sort_done[2] = {e[8], e[9]},
-             sel_done[2] = {e[10], e[11]};
+             sel_done[2] = {e[10], e[11]}, ppf_done[2] = {e[12], e[13]};
   PCR_HIP(hipEventRecord(fork, org), "fork record");
   for (hipStream_t st : {sn, sp, sv}) PCR_HIP(hipStreamWaitEvent(st, fork, 0), "fork wait");
   const size_t dstride = (size_t)a->b * a->c;
@@ -264,6 +264,30 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
       // (the PPF launch reads the workspace too: the slot is free after it)
       PCR_TRY(knn_select_ppf(a, io, q, sorted, sn));
       PCR_HIP(hipEventRecord(sel_done[q], sn), "select record");
+    } else if (schedule == 3) {
+      // sort + selection of step s on s_nbr into KNN workspace q, the local
+      // PPF of step s on `origin` (the fourth stream) after it, so the PPF of
+      // step s runs beside the sort + selection of step s + 1; workspace q
+      // is rewritten by step s + 2 only after the PPF of step s read it
+      if (s == 0) PCR_HIP(hipStreamWaitEvent(sn, means_done[q], 0), "head wait");
+      if (s >= 2) PCR_HIP(hipStreamWaitEvent(sn, ppf_done[q], 0), "knn slot wait");
+      PCR_TRY(knn_sort(a, io, q, sn, &sorted));
+      pcr_status rs = PCR_ERR_UNSUPPORTED;
+      if (sorted && !io.knn_dist)
+        rs = pcr_knn_select_sorted(io.xyz, a->b, a->n, a->k, a->knn_ws[q], a->knn_ws_bytes, sn);
+      if (rs == PCR_OK) {
+        PCR_HIP(hipEventRecord(sel_done[q], sn), "select record");
+        PCR_HIP(hipStreamWaitEvent(org, sel_done[q], 0), "select wait");
+        PCR_TRY(pcr_knn_ppf_sorted(io.xyz, io.normals, a->b, a->n, a->k, a->relative,
+                                   io.knn_idx, io.local_ppf, a->knn_ws[q], a->knn_ws_bytes, org));
+        PCR_HIP(hipEventRecord(ppf_done[q], org), "ppf record");
+      } else {
+        if (rs != PCR_ERR_UNSUPPORTED) return rs;
+        // no sorted rows (k > 32, clouds past 2048 points, distances
+        // requested): selection + PPF on s_nbr as schedule 1
+        PCR_TRY(knn_select_ppf(a, io, q, sorted, sn));
+        PCR_HIP(hipEventRecord(ppf_done[q], sn), "ppf record");
+      }
     } else {
       // the first step's neighbour stream starts after that step's voxel
       // means: prep + means (the grid stream's chain) get the chip first, so

@@ -490,7 +490,9 @@ class SphExtractor:
     def run_native(self, xyz, normals, features, steps, desc_steps=None, schedule=1,
                    timed=False, match=None):
         """`steps` pipelined steps enqueued by the library's native runner
-        (pcr_extractor_run): schedule 1 = three streams (prep + means / devox
+        (pcr_extractor_run): schedule 3 = as 1 with the local PPF of each step
+        on the caller's stream beside the next step's sort + selection;
+        schedule 1 = three streams (prep + means / devox
         on s_pre, the grid stream on s_vox, sort + select + PPF on s_nbr,
         voxel buffer sets alternating), 2 = as 1 with the Morton sort on
         s_pre, 0 = two streams with the fused grid kernel.  One ctypes call
@@ -562,8 +564,8 @@ class SphExtractor:
         the current stream after it.  match: a
         registration.PairMatch (its workspace; the matching outputs go to
         the ring sets).  Returns the ring's output sets."""
-        if schedule not in (1, 2):
-            raise RuntimeError("run_ring needs schedule 1 or 2")
+        if schedule not in (1, 2, 3):
+            raise RuntimeError("run_ring needs schedule 1, 2 or 3")
         R = len(batches)
         if R < 1:
             raise RuntimeError("run_ring needs at least one batch")
