@@ -138,15 +138,39 @@ extern "C" pcr_status pcr_runner_create(int timed_steps, pcr_runner** out) {
     return PCR_ERR_LAUNCH;
   }
   bool ok = true;
+  // the sync events only order the runner's streams on this device (every
+  // kernel's own dispatch packet carries its acquire / release), so their
+  // system-scope fences -- host visibility, cache write-backs at every record
+  // -- are dropped: c2 A/B on one box, 3 interleaved rounds, 0.0971 -> 0.0953
+  // ms per step (profiles/r04_ab_events.log); hipEventReleaseToDevice alone
+  // measured no better than the default.  The caller's stream is joined
+  // after the run with these events, and the host synchronises through its
+  // own (system-scope) events.
+#if defined(KNN_EXP) && KNN_EXP == 26
+  const unsigned scope = hipEventReleaseToDevice;
+#elif defined(KNN_EXP) && KNN_EXP == 27
+  const unsigned scope = 0;
+#else
+  const unsigned scope = hipEventDisableSystemFence;
+#endif
   for (int i = 0; i < kSyncEvents; i++)
-    ok = ok && hipEventCreateWithFlags(&rn->sync[i], hipEventDisableTiming) == hipSuccess;
+    ok = ok && hipEventCreateWithFlags(&rn->sync[i], hipEventDisableTiming | scope) == hipSuccess;
+  // timing events: device-scope release (hipEventReleaseToDevice: more
+  // precise timings, no system-scope write-back inside the timed kernel's
+  // bracket); the experiment build 28 keeps the default
+#if defined(KNN_EXP) && KNN_EXP == 28
+  const unsigned tscope = 0;
+#else
+  const unsigned tscope = hipEventReleaseToDevice;
+#endif
   if (ok && timed_steps > 0) {
     rn->t0 = new hipEvent_t[timed_steps]();
     rn->t1 = new hipEvent_t[timed_steps]();
     rn->timed_cap = timed_steps;
     rn->timed_want = timed_steps;
     for (int i = 0; i < timed_steps && ok; i++)
-      ok = hipEventCreate(&rn->t0[i]) == hipSuccess && hipEventCreate(&rn->t1[i]) == hipSuccess;
+      ok = hipEventCreateWithFlags(&rn->t0[i], tscope) == hipSuccess &&
+           hipEventCreateWithFlags(&rn->t1[i], tscope) == hipSuccess;
   }
   if (!ok) {
     delete rn;
