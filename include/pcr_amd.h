@@ -402,6 +402,11 @@ pcr_status pcr_read_xyzn_txt(const char *path, float *out, long long rows, int c
  *               stream) after the selection of step s, beside the sort +
  *               selection of step s+1 on s_nbr (KNN workspace s % 2, reused
  *               by step s+2 after that PPF read it).
+ *   schedule 4: as 1, with three voxel workspaces (step s in s % 3, reused
+ *               by step s+3) and the grid-stream kernels of even steps on
+ *               s_vox, of odd steps on `origin`: a stream kernel's completion
+ *               (its write stream drained, ~10 us after its last wave) is no
+ *               longer on the next step's path.
  * Buffers with two entries are the alternating sets (schedule 0 uses set 0).
  * desc_steps: [steps][b][c] per-step descriptors, or NULL (then desc).
  *
@@ -472,6 +477,8 @@ typedef struct pcr_extractor_args {
    * (set0 + s) % nsets; nsets = 0: the single set above */
   int nsets, set0;
   const pcr_extractor_set *sets;
+  /* schedule 4: the third voxel workspace (vox_ws_bytes) */
+  void *vox_ws3;
 } pcr_extractor_args;
 pcr_status pcr_extractor_run(pcr_runner *runner, const pcr_extractor_args *args, int steps,
                              int schedule, float *desc_steps, void *origin, void *s_nbr,

@@ -204,7 +204,7 @@ extern "C" pcr_status pcr_runner_grid_times(pcr_runner* rn, float* ms, int cap, 
 extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_args* a,
                                         int steps, int schedule, float* desc_steps, void* origin,
                                         void* s_nbr_p, void* s_pre_p, void* s_vox_p) {
-  PCR_REQUIRE(a != nullptr && steps >= 0 && schedule >= 0 && schedule <= 3,
+  PCR_REQUIRE(a != nullptr && steps >= 0 && schedule >= 0 && schedule <= 4,
               "extractor_run: invalid arguments");
   PCR_REQUIRE(a->b >= 0 && a->n >= 1 && a->c >= 1 && a->k >= 1 && a->r >= 1,
               "extractor_run: invalid sizes");
@@ -216,7 +216,9 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
                     sv = as_stream(s_vox_p);
   const int nslots = schedule >= 1 ? 2 : 1;
   PCR_REQUIRE(a->nsets >= 0 && (a->nsets == 0 || (a->sets && schedule >= 1 && a->set0 >= 0)),
-              "extractor_run: a batch ring needs sets, set0 >= 0 and schedule 1 or 2");
+              "extractor_run: a batch ring needs sets, set0 >= 0 and schedule >= 1");
+  PCR_REQUIRE(schedule != 4 || a->vox_ws3 != nullptr,
+              "extractor_run: schedule 4 needs the third voxel workspace (vox_ws3)");
   for (int q = 0; q < nslots; q++)
     PCR_REQUIRE(a->vox_ws[q] && a->knn_ws[schedule >= 2 ? q : 0] &&
                     (a->nsets > 0 || (a->dinds[q] && a->dwgts[q])),
@@ -242,9 +244,13 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
   // the LAST timed_last steps of the run are timed (the pipeline is full)
   const int t_first = steps - rn->timed_last;
   hipEvent_t* e = rn->sync;
-  hipEvent_t fork = e[0], means_done[2] = {e[1], e[2]}, stream_done[2] = {e[3], e[4]},
-             join[3] = {e[5], e[6], e[7]}, sort_done[2] = {e[8], e[9]},
-             sel_done[2] = {e[10], e[11]}, ppf_done[2] = {e[12], e[13]};
+  hipEvent_t fork = e[0], means_done[3] = {e[1], e[2], e[8]},
+             stream_done[3] = {e[3], e[4], e[9]}, join[3] = {e[5], e[6], e[7]},
+             sort_done[2] = {e[8], e[9]}, sel_done[2] = {e[10], e[11]},
+             ppf_done[2] = {e[12], e[13]};
+  // schedule 4: three voxel workspaces (step s in s % 3) and the grid-stream
+  // kernels of consecutive steps on alternating queues (s_vox, origin)
+  void* const vws[3] = {a->vox_ws[0], a->vox_ws[1], a->vox_ws3};
   PCR_HIP(hipEventRecord(fork, org), "fork record");
   for (hipStream_t st : {sn, sp, sv}) PCR_HIP(hipStreamWaitEvent(st, fork, 0), "fork wait");
   const size_t dstride = (size_t)a->b * a->c;
@@ -268,21 +274,25 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
       PCR_TRY(knn_sort(a, io, q, sp, &sorted));
       PCR_HIP(hipEventRecord(sort_done[q], sp), "sort record");
     }
-    if (s >= 2) PCR_HIP(hipStreamWaitEvent(sp, stream_done[q], 0), "slot wait");
+    // voxel workspace slot and the queue of this step's grid stream
+    const int nv = schedule == 4 ? 3 : 2;
+    const int qv = s % nv;
+    void* const vw = vws[qv];
+    const hipStream_t sg = (schedule == 4 && (s & 1)) ? org : sv;
+    if (s >= nv) PCR_HIP(hipStreamWaitEvent(sp, stream_done[qv], 0), "slot wait");
     PCR_TRY(pcr_extractor_voxel_prep(io.xyz, a->b, a->n, a->r, io.norm_coords, io.ind, io.dinds,
-                                       io.dwgts, a->vox_ws[q], a->vox_ws_bytes, sp));
+                                       io.dwgts, vw, a->vox_ws_bytes, sp));
     PCR_TRY(pcr_extractor_voxel_means_devox(io.features, a->b, a->c, a->n, a->r, io.devox,
-                                            io.dinds, io.dwgts, desc, a->vox_ws[q],
-                                            a->vox_ws_bytes, sp));
-    PCR_HIP(hipEventRecord(means_done[q], sp), "means record");
+                                            io.dinds, io.dwgts, desc, vw, a->vox_ws_bytes, sp));
+    PCR_HIP(hipEventRecord(means_done[qv], sp), "means record");
     PCR_TRY(match_pairs(a, io, sp));
-    PCR_HIP(hipStreamWaitEvent(sv, means_done[q], 0), "means wait");
+    PCR_HIP(hipStreamWaitEvent(sg, means_done[qv], 0), "means wait");
     const bool timed = s >= t_first;
-    if (timed) PCR_HIP(hipEventRecord(rn->t0[s - t_first], sv), "timing record");
-    PCR_TRY(pcr_extractor_voxel_stream(a->b, a->c, a->n, a->r, io.cnt, io.grid, a->vox_ws[q],
-                                       a->vox_ws_bytes, sv));
-    if (timed) PCR_HIP(hipEventRecord(rn->t1[s - t_first], sv), "timing record");
-    PCR_HIP(hipEventRecord(stream_done[q], sv), "stream record");
+    if (timed) PCR_HIP(hipEventRecord(rn->t0[s - t_first], sg), "timing record");
+    PCR_TRY(pcr_extractor_voxel_stream(a->b, a->c, a->n, a->r, io.cnt, io.grid, vw,
+                                       a->vox_ws_bytes, sg));
+    if (timed) PCR_HIP(hipEventRecord(rn->t1[s - t_first], sg), "timing record");
+    PCR_HIP(hipEventRecord(stream_done[qv], sg), "stream record");
     if (schedule == 2) {
       PCR_HIP(hipStreamWaitEvent(sn, sort_done[q], 0), "sort wait");
       // (the PPF launch reads the workspace too: the slot is free after it)

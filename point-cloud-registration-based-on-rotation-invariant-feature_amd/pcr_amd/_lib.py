@@ -102,7 +102,8 @@ class ExtractorArgs(ctypes.Structure):
                 ("knn_ws_bytes", SZ), ("vox_ws", P * 2), ("vox_ws_bytes", SZ),
                 ("match_pairs", I), ("corr12", P), ("corr21", P), ("idx1", P), ("idx2", P),
                 ("match_count", P), ("match_ws", P), ("match_ws_bytes", SZ),
-                ("nsets", I), ("set0", I), ("sets", ctypes.POINTER(ExtractorSet))]
+                ("nsets", I), ("set0", I), ("sets", ctypes.POINTER(ExtractorSet)),
+                ("vox_ws3", P)]
 
 
 _lib = None

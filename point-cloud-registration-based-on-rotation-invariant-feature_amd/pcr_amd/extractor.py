@@ -476,6 +476,11 @@ class SphExtractor:
         a.knn_ws_bytes = self.knn_ws.numel()
         a.vox_ws[0], a.vox_ws[1] = _ptr(self.ws), _ptr(s1[1])
         a.vox_ws_bytes = self.ws.numel()
+        if getattr(self, "_ws3", None) is None:
+            # the third voxel workspace of runner schedule 4
+            self._ws3 = torch.empty_like(self.ws)
+            self._order_new_buffers()
+        a.vox_ws3 = _ptr(self._ws3)
         if match is not None:
             if 2 * match.pairs != self.b or match.n != self.n:
                 raise RuntimeError("match buffers are for %d pairs of %d points"
@@ -490,7 +495,9 @@ class SphExtractor:
     def run_native(self, xyz, normals, features, steps, desc_steps=None, schedule=1,
                    timed=False, match=None):
         """`steps` pipelined steps enqueued by the library's native runner
-        (pcr_extractor_run): schedule 3 = as 1 with the local PPF of each step
+        (pcr_extractor_run): schedule 4 = as 1 with three voxel workspaces and
+        the grid-stream kernels alternating between s_vox and the caller's
+        stream; schedule 3 = as 1 with the local PPF of each step
         on the caller's stream beside the next step's sort + selection;
         schedule 1 = three streams (prep + means / devox
         on s_pre, the grid stream on s_vox, sort + select + PPF on s_nbr,
@@ -564,8 +571,8 @@ class SphExtractor:
         the current stream after it.  match: a
         registration.PairMatch (its workspace; the matching outputs go to
         the ring sets).  Returns the ring's output sets."""
-        if schedule not in (1, 2, 3):
-            raise RuntimeError("run_ring needs schedule 1, 2 or 3")
+        if schedule not in (1, 2, 3, 4):
+            raise RuntimeError("run_ring needs schedule 1 to 4")
         R = len(batches)
         if R < 1:
             raise RuntimeError("run_ring needs at least one batch")
