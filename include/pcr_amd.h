@@ -407,6 +407,9 @@ pcr_status pcr_read_xyzn_txt(const char *path, float *out, long long rows, int c
  *               s_vox, of odd steps on `origin`: a stream kernel's completion
  *               (its write stream drained, ~10 us after its last wave) is no
  *               longer on the next step's path.
+ *   schedule 5: as 4, with the local PPF of step s on step s's grid queue,
+ *               ahead of its grid stream (s_nbr only sorts and selects; KNN
+ *               workspace s % 2, reused by step s+2 after that PPF).
  * Buffers with two entries are the alternating sets (schedule 0 uses set 0).
  * desc_steps: [steps][b][c] per-step descriptors, or NULL (then desc).
  *

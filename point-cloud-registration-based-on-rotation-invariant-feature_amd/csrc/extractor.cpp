@@ -204,7 +204,7 @@ extern "C" pcr_status pcr_runner_grid_times(pcr_runner* rn, float* ms, int cap, 
 extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_args* a,
                                         int steps, int schedule, float* desc_steps, void* origin,
                                         void* s_nbr_p, void* s_pre_p, void* s_vox_p) {
-  PCR_REQUIRE(a != nullptr && steps >= 0 && schedule >= 0 && schedule <= 4,
+  PCR_REQUIRE(a != nullptr && steps >= 0 && schedule >= 0 && schedule <= 5,
               "extractor_run: invalid arguments");
   PCR_REQUIRE(a->b >= 0 && a->n >= 1 && a->c >= 1 && a->k >= 1 && a->r >= 1,
               "extractor_run: invalid sizes");
@@ -217,8 +217,8 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
   const int nslots = schedule >= 1 ? 2 : 1;
   PCR_REQUIRE(a->nsets >= 0 && (a->nsets == 0 || (a->sets && schedule >= 1 && a->set0 >= 0)),
               "extractor_run: a batch ring needs sets, set0 >= 0 and schedule >= 1");
-  PCR_REQUIRE(schedule != 4 || a->vox_ws3 != nullptr,
-              "extractor_run: schedule 4 needs the third voxel workspace (vox_ws3)");
+  PCR_REQUIRE(schedule < 4 || a->vox_ws3 != nullptr,
+              "extractor_run: schedules 4 and 5 need the third voxel workspace (vox_ws3)");
   for (int q = 0; q < nslots; q++)
     PCR_REQUIRE(a->vox_ws[q] && a->knn_ws[schedule >= 2 ? q : 0] &&
                     (a->nsets > 0 || (a->dinds[q] && a->dwgts[q])),
@@ -275,10 +275,31 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
       PCR_HIP(hipEventRecord(sort_done[q], sp), "sort record");
     }
     // voxel workspace slot and the queue of this step's grid stream
-    const int nv = schedule == 4 ? 3 : 2;
+    const int nv = schedule >= 4 ? 3 : 2;
     const int qv = s % nv;
     void* const vw = vws[qv];
-    const hipStream_t sg = (schedule == 4 && (s & 1)) ? org : sv;
+    const hipStream_t sg = (schedule >= 4 && (s & 1)) ? org : sv;
+    if (schedule == 5) {
+      // sort + selection of step s on s_nbr into KNN workspace q; the local
+      // PPF of step s on this step's grid queue, ahead of its grid stream
+      // (each grid queue runs every other step, so it has the time)
+      if (s >= 2) PCR_HIP(hipStreamWaitEvent(sn, ppf_done[q], 0), "knn slot wait");
+      PCR_TRY(knn_sort(a, io, q, sn, &sorted));
+      pcr_status rs = PCR_ERR_UNSUPPORTED;
+      if (sorted && !io.knn_dist)
+        rs = pcr_knn_select_sorted(io.xyz, a->b, a->n, a->k, a->knn_ws[q], a->knn_ws_bytes, sn);
+      if (rs == PCR_OK) {
+        PCR_HIP(hipEventRecord(sel_done[q], sn), "select record");
+        PCR_HIP(hipStreamWaitEvent(sg, sel_done[q], 0), "select wait");
+        PCR_TRY(pcr_knn_ppf_sorted(io.xyz, io.normals, a->b, a->n, a->k, a->relative,
+                                   io.knn_idx, io.local_ppf, a->knn_ws[q], a->knn_ws_bytes, sg));
+        PCR_HIP(hipEventRecord(ppf_done[q], sg), "ppf record");
+      } else {
+        if (rs != PCR_ERR_UNSUPPORTED) return rs;
+        PCR_TRY(knn_select_ppf(a, io, q, sorted, sn));
+        PCR_HIP(hipEventRecord(ppf_done[q], sn), "ppf record");
+      }
+    }
     if (s >= nv) PCR_HIP(hipStreamWaitEvent(sp, stream_done[qv], 0), "slot wait");
     PCR_TRY(pcr_extractor_voxel_prep(io.xyz, a->b, a->n, a->r, io.norm_coords, io.ind, io.dinds,
                                        io.dwgts, vw, a->vox_ws_bytes, sp));
@@ -322,7 +343,7 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
         PCR_TRY(knn_select_ppf(a, io, q, sorted, sn));
         PCR_HIP(hipEventRecord(ppf_done[q], sn), "ppf record");
       }
-    } else {
+    } else if (schedule != 5) {
       // the first step's neighbour stream starts after that step's voxel
       // means: prep + means (the grid stream's chain) get the chip first, so
       // the grid stream starts ~1/3 sooner (a 20-step call: 289k -> 298k

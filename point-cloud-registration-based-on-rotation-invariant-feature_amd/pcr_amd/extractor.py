@@ -571,8 +571,8 @@ class SphExtractor:
         the current stream after it.  match: a
         registration.PairMatch (its workspace; the matching outputs go to
         the ring sets).  Returns the ring's output sets."""
-        if schedule not in (1, 2, 3, 4):
-            raise RuntimeError("run_ring needs schedule 1 to 4")
+        if schedule not in (1, 2, 3, 4, 5):
+            raise RuntimeError("run_ring needs schedule 1 to 5")
         R = len(batches)
         if R < 1:
             raise RuntimeError("run_ring needs at least one batch")

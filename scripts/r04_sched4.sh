@@ -18,7 +18,7 @@ print("%-22s %9.1f clouds/s  %.4f ms/step  grid kernel %s ms  verified %s" % (
 PY
 }
 for r in 1 2 3; do
-  for sc in 1 4; do
+  for sc in 1 4 5; do
     timeout -k 10 120 python bench.py --schedule $sc --no-cpu-baseline > gpurun_out/sched.tmp 2>&1 || exit $?
     line "sched$sc-200"
     timeout -k 10 120 python bench.py --schedule $sc --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/sched.tmp 2>&1 || exit $?
@@ -26,5 +26,5 @@ for r in 1 2 3; do
   done
 done
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c2s4 -o run --output-format csv -- python3 bench.py --schedule 4 --steps 80 --warmup 40 --no-cpu-baseline > gpurun_out/prof_c2s4.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c2s5 -o run --output-format csv -- python3 bench.py --schedule 5 --steps 80 --warmup 40 --no-cpu-baseline > gpurun_out/prof_c2s5.log 2>&1
 echo "prof rc=$?"

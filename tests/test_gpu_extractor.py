@@ -72,7 +72,7 @@ def poison(ex):
         t.view(-1).view(torch.uint8).fill_(0xFF)
 
 
-@pytest.mark.parametrize("schedule", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("schedule", [0, 1, 2, 3, 4, 5])
 def test_extractor_native_runner(dev, schedule):
     """pcr_extractor_run (the bench's native multi-step enqueue): every
     step's descriptor and the final outputs equal the single-step results."""
@@ -103,7 +103,7 @@ def test_extractor_native_runner(dev, schedule):
             assert all(0 < t < 100 for t in ms)
 
 
-@pytest.mark.parametrize("schedule", [1, 2, 3, 4])
+@pytest.mark.parametrize("schedule", [1, 2, 3, 4, 5])
 def test_extractor_runner_batch_ring(dev, schedule):
     """pcr_extractor_run over a batch ring of 3 distinct batches (each with
     its own output set): one call of 3 steps, then a call of 5 steps that

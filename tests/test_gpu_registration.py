@@ -57,7 +57,7 @@ def test_pair_step_matches_oracle(dev, p, n, c, k, r):
         assert np.array_equal(N(g), e), name
     # the native runner's per-step matching gives the same, every step
     from test_gpu_extractor import poison
-    for schedule in (0, 1, 2, 3, 4):
+    for schedule in (0, 1, 2, 3, 4, 5):
         desc_steps = torch.empty((4, 2 * p, c), device=dev)
         poison(pe.ex)
         for t in (pe.match.corr12, pe.match.corr21, pe.match.idx1, pe.match.idx2,
