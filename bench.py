@@ -78,13 +78,15 @@ def parse(argv=None):
     ap.add_argument("--kernel-iters", type=int, default=50, help="(kept for old command lines)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--schedule", type=int, choices=(1, 2, 3, 4, 5), default=1,
+    ap.add_argument("--schedule", type=int, choices=(1, 2, 3, 4, 5, 6), default=1,
                     help="pcr_extractor_run schedule (include/pcr_amd.h): 1 = three streams "
                          "(sort+select+PPF / prep+means+devox / dense-grid stream), 2 = as 1 "
                          "with the Morton sort on the prep stream, 3 = as 1 with the local PPF "
                          "on a fourth stream beside the next step's sort + selection, 4 = as 1 "
                          "with three voxel workspaces and the grid stream alternating between "
-                         "two queues, 5 = as 4 with the local PPF on the grid queues")
+                         "two queues, 5 = as 4 with the local PPF on the grid queues, 6 = two "
+                         "independent pipelines per chain (voxel chain on s_vox / origin, KNN "
+                         "chain on s_nbr / s_pre by step parity), no cross-queue events")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="diagnostic: no timing events around the dominant kernel")
     ap.add_argument("--no-verify", action="store_true",

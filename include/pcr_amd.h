@@ -410,6 +410,18 @@ pcr_status pcr_read_xyzn_txt(const char *path, float *out, long long rows, int c
  *   schedule 5: as 4, with the local PPF of step s on step s's grid queue,
  *               ahead of its grid stream (s_nbr only sorts and selects; KNN
  *               workspace s % 2, reused by step s+2 after that PPF).
+ *   schedule 6: two independent pipelines per chain and no cross-queue event
+ *               inside the run: the voxel chain (prep, means / devox /
+ *               descriptor, matching, grid stream) of step s on s_vox (even
+ *               s) or `origin` (odd s) with voxel workspace s % 2, the KNN
+ *               chain (sort, selection, local PPF) on s_nbr (even) or s_pre
+ *               (odd) with KNN workspace s % 2, so every workspace is reused
+ *               only on its own queue.  The odd voxel queue starts after step
+ *               0's means (one wait per call) so the two grid streams
+ *               alternate rather than coincide.  Needs a batch ring of >= 2
+ *               sets (consecutive steps write distinct sets); a ring of odd
+ *               size that one call wraps orders each set's rewrite behind its
+ *               previous step with per-set events (made on first use).
  * Buffers with two entries are the alternating sets (schedule 0 uses set 0).
  * desc_steps: [steps][b][c] per-step descriptors, or NULL (then desc).
  *
@@ -422,7 +434,7 @@ pcr_status pcr_read_xyzn_txt(const char *path, float *out, long long rows, int c
  * pcr_runner_grid_times waits for them and returns the per-step durations
  * (ms) of the last run -- the dominant kernel's in-step duration.
  *
- * Batch ring (nsets > 0, schedules 1 / 2): step s of a call reads its clouds
+ * Batch ring (nsets > 0, schedules 1 to 6): step s of a call reads its clouds
  * from, and writes every output into, sets[(set0 + s) % nsets] -- a fresh
  * batch per step, as the reference's loaders hand one over per iteration
  * (datasets/deepgmr_mn40.py:71-97, train.py:138-153) -- and the single-set

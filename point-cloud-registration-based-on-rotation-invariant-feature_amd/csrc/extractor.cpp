@@ -6,6 +6,8 @@
 // ctypes / torch.cuda.Event operations per step.
 #include <hip/hip_runtime.h>
 
+#include <vector>
+
 #include "common.hpp"
 
 namespace pcr {
@@ -27,8 +29,13 @@ struct pcr_runner {
   hipEvent_t* t1 = nullptr;       // [timed_cap] after it
   int timed_last = 0;             // pairs recorded by the last run
   int timed_want = 0;             // steps each run times (<= timed_cap)
+  // schedule 6 with an odd batch ring reused inside one call: per-set events
+  // (the step that rewrites set t runs on the other queue of its chain)
+  std::vector<hipEvent_t> ring_ev;  // [2 * nsets]: voxel chain, KNN chain
   ~pcr_runner() {
     for (hipEvent_t e : sync)
+      if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : ring_ev)
       if (e) (void)hipEventDestroy(e);
     for (int i = 0; i < timed_cap; i++) {
       if (t0 && t0[i]) (void)hipEventDestroy(t0[i]);
@@ -204,7 +211,7 @@ extern "C" pcr_status pcr_runner_grid_times(pcr_runner* rn, float* ms, int cap, 
 extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_args* a,
                                         int steps, int schedule, float* desc_steps, void* origin,
                                         void* s_nbr_p, void* s_pre_p, void* s_vox_p) {
-  PCR_REQUIRE(a != nullptr && steps >= 0 && schedule >= 0 && schedule <= 5,
+  PCR_REQUIRE(a != nullptr && steps >= 0 && schedule >= 0 && schedule <= 6,
               "extractor_run: invalid arguments");
   PCR_REQUIRE(a->b >= 0 && a->n >= 1 && a->c >= 1 && a->k >= 1 && a->r >= 1,
               "extractor_run: invalid sizes");
@@ -217,10 +224,14 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
   const int nslots = schedule >= 1 ? 2 : 1;
   PCR_REQUIRE(a->nsets >= 0 && (a->nsets == 0 || (a->sets && schedule >= 1 && a->set0 >= 0)),
               "extractor_run: a batch ring needs sets, set0 >= 0 and schedule >= 1");
-  PCR_REQUIRE(schedule < 4 || a->vox_ws3 != nullptr,
+  // schedule 6 writes consecutive steps from different queues: they need
+  // distinct output sets (the c5 voxel path counts into cnt with atomics)
+  PCR_REQUIRE(schedule != 6 || a->nsets >= 2,
+              "extractor_run: schedule 6 needs a batch ring of at least two sets");
+  PCR_REQUIRE(schedule < 4 || schedule == 6 || a->vox_ws3 != nullptr,
               "extractor_run: schedules 4 and 5 need the third voxel workspace (vox_ws3)");
   for (int q = 0; q < nslots; q++)
-    PCR_REQUIRE(a->vox_ws[q] && a->knn_ws[schedule >= 2 ? q : 0] &&
+    PCR_REQUIRE(a->vox_ws[q] && a->knn_ws[schedule >= 2 || schedule == 6 ? q : 0] &&
                     (a->nsets > 0 || (a->dinds[q] && a->dwgts[q])),
                 "extractor_run: buffer set %d missing", q);
   for (int t = 0; t < a->nsets; t++)
@@ -251,6 +262,16 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
   // schedule 4: three voxel workspaces (step s in s % 3) and the grid-stream
   // kernels of consecutive steps on alternating queues (s_vox, origin)
   void* const vws[3] = {a->vox_ws[0], a->vox_ws[1], a->vox_ws3};
+  // schedule 6 over an odd ring that one call wraps: per-set events, made
+  // once per ring size (the first call, outside any timed region)
+  const bool ring_wait = schedule == 6 && a->nsets > 0 && (a->nsets & 1) && steps > a->nsets;
+  if (ring_wait && rn->ring_ev.size() != (size_t)(2 * a->nsets)) {
+    for (hipEvent_t ev : rn->ring_ev)
+      if (ev) (void)hipEventDestroy(ev);
+    rn->ring_ev.assign(2 * a->nsets, nullptr);
+    const unsigned fl = hipEventDisableTiming | hipEventDisableSystemFence;
+    for (hipEvent_t& ev : rn->ring_ev) PCR_HIP(hipEventCreateWithFlags(&ev, fl), "ring event");
+  }
   PCR_HIP(hipEventRecord(fork, org), "fork record");
   for (hipStream_t st : {sn, sp, sv}) PCR_HIP(hipStreamWaitEvent(st, fork, 0), "fork wait");
   const size_t dstride = (size_t)a->b * a->c;
@@ -267,6 +288,52 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
                                         io.dinds, io.dwgts, desc, a->vox_ws[0],
                                         a->vox_ws_bytes, sv));
       PCR_TRY(match_pairs(a, io, sv));
+      continue;
+    }
+    if (schedule == 6) {
+      // two independent pipelines per chain, no cross-queue events: the voxel
+      // chain (prep, means / devox, match, grid stream) of step s on
+      // {s_vox, origin}[s & 1] with voxel workspace s & 1, the KNN chain
+      // (sort, selection, local PPF) on {s_nbr, s_pre}[s & 1] with KNN
+      // workspace s & 1; every workspace is reused only by its own queue
+      const hipStream_t vq = q ? org : sv, kq = q ? sp : sn;
+      const int t = a->nsets > 0 ? (a->set0 + s) % a->nsets : 0;
+      hipEvent_t* const rv = ring_wait ? rn->ring_ev.data() : nullptr;
+      if (rv && s >= a->nsets) {  // set t last written on the other queues
+        PCR_HIP(hipStreamWaitEvent(vq, rv[2 * t], 0), "ring wait");
+        PCR_HIP(hipStreamWaitEvent(kq, rv[2 * t + 1], 0), "ring wait");
+      }
+      // the odd queues start half a chain behind the even ones: step 1's
+      // voxel chain waits for step 0's means (so one grid stream runs while
+      // the other queue does prep + means; aligned, the two grid streams
+      // fight for HBM and then leave it idle together)
+#if defined(KNN_EXP) && KNN_EXP == 31
+      if (s == 1) PCR_HIP(hipStreamWaitEvent(kq, sel_done[0], 0), "offset wait");
+#endif
+      PCR_TRY(knn_sort(a, io, q, kq, &sorted));
+      PCR_TRY(knn_select_ppf(a, io, q, sorted, kq));
+#if defined(KNN_EXP) && KNN_EXP == 31
+      if (s == 0) PCR_HIP(hipEventRecord(sel_done[0], kq), "offset record");
+#endif
+#if !defined(KNN_EXP) || KNN_EXP != 30
+      if (s == 1) PCR_HIP(hipStreamWaitEvent(vq, means_done[0], 0), "offset wait");
+#endif
+      PCR_TRY(pcr_extractor_voxel_prep(io.xyz, a->b, a->n, a->r, io.norm_coords, io.ind,
+                                       io.dinds, io.dwgts, a->vox_ws[q], a->vox_ws_bytes, vq));
+      PCR_TRY(pcr_extractor_voxel_means_devox(io.features, a->b, a->c, a->n, a->r, io.devox,
+                                              io.dinds, io.dwgts, desc, a->vox_ws[q],
+                                              a->vox_ws_bytes, vq));
+      if (s == 0) PCR_HIP(hipEventRecord(means_done[0], vq), "offset record");
+      PCR_TRY(match_pairs(a, io, vq));
+      const bool timed = s >= t_first;
+      if (timed) PCR_HIP(hipEventRecord(rn->t0[s - t_first], vq), "timing record");
+      PCR_TRY(pcr_extractor_voxel_stream(a->b, a->c, a->n, a->r, io.cnt, io.grid, a->vox_ws[q],
+                                         a->vox_ws_bytes, vq));
+      if (timed) PCR_HIP(hipEventRecord(rn->t1[s - t_first], vq), "timing record");
+      if (rv && s + a->nsets < steps) {
+        PCR_HIP(hipEventRecord(rv[2 * t], vq), "ring record");
+        PCR_HIP(hipEventRecord(rv[2 * t + 1], kq), "ring record");
+      }
       continue;
     }
     if (schedule == 2) {

@@ -1,0 +1,32 @@
+#!/bin/bash
+# round-4: schedule 6 queue start offsets -- interleaved c2 bench lines of the
+# product library (voxel queues offset), s6none (no offset) and s6both (voxel
+# and KNN queues offset), then a kernel trace of the product library
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+L=point-cloud-registration-based-on-rotation-invariant-feature_amd/lib
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider \
+  tests/test_gpu_extractor.py tests/test_gpu_registration.py -k "runner or ring or schedule6" > gpurun_out/pt_s6.log 2>&1
+rc=$?; tail -3 gpurun_out/pt_s6.log; [ $rc -eq 0 ] || exit $rc
+line() {
+  python - "$1" <<'PY'
+import json, sys
+d = json.loads([l for l in open("gpurun_out/s6.tmp") if l.startswith("{")][-1])
+k = d["roofline"]["kernel"]
+print("%-22s %9.1f clouds/s  %.4f ms/step  grid kernel %s ms  verified %s" % (
+    sys.argv[1], d["value"], d["ms_per_step"], k and k.get("avg_ms_in_step"), d["outputs_verified"]))
+PY
+}
+for r in 1 2 3; do
+  for v in prod s6none s6both; do
+    lib=$L/libpcr_amd.so; [ $v = prod ] || lib=$L/libpcr_amd_exp_$v.so
+    PCR_AMD_LIB=$lib timeout -k 10 120 python bench.py --schedule 6 --no-cpu-baseline > gpurun_out/s6.tmp 2>&1 || exit $?
+    line "$v-200"
+    PCR_AMD_LIB=$lib timeout -k 10 120 python bench.py --schedule 6 --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/s6.tmp 2>&1 || exit $?
+    line "$v-20"
+  done
+done
+cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c2s6o -o run --output-format csv -- python3 bench.py --schedule 6 --steps 80 --warmup 40 --no-cpu-baseline > gpurun_out/prof_c2s6o.log 2>&1
+echo "prof rc=$?"

@@ -103,7 +103,7 @@ def test_extractor_native_runner(dev, schedule):
             assert all(0 < t < 100 for t in ms)
 
 
-@pytest.mark.parametrize("schedule", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("schedule", [1, 2, 3, 4, 5, 6])
 def test_extractor_runner_batch_ring(dev, schedule):
     """pcr_extractor_run over a batch ring of 3 distinct batches (each with
     its own output set): one call of 3 steps, then a call of 5 steps that
@@ -135,6 +135,40 @@ def test_extractor_runner_batch_ring(dev, schedule):
         for s in range(steps):
             assert np.array_equal(N(desc_steps[s]), exp[(set0 + s) % 3]["desc"]), (steps, s)
         set0 = (set0 + steps) % 3
+
+
+def test_extractor_runner_schedule6_even_ring(dev):
+    """Schedule 6 (two independent pipelines per chain) over an even ring
+    that one call wraps twice (2 sets, 5 steps: set t is rewritten on the
+    same queue, no ring events), then over a 5-set ring with 7 steps (odd:
+    the rewrite runs on the other queue behind the per-set event).  The
+    single-set runner refuses schedule 6."""
+    from pcr_amd.extractor import SphExtractor
+    b, n, c, k, r = 4, 1024, 16, 32, 32
+    batches = [gaussian_clouds(b, n, seed=110 + i, c=c) for i in range(5)]
+    tb = [tuple(T(a, dev) for a in bt) for bt in batches]
+    exp = [expected_step(*bt, k, r) for bt in batches]
+    ex = SphExtractor(b, n, c, k, r, device=dev)
+    for R, steps in ((2, 5), (5, 7)):
+        ring = ex.ring_outputs(R)
+        for o in ring:
+            for t in o.values():
+                t.view(-1).view(torch.uint8).fill_(0xFF)
+        desc_steps = torch.full((steps, b, c), float("nan"), device=dev)
+        ex.run_ring(tb[:R], steps, 0, desc_steps, schedule=6)
+        torch.cuda.synchronize()
+        for i in range(R):
+            for key in ("knn_idx", "ind", "cnt", "dinds", "dwgts", "norm_coords", "grid",
+                        "devox"):
+                assert np.array_equal(N(ring[i][key]), exp[i][key]), (R, i, key)
+            assert np.array_equal(N(ring[i]["local_ppf"]), exp[i]["local_ppf"],
+                                  equal_nan=True), (R, i)
+        for s in range(steps):
+            assert np.array_equal(N(desc_steps[s]), exp[s % R]["desc"]), (R, s)
+    with pytest.raises(RuntimeError):
+        ex.run_native(*tb[0], 2, schedule=6)
+    with pytest.raises(RuntimeError):
+        ex.run_ring(tb[:1], 2, schedule=6)
 
 
 def test_extractor_full_size_properties(dev):

@@ -96,7 +96,8 @@ def _pair_batch(p, n, c, seed):
     return xyz.astype(np.float32), nrm.astype(np.float32), feat
 
 
-def test_pair_runner_batch_ring(dev):
+@pytest.mark.parametrize("schedule", [1, 6])
+def test_pair_runner_batch_ring(dev, schedule):
     """BASELINE c4 over distinct pair batches (datasets/deepgmr_mn40.py:71-97,
     a new pair per item): the native runner's batch ring, 3 batches of 2
     pairs, 3 steps; every ring set's extractor outputs and matching against
@@ -110,7 +111,7 @@ def test_pair_runner_batch_ring(dev):
     for o in ring:
         for t in o.values():
             t.view(-1).view(torch.uint8).fill_(0xFF)
-    pe.run_ring(tb, 3)
+    pe.run_ring(tb, 3, schedule=schedule)
     torch.cuda.synchronize()
     for i, bt in enumerate(batches):
         exp = oracle_pair_step(*bt, k, r, p)
