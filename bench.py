@@ -78,7 +78,7 @@ def parse(argv=None):
     ap.add_argument("--kernel-iters", type=int, default=50, help="(kept for old command lines)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--schedule", type=int, choices=(1, 2, 3, 4, 5, 6), default=1,
+    ap.add_argument("--schedule", type=int, choices=(1, 2, 3, 4, 5, 6), default=6,
                     help="pcr_extractor_run schedule (include/pcr_amd.h): 1 = three streams "
                          "(sort+select+PPF / prep+means+devox / dense-grid stream), 2 = as 1 "
                          "with the Morton sort on the prep stream, 3 = as 1 with the local PPF "
@@ -122,6 +122,8 @@ def parse(argv=None):
         args.batches = 8 if args.workload == "pairs" else 20
     if args.batches < 1:
         ap.error("--batches must be >= 1")
+    if args.schedule == 6 and args.batches < 2 and args.workload in ("extract", "pairs"):
+        ap.error("--schedule 6 needs --batches >= 2 (consecutive steps write distinct sets)")
     if args.workload == "pairs" and args.batch % 2:
         ap.error("--workload pairs needs an even --batch (source + target clouds)")
     if args.gpus < 1:
@@ -376,8 +378,9 @@ class ExtractWorkload:
 
     def run(self, steps, timed):
         """`steps` steps over the batch ring, continuing the cycle across
-        calls; timed: the last call brackets the grid kernel of its last
-        KTIMED steps with HIP events on its stream (in-step durations)."""
+        calls; timed: the last call brackets the grid kernel of KTIMED
+        steps in its middle (pipeline full) with HIP events on its stream
+        (in-step durations)."""
         from pcr_amd.distributed import run_pipelined
         ncalls = len(self.chunks(steps))
 
