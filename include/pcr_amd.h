@@ -429,7 +429,7 @@ pcr_status pcr_read_xyzn_txt(const char *path, float *out, long long rows, int c
  * pcr_runner_create on the current device and reused by every call (NULL:
  * transient events for this call only).  With timed_steps > 0 the runner
  * also brackets the grid-stream kernel (pcr_extractor_voxel_stream) of the
- * last min(steps, timed_steps) steps of each run (pipeline full; fewer after
+ * min(steps, timed_steps) steps in the middle of each run (pipeline full; fewer after
  * pcr_runner_set_timed) with timing events on its stream;
  * pcr_runner_grid_times waits for them and returns the per-step durations
  * (ms) of the last run -- the dominant kernel's in-step duration.

@@ -504,12 +504,12 @@ class SphExtractor:
         voxel buffer sets alternating), 2 = as 1 with the Morton sort on
         s_pre, 0 = two streams with the fused grid kernel.  One ctypes call
         for all steps.  timed: bracket the grid-stream kernel of every step
-        (True) or of the last N steps (an int N) with timing events (read
+        (True) or of N steps in the middle of the run (an int N) with timing events (read
         back with grid_kernel_times()).  match: a
         registration.PairMatch whose buffers receive, every step, the
         mutual-NN matching of clouds [0, B/2) against [B/2, B)."""
         self._check_inputs(xyz, normals, features)
-        # timed: True = every step, an int N = the last N steps
+        # timed: True = every step, an int N = N steps in the middle of the run
         ntimed = min(steps, (steps if timed is True else int(timed)) if timed else 0)
         runner = self._get_runner(ntimed)
         if self._runner_cap:
