@@ -1723,15 +1723,22 @@ static pcr_status run_voxelize(const float* features, const float* coords_f, con
               name, ws_bytes, need);
   PCR_PRIO_INIT();
   if (what & 1) {
-    // clouds of <= 1024 points: 256 threads (four points each), so a prep
-    // workgroup fits on a CU beside the other stream's KNN selection instead
-    // of waiting for whole CUs to drain
+    // clouds of <= 1024 points: a 256- or 512-thread workgroup (PCR_PREP_NT_DEF
+    // below) rather than 1024, so a prep workgroup fits on a CU beside the
+    // other queues' kernels instead of waiting for whole CUs to drain
     const bool small = n <= kSmallPrepN;
     const int nt = small ? kSmallPrepThreads : kPrepThreads;
     const int npad = next_pow2(n < nt ? nt : n);
     size_t prep_smem = (size_t)npad * 8 + (size_t)ws.W * 8 + (size_t)n * 8;
     PCR_REQUIRE(prep_smem <= 150 * 1024, "%s: prep LDS %zu too large", name, prep_smem);
-    static const int exp_nt = PCR_KNOB("PCR_PREP_NT", 256);
+// clouds of 257..1024 points: 512 threads (two points each).  Under the
+// runner's schedule 6 the prep kernel heads the critical voxel chain: c2
+// 379-385k -> 385-394k clouds/s against 256 threads (3 interleaved rounds,
+// profiles/r04_ab_prep.log); 1024 threads measured between the two
+#ifndef PCR_PREP_NT_DEF
+#define PCR_PREP_NT_DEF 512
+#endif
+    static const int exp_nt = PCR_KNOB("PCR_PREP_NT", PCR_PREP_NT_DEF);
     if (small && exp_nt == 512 && n > 256) {
       const int npad5 = next_pow2(n < 512 ? 512 : n);
       const size_t sm5 = (size_t)npad5 * 8 + (size_t)ws.W * 8 + (size_t)n * 8;
