@@ -661,8 +661,74 @@ class C5Workload:
         self.knn_ops = 9.0 * n * n * b
         self.side = torch.cuda.Stream(device=dev)
 
+    def _step_outputs(self):
+        ops, a = self.ops, self.args
+        xyz, nrm, feat = self.inputs
+        nc = ops.spherical_normalize(xyz)
+        grid, ind, cnt = ops.spherical_avg_voxelize_forward(feat, nc, a.res)
+        dv = ops.spherical_trilinear_devoxelize_forward(a.res, True, nc, grid, ind)
+        idx, ppf, _ = ops.knn_local_ppf(xyz, nrm, a.k)
+        return {"norm_coords": nc, "grid": grid, "ind": ind, "cnt": cnt, "devox": dv[0],
+                "knn_idx": idx, "local_ppf": ppf}
+
     def verify(self):
-        return None
+        """The c5 step's outputs, checked on the GPU (the CPU oracle takes
+        minutes at this size; tests/test_gpu_large.py holds the sampled
+        oracle checks): two runs of the step are bit-identical; for 64
+        sampled queries per cloud the k neighbours are the k nearest by a
+        float64 brute force (each within 1e-5 relative of the float64 k-th
+        distance, slot 0 at distance 0), their PPF distance channel is the
+        float64 |2c - p| within 1e-5; every point with a voxel is counted in
+        cnt, and the grid holds the float64 mean of its voxel's features
+        within 1e-5 at 64 sampled occupied voxels per cloud."""
+        a = self.args
+        b, n, k, r3 = a.batch, a.points, a.k, a.res ** 3
+        first = {kk: v.clone() for kk, v in self._step_outputs().items()}
+        again = self._step_outputs()
+        torch.cuda.synchronize(self.dev)
+        for key, v in first.items():
+            if not torch.equal(v.view(torch.int32), again[key].view(torch.int32)):
+                raise SystemExit("bench: c5 output %s differs between two runs" % key)
+        xyz, _, feat = self.inputs
+        g = torch.Generator(device=self.dev).manual_seed(7)
+        qi = torch.randint(0, n, (b, 64), generator=g, device=self.dev)
+        idx, ppf = first["knn_idx"].long(), first["local_ppf"]
+        for c in range(b):
+            X = xyz[c].double()
+            D = ((X[:, None, :] - X[:, qi[c]][:, :, None]) ** 2).sum(0)  # [64, n]
+            kth = D.topk(k, largest=False).values[:, -1]
+            sel = idx[c][:, qi[c]].t()  # [64, k]
+            ds = D.gather(1, sel)
+            dn = ppf[c, 3][:, qi[c]].t().double()
+            # the PPF distance channel: |c - (p - c)| with the reference's
+            # relative neighbour coordinates (pvcnn_classify.py:252-262)
+            gq = 2.0 * X[:, qi[c]][:, :, None] - X[:, sel]  # [3, 64, k]
+            de = (gq ** 2).sum(0).sqrt()
+            checks = {
+                "ids in range": bool(((sel >= 0) & (sel < n)).all()),
+                "k nearest": bool((ds <= kth[:, None] * (1 + 1e-5) + 1e-12).all()),
+                "slot 0 at distance 0": bool((ds[:, 0] == 0).all()),
+                "ids distinct": bool((sel.sort(1).values.diff(dim=1) > 0).all()),
+                "PPF distance": bool(((dn - de).abs() <= 1e-5 * de + 1e-6).all())}
+            bad = [name for name, v in checks.items() if not v]
+            if bad:
+                raise SystemExit("bench: c5 KNN / PPF of cloud %d fail the float64 check: %s"
+                                 % (c, ", ".join(bad)))
+            ind, cnt = first["ind"][c].long(), first["cnt"][c].long()
+            valid = ind >= 0
+            if int(cnt.sum()) != int(valid.sum()) or not torch.equal(
+                    torch.bincount(ind[valid], minlength=r3), cnt):
+                raise SystemExit("bench: c5 cnt of cloud %d does not count ind" % c)
+            occ = torch.nonzero(cnt > 0).flatten()
+            vs = occ[torch.randint(0, occ.numel(), (64,), generator=g, device=self.dev)]
+            for v in vs.tolist():
+                pts = torch.nonzero(ind == v).flatten()
+                mean = feat[c][:, pts].double().mean(1)
+                got = first["grid"][c][:, v].double()
+                if not bool(((got - mean).abs() <= 1e-5 * mean.abs() + 1e-6).all()):
+                    raise SystemExit("bench: c5 grid voxel %d of cloud %d is not its mean"
+                                     % (v, c))
+        return True
 
     def prepare_timing(self):
         self.ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
