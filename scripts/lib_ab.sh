@@ -13,7 +13,7 @@ for r in $(seq 1 "$rounds"); do
     for name in "$@"; do
       out=gpurun_out/ab_${wl}_${name}_$r.log
       PCR_AMD_LIB=$LIBDIR/libpcr_amd_exp_$name.so timeout -k 10 300 \
-        python bench.py --workload "$wl" --no-cpu-baseline > "$out" 2>&1
+        python bench.py --workload "$wl" --no-cpu-baseline $BENCH_ARGS > "$out" 2>&1
       rc=$?
       if [ $rc -ne 0 ]; then echo "$wl $name rc=$rc"; tail -5 "$out"; exit $rc; fi
       python - "$out" "$wl" "$name" <<'PY'
