@@ -1,5 +1,5 @@
 """Diagnostic: the KNN selection of the diagnostic library at c2 (or B / N
-from the environment) under PCR_KNN_DBG 0 (whole kernel), 4 (stop after the
+/ K from the environment; c5: B=8 N=65536 K=64) under PCR_KNN_DBG 0 (whole kernel), 4 (stop after the
 count) and 8 (stop after the collect), two launches each, in that order --
 run under `rocprofv3 --pmc SQ_INSTS_VALU ...` and split the counts with
 --report <counter_collection.csv>.  Not part of the product."""
@@ -33,17 +33,22 @@ sys.path[:0] = [ROOT, PKG]
 import torch  # noqa: E402
 from pcr_amd.extractor import SphExtractor  # noqa: E402
 
-b, n, k = int(os.environ.get("B", 32)), int(os.environ.get("N", 1024)), 32
+b, n, k = int(os.environ.get("B", 32)), int(os.environ.get("N", 1024)), int(os.environ.get("K", 32))
 dev = torch.device("cuda:0")
 g = torch.Generator(device=dev).manual_seed(0)
 xyz = torch.randn((b, 3, n), generator=g, device=dev)
 nrm = torch.randn((b, 3, n), generator=g, device=dev)
-ex = SphExtractor(b, n, 8, k, 8, device=dev)
-s = torch.cuda.current_stream().cuda_stream
-ok = ex.knn_sort(xyz, s)
+if n <= 2048:
+    ex = SphExtractor(b, n, 8, k, 8, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    ok = ex.knn_sort(xyz, s)
+    run = lambda: ex.knn_select(xyz, nrm, s, sorted_ok=ok, ppf=False)  # noqa: E731
+else:  # large clouds: the whole KNN + PPF call (sort, selection, emit)
+    from pcr_amd import ops  # noqa: E402
+    run = lambda: ops.knn_local_ppf(xyz, nrm, k)  # noqa: E731
 for bits in BITS:
     os.environ["PCR_KNN_DBG"] = str(bits)
     for _ in range(2):
-        ex.knn_select(xyz, nrm, s, sorted_ok=ok, ppf=False)
+        run()
     torch.cuda.synchronize()
 print("done b=%d n=%d" % (b, n))
