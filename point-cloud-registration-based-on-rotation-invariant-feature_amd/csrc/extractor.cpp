@@ -292,6 +292,40 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
       PCR_TRY(match_pairs(a, io, sv));
       continue;
     }
+#if defined(KNN_EXP) && KNN_EXP == 33
+    if (schedule == 6) {
+      // experiment: four whole-step pipelines, step s entirely on queue s % 4
+      // (extra workspaces allocated once here; rings of a multiple of 4)
+      static void* xk[2] = {nullptr, nullptr};
+      static void* xv = nullptr;
+      if (!xv) {
+        PCR_HIP(hipMalloc(&xk[0], a->knn_ws_bytes), "exp alloc");
+        PCR_HIP(hipMalloc(&xk[1], a->knn_ws_bytes), "exp alloc");
+        PCR_HIP(hipMalloc(&xv, a->vox_ws_bytes), "exp alloc");
+      }
+      const int i4 = s & 3;
+      const hipStream_t qs4[4] = {sn, sp, sv, org};
+      const hipStream_t qq = qs4[i4];
+      void* const kw = i4 < 2 ? a->knn_ws[i4] : xk[i4 - 2];
+      void* const vw4 = i4 < 2 ? a->vox_ws[i4] : (i4 == 2 ? a->vox_ws3 : xv);
+      pcr_extractor_args a2 = *a;
+      a2.knn_ws[0] = kw;
+      PCR_TRY(knn_sort(&a2, io, 0, qq, &sorted));
+      PCR_TRY(knn_select_ppf(&a2, io, 0, sorted, qq));
+      PCR_TRY(pcr_extractor_voxel_prep(io.xyz, a->b, a->n, a->r, io.norm_coords, io.ind,
+                                       io.dinds, io.dwgts, vw4, a->vox_ws_bytes, qq));
+      PCR_TRY(pcr_extractor_voxel_means_devox(io.features, a->b, a->c, a->n, a->r, io.devox,
+                                              io.dinds, io.dwgts, desc, vw4, a->vox_ws_bytes,
+                                              qq));
+      PCR_TRY(match_pairs(a, io, qq));
+      const bool timed = s >= t_first && s < t_first + rn->timed_last;
+      if (timed) PCR_HIP(hipEventRecord(rn->t0[s - t_first], qq), "timing record");
+      PCR_TRY(pcr_extractor_voxel_stream(a->b, a->c, a->n, a->r, io.cnt, io.grid, vw4,
+                                         a->vox_ws_bytes, qq));
+      if (timed) PCR_HIP(hipEventRecord(rn->t1[s - t_first], qq), "timing record");
+      continue;
+    }
+#endif
     if (schedule == 6) {
       // two independent pipelines per chain, no cross-queue events: the voxel
       // chain (prep, means / devox, match, grid stream) of step s on
@@ -305,33 +339,48 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
         PCR_HIP(hipStreamWaitEvent(vq, rv[2 * t], 0), "ring wait");
         PCR_HIP(hipStreamWaitEvent(kq, rv[2 * t + 1], 0), "ring wait");
       }
-      // the odd queues start half a chain behind the even ones: step 1's
-      // voxel chain waits for step 0's means (so one grid stream runs while
-      // the other queue does prep + means; aligned, the two grid streams
-      // fight for HBM and then leave it idle together)
-#if defined(KNN_EXP) && KNN_EXP == 31
-      if (s == 1) PCR_HIP(hipStreamWaitEvent(kq, sel_done[0], 0), "offset wait");
+      auto knn_part = [&]() -> pcr_status {
+#if defined(KNN_EXP) && KNN_EXP == 34
+        // experiment: the first two steps' KNN chains start after step 0's
+        // means, so the first grid stream gets the chip sooner
+        if (s <= 1) PCR_HIP(hipStreamWaitEvent(kq, means_done[0], 0), "head wait");
 #endif
-      PCR_TRY(knn_sort(a, io, q, kq, &sorted));
-      PCR_TRY(knn_select_ppf(a, io, q, sorted, kq));
-#if defined(KNN_EXP) && KNN_EXP == 31
-      if (s == 0) PCR_HIP(hipEventRecord(sel_done[0], kq), "offset record");
+        PCR_TRY(knn_sort(a, io, q, kq, &sorted));
+        return knn_select_ppf(a, io, q, sorted, kq);
+      };
+      auto vox_part = [&]() -> pcr_status {
+        // the odd queues start half a chain behind the even ones: step 1's
+        // voxel chain waits for step 0's means (so one grid stream runs while
+        // the other queue does prep + means; aligned, the two grid streams
+        // fight for HBM and then leave it idle together)
+        if (s == 1) PCR_HIP(hipStreamWaitEvent(vq, means_done[0], 0), "offset wait");
+        PCR_TRY(pcr_extractor_voxel_prep(io.xyz, a->b, a->n, a->r, io.norm_coords, io.ind,
+                                         io.dinds, io.dwgts, a->vox_ws[q], a->vox_ws_bytes,
+                                         vq));
+        PCR_TRY(pcr_extractor_voxel_means_devox(io.features, a->b, a->c, a->n, a->r, io.devox,
+                                                io.dinds, io.dwgts, desc, a->vox_ws[q],
+                                                a->vox_ws_bytes, vq));
+        if (s == 0) PCR_HIP(hipEventRecord(means_done[0], vq), "offset record");
+        PCR_TRY(match_pairs(a, io, vq));
+        const bool timed = s >= t_first && s < t_first + rn->timed_last;
+        if (timed) PCR_HIP(hipEventRecord(rn->t0[s - t_first], vq), "timing record");
+        PCR_TRY(pcr_extractor_voxel_stream(a->b, a->c, a->n, a->r, io.cnt, io.grid,
+                                           a->vox_ws[q], a->vox_ws_bytes, vq));
+        if (timed) PCR_HIP(hipEventRecord(rn->t1[s - t_first], vq), "timing record");
+        return PCR_OK;
+      };
+#if defined(KNN_EXP) && KNN_EXP == 34
+      if (s <= 1) {  // the head wait needs step 0's means recorded first
+        PCR_TRY(vox_part());
+        PCR_TRY(knn_part());
+      } else {
+        PCR_TRY(knn_part());
+        PCR_TRY(vox_part());
+      }
+#else
+      PCR_TRY(knn_part());
+      PCR_TRY(vox_part());
 #endif
-#if !defined(KNN_EXP) || KNN_EXP != 30
-      if (s == 1) PCR_HIP(hipStreamWaitEvent(vq, means_done[0], 0), "offset wait");
-#endif
-      PCR_TRY(pcr_extractor_voxel_prep(io.xyz, a->b, a->n, a->r, io.norm_coords, io.ind,
-                                       io.dinds, io.dwgts, a->vox_ws[q], a->vox_ws_bytes, vq));
-      PCR_TRY(pcr_extractor_voxel_means_devox(io.features, a->b, a->c, a->n, a->r, io.devox,
-                                              io.dinds, io.dwgts, desc, a->vox_ws[q],
-                                              a->vox_ws_bytes, vq));
-      if (s == 0) PCR_HIP(hipEventRecord(means_done[0], vq), "offset record");
-      PCR_TRY(match_pairs(a, io, vq));
-      const bool timed = s >= t_first && s < t_first + rn->timed_last;
-      if (timed) PCR_HIP(hipEventRecord(rn->t0[s - t_first], vq), "timing record");
-      PCR_TRY(pcr_extractor_voxel_stream(a->b, a->c, a->n, a->r, io.cnt, io.grid, a->vox_ws[q],
-                                         a->vox_ws_bytes, vq));
-      if (timed) PCR_HIP(hipEventRecord(rn->t1[s - t_first], vq), "timing record");
       if (rv && s + a->nsets < steps) {
         PCR_HIP(hipEventRecord(rv[2 * t], vq), "ring record");
         PCR_HIP(hipEventRecord(rv[2 * t + 1], kq), "ring record");

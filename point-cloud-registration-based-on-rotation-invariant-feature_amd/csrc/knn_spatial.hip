@@ -761,7 +761,10 @@ __global__ __launch_bounds__(KnnNW<KMAX>::wg * 64) void knn_block_kernel(
 // reference's result: the k lexicographically smallest (d, index) with
 // d < 10000, unfilled slots (10000, 0).
 constexpr int kNB = 24;
-constexpr int kCap = 88;
+#ifndef PCR_KNN_CAP
+#define PCR_KNN_CAP 88
+#endif
+constexpr int kCap = PCR_KNN_CAP;
 constexpr int kSelCache = 1024;  // candidates staged in LDS per workgroup
 constexpr int kSelMaxK = 32;
 constexpr int kCap64 = 112;  // the same selection for 32 < k <= 64 (large clouds): two workgroups per CU
