@@ -19,16 +19,22 @@ if len(sys.argv) > 2 and sys.argv[1] == "--report":
             if "knn_select" in r["Kernel_Name"]:
                 per[int(r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
     ids = sorted(per)
-    ids = ids[-2 * len(BITS):]
-    for i, bits in enumerate(BITS):
+    bits = BITS if len(ids) >= 2 * len(BITS) else (0,)
+    ids = ids[-2 * len(bits):]
+    for i, bv in enumerate(bits):
         cs = defaultdict(float)
         for d in ids[2 * i:2 * i + 2]:
             for c, v in per[d].items():
                 cs[c] += v / 2
-        print("dbg %d: " % bits + "  ".join("%s %.4g" % kv for kv in sorted(cs.items())))
+        print("dbg %d: " % bv + "  ".join("%s %.4g" % kv for kv in sorted(cs.items())))
     sys.exit(0)
 
-os.environ["PCR_AMD_LIB"] = os.path.join(PKG, "lib", "libpcr_amd_diag.so")
+# the diagnostic build (the PCR_KNN_DBG phase stops); PRODUCT=1: the product
+# library, whole launches only
+if os.environ.get("PRODUCT") == "1":
+    BITS = (0,)
+else:
+    os.environ["PCR_AMD_LIB"] = os.path.join(PKG, "lib", "libpcr_amd_diag.so")
 sys.path[:0] = [ROOT, PKG]
 import torch  # noqa: E402
 from pcr_amd.extractor import SphExtractor  # noqa: E402

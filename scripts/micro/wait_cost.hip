@@ -26,7 +26,7 @@ int main() {
   CK(hipMalloc(&buf, 4096));
   CK(hipMemset(buf, 0, 4096));
   unsigned* flag;
-  CK(hipExtMallocWithFlags((void**)&flag, 64, hipMallocSignalMemory));
+  CK(hipMalloc((void**)&flag, 64));
   CK(hipMemset(flag, 0, 64));
   hipEvent_t done, rec, t0, t1;
   CK(hipEventCreateWithFlags(&done, hipEventDisableTiming | hipEventDisableSystemFence));
