@@ -486,7 +486,9 @@ typedef struct pcr_extractor_args {
    * step's devox; outputs [P, n] (count [P]) as that function's. */
   int match_pairs;
   int *corr12, *corr21, *idx1, *idx2, *match_count;
-  void *match_ws;                         /* pcr_mutual_nn_workspace_size(P, n, n) */
+  void *match_ws;                         /* pcr_mutual_nn_workspace_size(P, n, n);
+                                             schedule 6: twice that + 512 B (one
+                                             half per voxel queue) */
   size_t match_ws_bytes;
   /* batch ring (see above): nsets sets, step s of the call uses set
    * (set0 + s) % nsets; nsets = 0: the single set above */

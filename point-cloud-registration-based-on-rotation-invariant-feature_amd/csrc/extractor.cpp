@@ -119,14 +119,22 @@ pcr_status knn_select_ppf(const pcr_extractor_args* a, const StepIO& io, int q, 
 }
 
 // the step's registration matching (source clouds [0, P) against targets
-// [P, 2P)) on the devox features the step just wrote
-pcr_status match_pairs(const pcr_extractor_args* a, const StepIO& io, hipStream_t st) {
+// [P, 2P)) on the devox features the step just wrote; half >= 0: schedule 6,
+// whose two voxel queues each match with their own half of the workspace
+pcr_status match_pairs(const pcr_extractor_args* a, const StepIO& io, hipStream_t st,
+                       int half = -1) {
   if (a->match_pairs <= 0) return PCR_OK;
   const int P = a->match_pairs;
   const float* src = io.devox;
   const float* tgt = io.devox + (size_t)P * a->c * a->n;
+  void* ws = a->match_ws;
+  size_t bytes = a->match_ws_bytes;
+  if (half >= 0) {
+    bytes = a->match_ws_bytes / 2 / 256 * 256;
+    ws = (char*)a->match_ws + (size_t)half * bytes;
+  }
   return pcr_mutual_nn_match_cm(src, tgt, P, a->n, a->n, a->c, io.corr12, io.corr21, io.idx1,
-                                io.idx2, io.match_count, a->match_ws, a->match_ws_bytes, st);
+                                io.idx2, io.match_count, ws, bytes, st);
 }
 
 }  // namespace
@@ -228,6 +236,13 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
   // distinct output sets (the c5 voxel path counts into cnt with atomics)
   PCR_REQUIRE(schedule != 6 || a->nsets >= 2,
               "extractor_run: schedule 6 needs a batch ring of at least two sets");
+  // schedule 6 matches consecutive steps on two queues at once: each half of
+  // the matching workspace must hold one matching
+  PCR_REQUIRE(schedule != 6 || a->match_pairs <= 0 ||
+                  a->match_ws_bytes / 2 / 256 * 256 >=
+                      pcr_mutual_nn_workspace_size(a->match_pairs, a->n, a->n),
+              "extractor_run: schedule 6 with match_pairs needs a matching workspace of "
+              "twice pcr_mutual_nn_workspace_size (plus 512 B)");
   PCR_REQUIRE(schedule < 4 || schedule == 6 || a->vox_ws3 != nullptr,
               "extractor_run: schedules 4 and 5 need the third voxel workspace (vox_ws3)");
   for (int q = 0; q < nslots; q++)
@@ -361,7 +376,7 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
                                                 io.dinds, io.dwgts, desc, a->vox_ws[q],
                                                 a->vox_ws_bytes, vq));
         if (s == 0) PCR_HIP(hipEventRecord(means_done[0], vq), "offset record");
-        PCR_TRY(match_pairs(a, io, vq));
+        PCR_TRY(match_pairs(a, io, vq, q));
         const bool timed = s >= t_first && s < t_first + rn->timed_last;
         if (timed) PCR_HIP(hipEventRecord(rn->t0[s - t_first], vq), "timing record");
         PCR_TRY(pcr_extractor_voxel_stream(a->b, a->c, a->n, a->r, io.cnt, io.grid,

@@ -39,7 +39,10 @@ class PairMatch:
         self.idx2 = torch.empty((pairs, npoints), **i32)
         self.count = torch.empty((pairs,), **i32)
         need = _lib.load().pcr_mutual_nn_workspace_size(pairs, npoints, npoints)
-        self.ws = torch.empty(max(256, need), dtype=torch.uint8, device=device)
+        # two halves: the runner's schedule 6 matches consecutive steps on
+        # two queues at once, each in its own half
+        half = (max(256, need) + 255) // 256 * 256
+        self.ws = torch.empty(2 * half + 512, dtype=torch.uint8, device=device)
 
     def outputs(self):
         return {"corr12": self.corr12, "corr21": self.corr21, "idx1": self.idx1,

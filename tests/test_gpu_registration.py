@@ -99,23 +99,26 @@ def _pair_batch(p, n, c, seed):
 @pytest.mark.parametrize("schedule", [1, 6])
 def test_pair_runner_batch_ring(dev, schedule):
     """BASELINE c4 over distinct pair batches (datasets/deepgmr_mn40.py:71-97,
-    a new pair per item): the native runner's batch ring, 3 batches of 2
-    pairs, 3 steps; every ring set's extractor outputs and matching against
-    the oracle of its batch."""
+    a new pair per item): the native runner's batch ring, 4 batches of 2
+    pairs, two calls of 4 steps (schedule 6 matches consecutive steps on two
+    queues at once, each in its own half of the matching workspace); after
+    each call every ring set's extractor outputs and matching against the
+    oracle of its batch."""
     from pcr_amd.registration import PairExtractor
     p, n, c, k, r = 2, 1024, 32, 32, 32
-    batches = [_pair_batch(p, n, c, 90 + i) for i in range(3)]
+    batches = [_pair_batch(p, n, c, 90 + i) for i in range(4)]
     tb = [tuple(T(a, dev) for a in bt) for bt in batches]
+    exp = [oracle_pair_step(*bt, k, r, p) for bt in batches]
     pe = PairExtractor(p, n, c, k, r, device=dev)
-    ring = pe.ex.ring_outputs(3, p)
-    for o in ring:
-        for t in o.values():
-            t.view(-1).view(torch.uint8).fill_(0xFF)
-    pe.run_ring(tb, 3, schedule=schedule)
-    torch.cuda.synchronize()
-    for i, bt in enumerate(batches):
-        exp = oracle_pair_step(*bt, k, r, p)
-        for key in ("knn_idx", "ind", "cnt", "grid", "devox", "desc"):
-            assert np.array_equal(N(ring[i][key]), exp[key]), (i, key)
-        for name, e in zip(("corr12", "corr21", "idx1", "idx2", "count"), exp["match"]):
-            assert np.array_equal(N(ring[i][name]), e), (i, name)
+    for call in range(2):
+        ring = pe.ex.ring_outputs(4, p)
+        for o in ring:
+            for t in o.values():
+                t.view(-1).view(torch.uint8).fill_(0xFF)
+        pe.run_ring(tb, 4, schedule=schedule)
+        torch.cuda.synchronize()
+        for i in range(4):
+            for key in ("knn_idx", "ind", "cnt", "grid", "devox", "desc"):
+                assert np.array_equal(N(ring[i][key]), exp[i][key]), (call, i, key)
+            for name, e in zip(("corr12", "corr21", "idx1", "idx2", "count"), exp[i]["match"]):
+                assert np.array_equal(N(ring[i][name]), e), (call, i, name)
