@@ -78,7 +78,7 @@ def parse(argv=None):
     ap.add_argument("--kernel-iters", type=int, default=50, help="(kept for old command lines)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--schedule", type=int, choices=(1, 2, 3, 4, 5, 6), default=6,
+    ap.add_argument("--schedule", type=int, choices=(1, 2, 3, 4, 5, 6, 7), default=6,
                     help="pcr_extractor_run schedule (include/pcr_amd.h): 1 = three streams "
                          "(sort+select+PPF / prep+means+devox / dense-grid stream), 2 = as 1 "
                          "with the Morton sort on the prep stream, 3 = as 1 with the local PPF "
@@ -86,7 +86,8 @@ def parse(argv=None):
                          "with three voxel workspaces and the grid stream alternating between "
                          "two queues, 5 = as 4 with the local PPF on the grid queues, 6 = two "
                          "independent pipelines per chain (voxel chain on s_vox / origin, KNN "
-                         "chain on s_nbr / s_pre by step parity), no cross-queue events")
+                         "chain on s_nbr / s_pre by step parity), no cross-queue events, 7 = as 6 "
+                         "with three voxel queues (s_vox / origin / s_pre) and one KNN queue")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="diagnostic: no timing events around the dominant kernel")
     ap.add_argument("--no-verify", action="store_true",
@@ -122,8 +123,10 @@ def parse(argv=None):
         args.batches = 8 if args.workload == "pairs" else 20
     if args.batches < 1:
         ap.error("--batches must be >= 1")
-    if args.schedule == 6 and args.batches < 2 and args.workload in ("extract", "pairs"):
-        ap.error("--schedule 6 needs --batches >= 2 (consecutive steps write distinct sets)")
+    if args.schedule >= 6 and args.batches < args.schedule - 4 and \
+            args.workload in ("extract", "pairs"):
+        ap.error("--schedule %d needs --batches >= %d (consecutive steps write distinct sets)"
+                 % (args.schedule, args.schedule - 4))
     if args.workload == "pairs" and args.batch % 2:
         ap.error("--workload pairs needs an even --batch (source + target clouds)")
     if args.gpus < 1:

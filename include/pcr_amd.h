@@ -422,6 +422,12 @@ pcr_status pcr_read_xyzn_txt(const char *path, float *out, long long rows, int c
  *               sets (consecutive steps write distinct sets); a ring of odd
  *               size that one call wraps orders each set's rewrite behind its
  *               previous step with per-set events (made on first use).
+ *   schedule 7: as 6 with three voxel queues (s_vox, origin, s_pre: voxel
+ *               workspaces vox_ws[0], vox_ws[1], vox_ws3) and one KNN queue
+ *               (s_nbr); needs a ring of >= 3 sets, per-set events when the
+ *               ring size is not a multiple of 3.  Schedules 6 / 7 with
+ *               match_pairs: each voxel queue matches in its own part (half
+ *               / third) of match_ws.
  * Buffers with two entries are the alternating sets (schedule 0 uses set 0).
  * desc_steps: [steps][b][c] per-step descriptors, or NULL (then desc).
  *

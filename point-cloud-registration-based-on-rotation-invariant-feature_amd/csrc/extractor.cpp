@@ -119,19 +119,19 @@ pcr_status knn_select_ppf(const pcr_extractor_args* a, const StepIO& io, int q, 
 }
 
 // the step's registration matching (source clouds [0, P) against targets
-// [P, 2P)) on the devox features the step just wrote; half >= 0: schedule 6,
-// whose two voxel queues each match with their own half of the workspace
+// [P, 2P)) on the devox features the step just wrote; nparts > 1: schedules
+// 6 / 7, whose voxel queues each match in their own part of the workspace
 pcr_status match_pairs(const pcr_extractor_args* a, const StepIO& io, hipStream_t st,
-                       int half = -1) {
+                       int part = 0, int nparts = 1) {
   if (a->match_pairs <= 0) return PCR_OK;
   const int P = a->match_pairs;
   const float* src = io.devox;
   const float* tgt = io.devox + (size_t)P * a->c * a->n;
   void* ws = a->match_ws;
   size_t bytes = a->match_ws_bytes;
-  if (half >= 0) {
-    bytes = a->match_ws_bytes / 2 / 256 * 256;
-    ws = (char*)a->match_ws + (size_t)half * bytes;
+  if (nparts > 1) {
+    bytes = a->match_ws_bytes / nparts / 256 * 256;
+    ws = (char*)a->match_ws + (size_t)part * bytes;
   }
   return pcr_mutual_nn_match_cm(src, tgt, P, a->n, a->n, a->c, io.corr12, io.corr21, io.idx1,
                                 io.idx2, io.match_count, ws, bytes, st);
@@ -219,7 +219,7 @@ extern "C" pcr_status pcr_runner_grid_times(pcr_runner* rn, float* ms, int cap, 
 extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_args* a,
                                         int steps, int schedule, float* desc_steps, void* origin,
                                         void* s_nbr_p, void* s_pre_p, void* s_vox_p) {
-  PCR_REQUIRE(a != nullptr && steps >= 0 && schedule >= 0 && schedule <= 6,
+  PCR_REQUIRE(a != nullptr && steps >= 0 && schedule >= 0 && schedule <= 7,
               "extractor_run: invalid arguments");
   PCR_REQUIRE(a->b >= 0 && a->n >= 1 && a->c >= 1 && a->k >= 1 && a->r >= 1,
               "extractor_run: invalid sizes");
@@ -232,21 +232,26 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
   const int nslots = schedule >= 1 ? 2 : 1;
   PCR_REQUIRE(a->nsets >= 0 && (a->nsets == 0 || (a->sets && schedule >= 1 && a->set0 >= 0)),
               "extractor_run: a batch ring needs sets, set0 >= 0 and schedule >= 1");
-  // schedule 6 writes consecutive steps from different queues: they need
-  // distinct output sets (the c5 voxel path counts into cnt with atomics)
-  PCR_REQUIRE(schedule != 6 || a->nsets >= 2,
-              "extractor_run: schedule 6 needs a batch ring of at least two sets");
-  // schedule 6 matches consecutive steps on two queues at once: each half of
-  // the matching workspace must hold one matching
-  PCR_REQUIRE(schedule != 6 || a->match_pairs <= 0 ||
-                  a->match_ws_bytes / 2 / 256 * 256 >=
+  // schedules 6 / 7: nvq voxel queues and nkq KNN queues, each running a
+  // whole chain of every nvq-th / nkq-th step
+  const int nvq = schedule == 7 ? 3 : 2, nkq = schedule == 7 ? 1 : 2;
+  const bool multi = schedule >= 6;
+  // consecutive steps are written from different queues: they need distinct
+  // output sets (the c5 voxel path counts into cnt with atomics)
+  PCR_REQUIRE(!multi || a->nsets >= nvq,
+              "extractor_run: schedule %d needs a batch ring of at least %d sets", schedule,
+              nvq);
+  // the voxel queues match at once: each part of the matching workspace
+  // must hold one matching
+  PCR_REQUIRE(!multi || a->match_pairs <= 0 ||
+                  a->match_ws_bytes / nvq / 256 * 256 >=
                       pcr_mutual_nn_workspace_size(a->match_pairs, a->n, a->n),
-              "extractor_run: schedule 6 with match_pairs needs a matching workspace of "
-              "twice pcr_mutual_nn_workspace_size (plus 512 B)");
+              "extractor_run: schedule %d with match_pairs needs a matching workspace of "
+              "%d x pcr_mutual_nn_workspace_size (plus 512 B)", schedule, nvq);
   PCR_REQUIRE(schedule < 4 || schedule == 6 || a->vox_ws3 != nullptr,
-              "extractor_run: schedules 4 and 5 need the third voxel workspace (vox_ws3)");
+              "extractor_run: schedules 4, 5 and 7 need the third voxel workspace (vox_ws3)");
   for (int q = 0; q < nslots; q++)
-    PCR_REQUIRE(a->vox_ws[q] && a->knn_ws[schedule >= 2 || schedule == 6 ? q : 0] &&
+    PCR_REQUIRE(a->vox_ws[q] && a->knn_ws[schedule >= 2 ? q : 0] &&
                     (a->nsets > 0 || (a->dinds[q] && a->dwgts[q])),
                 "extractor_run: buffer set %d missing", q);
   for (int t = 0; t < a->nsets; t++)
@@ -279,9 +284,11 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
   // schedule 4: three voxel workspaces (step s in s % 3) and the grid-stream
   // kernels of consecutive steps on alternating queues (s_vox, origin)
   void* const vws[3] = {a->vox_ws[0], a->vox_ws[1], a->vox_ws3};
-  // schedule 6 over an odd ring that one call wraps: per-set events, made
-  // once per ring size (the first call, outside any timed region)
-  const bool ring_wait = schedule == 6 && a->nsets > 0 && (a->nsets & 1) && steps > a->nsets;
+  // schedules 6 / 7 over a ring that one call wraps onto other queues
+  // (nsets not a multiple of the queue count): per-set events, made once
+  // per ring size (the first call, outside any timed region)
+  const bool ring_wait = multi && a->nsets > 0 && steps > a->nsets &&
+                         (a->nsets % nvq != 0 || a->nsets % nkq != 0);
   if (ring_wait && rn->ring_ev.size() != (size_t)(2 * a->nsets)) {
     for (hipEvent_t ev : rn->ring_ev)
       if (ev) (void)hipEventDestroy(ev);
@@ -307,47 +314,18 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
       PCR_TRY(match_pairs(a, io, sv));
       continue;
     }
-#if defined(KNN_EXP) && KNN_EXP == 33
-    if (schedule == 6) {
-      // experiment: four whole-step pipelines, step s entirely on queue s % 4
-      // (extra workspaces allocated once here; rings of a multiple of 4)
-      static void* xk[2] = {nullptr, nullptr};
-      static void* xv = nullptr;
-      if (!xv) {
-        PCR_HIP(hipMalloc(&xk[0], a->knn_ws_bytes), "exp alloc");
-        PCR_HIP(hipMalloc(&xk[1], a->knn_ws_bytes), "exp alloc");
-        PCR_HIP(hipMalloc(&xv, a->vox_ws_bytes), "exp alloc");
-      }
-      const int i4 = s & 3;
-      const hipStream_t qs4[4] = {sn, sp, sv, org};
-      const hipStream_t qq = qs4[i4];
-      void* const kw = i4 < 2 ? a->knn_ws[i4] : xk[i4 - 2];
-      void* const vw4 = i4 < 2 ? a->vox_ws[i4] : (i4 == 2 ? a->vox_ws3 : xv);
-      pcr_extractor_args a2 = *a;
-      a2.knn_ws[0] = kw;
-      PCR_TRY(knn_sort(&a2, io, 0, qq, &sorted));
-      PCR_TRY(knn_select_ppf(&a2, io, 0, sorted, qq));
-      PCR_TRY(pcr_extractor_voxel_prep(io.xyz, a->b, a->n, a->r, io.norm_coords, io.ind,
-                                       io.dinds, io.dwgts, vw4, a->vox_ws_bytes, qq));
-      PCR_TRY(pcr_extractor_voxel_means_devox(io.features, a->b, a->c, a->n, a->r, io.devox,
-                                              io.dinds, io.dwgts, desc, vw4, a->vox_ws_bytes,
-                                              qq));
-      PCR_TRY(match_pairs(a, io, qq));
-      const bool timed = s >= t_first && s < t_first + rn->timed_last;
-      if (timed) PCR_HIP(hipEventRecord(rn->t0[s - t_first], qq), "timing record");
-      PCR_TRY(pcr_extractor_voxel_stream(a->b, a->c, a->n, a->r, io.cnt, io.grid, vw4,
-                                         a->vox_ws_bytes, qq));
-      if (timed) PCR_HIP(hipEventRecord(rn->t1[s - t_first], qq), "timing record");
-      continue;
-    }
-#endif
-    if (schedule == 6) {
-      // two independent pipelines per chain, no cross-queue events: the voxel
-      // chain (prep, means / devox, match, grid stream) of step s on
-      // {s_vox, origin}[s & 1] with voxel workspace s & 1, the KNN chain
-      // (sort, selection, local PPF) on {s_nbr, s_pre}[s & 1] with KNN
-      // workspace s & 1; every workspace is reused only by its own queue
-      const hipStream_t vq = q ? org : sv, kq = q ? sp : sn;
+    if (multi) {
+      // independent pipelines per chain, no cross-queue events: the voxel
+      // chain (prep, means / devox, match, grid stream) of step s on voxel
+      // queue s % nvq with voxel workspace s % nvq, the KNN chain (sort,
+      // selection, local PPF) on KNN queue s % nkq with KNN workspace s % nkq;
+      // every workspace is reused only by its own queue.  Schedule 6: voxel
+      // queues {s_vox, origin}, KNN queues {s_nbr, s_pre}; schedule 7: voxel
+      // queues {s_vox, origin, s_pre}, KNN queue s_nbr
+      const hipStream_t vqs[3] = {sv, org, sp}, kqs[2] = {sn, sp};
+      const int iv = s % nvq, ik = s % nkq;
+      const hipStream_t vq = vqs[iv], kq = kqs[ik];
+      void* const vw6 = vws[iv];
       const int t = a->nsets > 0 ? (a->set0 + s) % a->nsets : 0;
       hipEvent_t* const rv = ring_wait ? rn->ring_ev.data() : nullptr;
       if (rv && s >= a->nsets) {  // set t last written on the other queues
@@ -355,47 +333,30 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
         PCR_HIP(hipStreamWaitEvent(kq, rv[2 * t + 1], 0), "ring wait");
       }
       auto knn_part = [&]() -> pcr_status {
-#if defined(KNN_EXP) && KNN_EXP == 34
-        // experiment: the first two steps' KNN chains start after step 0's
-        // means, so the first grid stream gets the chip sooner
-        if (s <= 1) PCR_HIP(hipStreamWaitEvent(kq, means_done[0], 0), "head wait");
-#endif
-        PCR_TRY(knn_sort(a, io, q, kq, &sorted));
-        return knn_select_ppf(a, io, q, sorted, kq);
+        PCR_TRY(knn_sort(a, io, ik, kq, &sorted));
+        return knn_select_ppf(a, io, ik, sorted, kq);
       };
       auto vox_part = [&]() -> pcr_status {
-        // the odd queues start half a chain behind the even ones: step 1's
-        // voxel chain waits for step 0's means (so one grid stream runs while
-        // the other queue does prep + means; aligned, the two grid streams
-        // fight for HBM and then leave it idle together)
-        if (s == 1) PCR_HIP(hipStreamWaitEvent(vq, means_done[0], 0), "offset wait");
+        // voxel queue i > 0 starts after step i - 1's means, so the queues'
+        // grid streams take turns rather than coincide (aligned, they fight
+        // for HBM and then leave it idle together)
+        if (s >= 1 && s < nvq) PCR_HIP(hipStreamWaitEvent(vq, means_done[s - 1], 0), "offset wait");
         PCR_TRY(pcr_extractor_voxel_prep(io.xyz, a->b, a->n, a->r, io.norm_coords, io.ind,
-                                         io.dinds, io.dwgts, a->vox_ws[q], a->vox_ws_bytes,
-                                         vq));
+                                         io.dinds, io.dwgts, vw6, a->vox_ws_bytes, vq));
         PCR_TRY(pcr_extractor_voxel_means_devox(io.features, a->b, a->c, a->n, a->r, io.devox,
-                                                io.dinds, io.dwgts, desc, a->vox_ws[q],
-                                                a->vox_ws_bytes, vq));
-        if (s == 0) PCR_HIP(hipEventRecord(means_done[0], vq), "offset record");
-        PCR_TRY(match_pairs(a, io, vq, q));
+                                                io.dinds, io.dwgts, desc, vw6, a->vox_ws_bytes,
+                                                vq));
+        if (s < nvq - 1) PCR_HIP(hipEventRecord(means_done[s], vq), "offset record");
+        PCR_TRY(match_pairs(a, io, vq, iv, nvq));
         const bool timed = s >= t_first && s < t_first + rn->timed_last;
         if (timed) PCR_HIP(hipEventRecord(rn->t0[s - t_first], vq), "timing record");
-        PCR_TRY(pcr_extractor_voxel_stream(a->b, a->c, a->n, a->r, io.cnt, io.grid,
-                                           a->vox_ws[q], a->vox_ws_bytes, vq));
+        PCR_TRY(pcr_extractor_voxel_stream(a->b, a->c, a->n, a->r, io.cnt, io.grid, vw6,
+                                           a->vox_ws_bytes, vq));
         if (timed) PCR_HIP(hipEventRecord(rn->t1[s - t_first], vq), "timing record");
         return PCR_OK;
       };
-#if defined(KNN_EXP) && KNN_EXP == 34
-      if (s <= 1) {  // the head wait needs step 0's means recorded first
-        PCR_TRY(vox_part());
-        PCR_TRY(knn_part());
-      } else {
-        PCR_TRY(knn_part());
-        PCR_TRY(vox_part());
-      }
-#else
       PCR_TRY(knn_part());
       PCR_TRY(vox_part());
-#endif
       if (rv && s + a->nsets < steps) {
         PCR_HIP(hipEventRecord(rv[2 * t], vq), "ring record");
         PCR_HIP(hipEventRecord(rv[2 * t + 1], kq), "ring record");

@@ -571,10 +571,11 @@ class SphExtractor:
         the current stream after it.  match: a
         registration.PairMatch (its workspace; the matching outputs go to
         the ring sets).  Returns the ring's output sets."""
-        if schedule not in (1, 2, 3, 4, 5, 6):
-            raise RuntimeError("run_ring needs schedule 1 to 6")
-        if schedule == 6 and len(batches) < 2:
-            raise RuntimeError("run_ring schedule 6 needs at least two batches")
+        if schedule not in (1, 2, 3, 4, 5, 6, 7):
+            raise RuntimeError("run_ring needs schedule 1 to 7")
+        if schedule >= 6 and len(batches) < schedule - 4:
+            raise RuntimeError("run_ring schedule %d needs at least %d batches"
+                               % (schedule, schedule - 4))
         R = len(batches)
         if R < 1:
             raise RuntimeError("run_ring needs at least one batch")

@@ -39,10 +39,10 @@ class PairMatch:
         self.idx2 = torch.empty((pairs, npoints), **i32)
         self.count = torch.empty((pairs,), **i32)
         need = _lib.load().pcr_mutual_nn_workspace_size(pairs, npoints, npoints)
-        # two halves: the runner's schedule 6 matches consecutive steps on
-        # two queues at once, each in its own half
-        half = (max(256, need) + 255) // 256 * 256
-        self.ws = torch.empty(2 * half + 512, dtype=torch.uint8, device=device)
+        # three parts: the runner's schedules 6 / 7 match consecutive steps
+        # on two / three queues at once, each in its own part
+        part = (max(256, need) + 255) // 256 * 256
+        self.ws = torch.empty(3 * part + 768, dtype=torch.uint8, device=device)
 
     def outputs(self):
         return {"corr12": self.corr12, "corr21": self.corr21, "idx1": self.idx1,

@@ -103,7 +103,7 @@ def test_extractor_native_runner(dev, schedule):
             assert all(0 < t < 100 for t in ms)
 
 
-@pytest.mark.parametrize("schedule", [1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("schedule", [1, 2, 3, 4, 5, 6, 7])
 def test_extractor_runner_batch_ring(dev, schedule):
     """pcr_extractor_run over a batch ring of 3 distinct batches (each with
     its own output set): one call of 3 steps, then a call of 5 steps that
@@ -137,25 +137,27 @@ def test_extractor_runner_batch_ring(dev, schedule):
         set0 = (set0 + steps) % 3
 
 
-def test_extractor_runner_schedule6_even_ring(dev):
-    """Schedule 6 (two independent pipelines per chain) over an even ring
-    that one call wraps twice (2 sets, 5 steps: set t is rewritten on the
-    same queue, no ring events), then over a 5-set ring with 7 steps (odd:
-    the rewrite runs on the other queue behind the per-set event).  The
-    single-set runner refuses schedule 6."""
+@pytest.mark.parametrize("schedule,rings", [(6, ((2, 5), (5, 7))), (7, ((3, 7), (4, 9)))])
+def test_extractor_runner_multi_queue_rings(dev, schedule, rings):
+    """Schedules 6 (two voxel + two KNN queues) and 7 (three voxel + one
+    KNN queue) over rings that one call wraps: a ring size that is a
+    multiple of the voxel queue count rewrites each set on its own queue (no
+    ring events: 2 sets x 5 steps, 3 x 7), another size on another queue
+    behind the per-set event (5 x 7, 4 x 9).  The single-set runner refuses
+    both, and a ring smaller than the voxel queue count is refused."""
     from pcr_amd.extractor import SphExtractor
     b, n, c, k, r = 4, 1024, 16, 32, 32
     batches = [gaussian_clouds(b, n, seed=110 + i, c=c) for i in range(5)]
     tb = [tuple(T(a, dev) for a in bt) for bt in batches]
     exp = [expected_step(*bt, k, r) for bt in batches]
     ex = SphExtractor(b, n, c, k, r, device=dev)
-    for R, steps in ((2, 5), (5, 7)):
+    for R, steps in rings:
         ring = ex.ring_outputs(R)
         for o in ring:
             for t in o.values():
                 t.view(-1).view(torch.uint8).fill_(0xFF)
         desc_steps = torch.full((steps, b, c), float("nan"), device=dev)
-        ex.run_ring(tb[:R], steps, 0, desc_steps, schedule=6)
+        ex.run_ring(tb[:R], steps, 0, desc_steps, schedule=schedule)
         torch.cuda.synchronize()
         for i in range(R):
             for key in ("knn_idx", "ind", "cnt", "dinds", "dwgts", "norm_coords", "grid",
@@ -166,9 +168,9 @@ def test_extractor_runner_schedule6_even_ring(dev):
         for s in range(steps):
             assert np.array_equal(N(desc_steps[s]), exp[s % R]["desc"]), (R, s)
     with pytest.raises(RuntimeError):
-        ex.run_native(*tb[0], 2, schedule=6)
+        ex.run_native(*tb[0], 2, schedule=schedule)
     with pytest.raises(RuntimeError):
-        ex.run_ring(tb[:1], 2, schedule=6)
+        ex.run_ring(tb[:schedule - 5], 2, schedule=schedule)
 
 
 def test_extractor_full_size_properties(dev):

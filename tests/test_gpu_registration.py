@@ -96,7 +96,7 @@ def _pair_batch(p, n, c, seed):
     return xyz.astype(np.float32), nrm.astype(np.float32), feat
 
 
-@pytest.mark.parametrize("schedule", [1, 6])
+@pytest.mark.parametrize("schedule", [1, 6, 7])
 def test_pair_runner_batch_ring(dev, schedule):
     """BASELINE c4 over distinct pair batches (datasets/deepgmr_mn40.py:71-97,
     a new pair per item): the native runner's batch ring, 4 batches of 2
