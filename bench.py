@@ -78,7 +78,7 @@ def parse(argv=None):
     ap.add_argument("--kernel-iters", type=int, default=50, help="(kept for old command lines)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--schedule", type=int, choices=(1, 2, 3, 4, 5, 6, 7), default=6,
+    ap.add_argument("--schedule", type=int, choices=(1, 2, 3, 4, 5, 6, 7), default=None,
                     help="pcr_extractor_run schedule (include/pcr_amd.h): 1 = three streams "
                          "(sort+select+PPF / prep+means+devox / dense-grid stream), 2 = as 1 "
                          "with the Morton sort on the prep stream, 3 = as 1 with the local PPF "
@@ -87,7 +87,8 @@ def parse(argv=None):
                          "two queues, 5 = as 4 with the local PPF on the grid queues, 6 = two "
                          "independent pipelines per chain (voxel chain on s_vox / origin, KNN "
                          "chain on s_nbr / s_pre by step parity), no cross-queue events, 7 = as 6 "
-                         "with three voxel queues (s_vox / origin / s_pre) and one KNN queue")
+                         "with three voxel queues (s_vox / origin / s_pre) and one KNN queue; default "
+                         "6 (extract), 7 (pairs: the matching lengthens the voxel chain)")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="diagnostic: no timing events around the dominant kernel")
     ap.add_argument("--no-verify", action="store_true",
@@ -121,6 +122,11 @@ def parse(argv=None):
         args.warmup = 3 if heavy else 40
     if args.batches is None:
         args.batches = 8 if args.workload == "pairs" else 20
+    if args.schedule is None:
+        # pairs: 250.5k vs 234.3k clouds/s with schedule 7 (the matching
+        # lengthens the voxel chain); extract: 381-395k with 6 against
+        # 305-319k with 7 (one KNN queue is then the critical chain)
+        args.schedule = 7 if args.workload == "pairs" else 6
     if args.batches < 1:
         ap.error("--batches must be >= 1")
     if args.schedule >= 6 and args.batches < args.schedule - 4 and \
