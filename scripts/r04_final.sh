@@ -20,7 +20,7 @@ run bench_pairs 300 python bench.py --workload pairs
 run bench_c3 300 python bench.py --workload c3
 run bench_c5 300 python bench.py --workload c5
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-run prof_c2 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c2 -o run --output-format csv -- python3 bench.py --steps 80 --warmup 40 --no-cpu-baseline
+run prof_c2 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c2 -o run --output-format csv -- python3 bench.py --steps 80 --warmup 40 --no-cpu-baseline --no-verify
 run prof_c3 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c3 -o run --output-format csv -- python3 bench.py --workload c3 --steps 10 --no-cpu-baseline
 run prof_c5 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c5 -o run --output-format csv -- python3 bench.py --workload c5 --steps 5 --no-cpu-baseline
 bash scripts/r04_pmc.sh
