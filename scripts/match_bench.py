@@ -23,9 +23,12 @@ for p, n, c in ((128, 1024, 64), (128, 1024, 512), (32, 1024, 512)):
     ws = torch.empty(lib.pcr_mutual_nn_workspace_size(p, n, n), dtype=torch.uint8, device=dev)
     s = torch.cuda.current_stream().cuda_stream
 
+    cm = os.environ.get("CM") == "1"  # channel-major [p][c][n] (the runner's matching)
+
     def run():
-        _lib.check(lib.pcr_mutual_nn_match(_ptr(f1), _ptr(f2), p, n, n, c, *[_ptr(o) for o in outs],
-                                           _ptr(ws), ws.numel(), s), "match")
+        fn = lib.pcr_mutual_nn_match_cm if cm else lib.pcr_mutual_nn_match
+        _lib.check(fn(_ptr(f1), _ptr(f2), p, n, n, c, *[_ptr(o) for o in outs],
+                      _ptr(ws), ws.numel(), s), "match")
     for _ in range(3):
         run()
     torch.cuda.synchronize()
@@ -36,5 +39,5 @@ for p, n, c in ((128, 1024, 64), (128, 1024, 512), (32, 1024, 512)):
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / it
     fl = 2.0 * p * n * n * c
-    print("p=%d n=%d c=%d: %.3f ms  %.0f pairs/s  %.1f TFLOP/s (%.0f%% of fp32 MFMA peak)"
-          % (p, n, c, dt * 1e3, p / dt, fl / dt / 1e12, 100 * fl / dt / PEAK), flush=True)
+    print("%sp=%d n=%d c=%d: %.3f ms  %.0f pairs/s  %.1f TFLOP/s (%.0f%% of fp32 MFMA peak)"
+          % ("cm " if cm else "", p, n, c, dt * 1e3, p / dt, fl / dt / 1e12, 100 * fl / dt / PEAK), flush=True)
