@@ -507,8 +507,10 @@ class C3Workload:
             res = self._backward(out, self.ev[s] if timed else None)
             if keep is not None:
                 keep.append(({kk: v.clone() for kk, v in out.items()}, res))
+        # prefetch: batch(s + 1) before step s's voxel side and consume; the
+        # bench's batch tensors are read-only, so that is allowed
         self.ex.pipelined_steps(steps, lambda s: self.inputs, consume,
-                                select_events=self.sev if timed else None)
+                                select_events=self.sev if timed else None, prefetch=True)
 
     def verify(self):
         """Three pipelined steps vs the serial forward + backwards: every

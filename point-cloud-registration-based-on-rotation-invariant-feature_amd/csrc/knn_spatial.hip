@@ -1656,6 +1656,510 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// knn_wsel_kernel (round 5): the self-KNN selection of clouds of <= 64 R
+// points, k <= 32, transposed -- one query per wave instruction, the cloud's
+// candidates in the lanes.  Lane l holds the Morton-sorted candidates
+// 64 r + l (r < R) in registers for the whole launch, so a query costs:
+//
+//  1. distances  its R distances per lane with the reference's FMA chain
+//                (knn.cu:20-23; two candidates per packed instruction);
+//  2. threshold  count(d <= t) over the wave is one v_cmp + s_bcnt1 per
+//                register (the count is a ballot across the lanes, so no
+//                per-pair atomic and no histogram).  t starts from the
+//                previous query's threshold (Morton neighbours have similar
+//                k-th distances) and moves by count ~ t^1.5 interpolation,
+//                bracketed, until k <= count <= 64: 1.5 passes on average;
+//  3. compact    the <= 64 keys with d <= t into one lane each (ballot +
+//                mbcnt slots in the wave's LDS row);
+//  4. sort       a 64-lane bitonic sort of 32-bit keys (d bits >> 5 << 6 |
+//                slot): DPP / swizzle partners, min / max / select per stage.
+//                Two keys whose truncated distances tie inside the first k
+//                send the query to the exact 64-bit sort, as do
+//  5. edge cases no t with k <= count <= 64 (exact duplicates, clusters):
+//                the exact k-th distance by bisection of its float bits, the
+//                tie at it broken by bisection of the original index, the
+//                exactly k members compacted and sorted on 64-bit keys.
+//
+// Result: the k lexicographically smallest (d, original index) with d <
+// 10000, unfilled slots index 0 -- the reference's insertion-sort result
+// (knn.cu:24-46).  Written as neighbour ids in sorted query order (KnnSet::
+// sidx rows, like knn_select_kernel's sorted_emit 1) through an LDS tile, so
+// every store is a whole 256-byte row.
+#ifndef PCR_WSEL_DEFAULT
+#define PCR_WSEL_DEFAULT 1  // A/B builds: 0 = the per-lane knn_select_kernel
+#endif
+constexpr int kWselChunk = 2;  // consecutive queries a wave takes at a time
+constexpr int kWselWaves = 8;  // waves per workgroup: one 64-query block
+constexpr int kWselCap = 64;   // keys collected per query (one per lane)
+constexpr int kWselTmax = 0x461C3FFF;  // bits of the largest float below 10000
+
+#ifdef PCR_WSEL_CSORT
+// One compare-exchange stage of the sort below on 31-bit keys (so partner -
+// x never overflows): t = partner - x, and the lower lane of the pair takes
+// the partner when t < 0, the upper lane when t > 0, i.e. when
+// (t ^ dir) < 0 with dir = 0 / -1 on lower / upper lanes: x += t & ((t ^
+// dir) >> 31).  Five plain VALU (the partner's DPP folds into the subtract),
+// no VCC / SGPR chain, so the compiler can interleave stages of two queries.
+__device__ inline unsigned wsel_ce(unsigned x, unsigned p, int dir) {
+  const int t = (int)(p - x);
+  return x + (unsigned)(t & ((t ^ dir) >> 31));
+}
+template <int CTRL>
+__device__ inline unsigned wsel_dpp(unsigned v) {
+  return (unsigned)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+}
+// lane ^ 4 / lane ^ 8 inside a 16-lane row: two bank-masked row shifts
+template <int SH>
+__device__ inline unsigned wsel_xrow(unsigned v) {
+  constexpr int lo_banks = SH == 4 ? 0x5 : 0x3;  // lanes that read lane + SH
+  const int a = __builtin_amdgcn_update_dpp(0, (int)v, 0x100 + SH, 0xF, lo_banks, false);
+  return (unsigned)__builtin_amdgcn_update_dpp(a, (int)v, 0x110 + SH, 0xF, 0xF ^ lo_banks, false);
+}
+// lane ^ 16 / lane ^ 32: gfx950's permlane swaps of a register with itself
+__device__ inline unsigned wsel_x16p(unsigned v) {
+  return __builtin_amdgcn_permlane16_swap(v, v, false, false)[0] |
+         0u;  // element 0: the first operand after the swap (rows swapped pairwise)
+}
+__device__ inline unsigned wsel_x32p(unsigned v) {
+  return __builtin_amdgcn_permlane32_swap(v, v, false, false)[0] | 0u;
+}
+
+// ascending 64-lane bitonic sort of unique 31-bit keys ("mirror" form: the
+// first stage of each merge compares i with its mirror i ^ (kk - 1), so every
+// block sorts ascending and the lower lane of a pair always keeps the min).
+// d[m] = 0 on the lanes with (lane & 2^m) == 0, else -1.
+__device__ inline unsigned wsel_sort64(unsigned x, const int (&d)[6]) {
+  constexpr int X1 = 0xB1, X2 = 0x4E, M4 = 0x1B, M8 = 0x141, M16 = 0x140;
+  x = wsel_ce(x, wsel_dpp<X1>(x), d[0]);
+  x = wsel_ce(x, wsel_dpp<M4>(x), d[1]);
+  x = wsel_ce(x, wsel_dpp<X1>(x), d[0]);
+  x = wsel_ce(x, wsel_dpp<M8>(x), d[2]);
+  x = wsel_ce(x, wsel_dpp<X2>(x), d[1]);
+  x = wsel_ce(x, wsel_dpp<X1>(x), d[0]);
+  x = wsel_ce(x, wsel_dpp<M16>(x), d[3]);
+  x = wsel_ce(x, wsel_xrow<4>(x), d[2]);
+  x = wsel_ce(x, wsel_dpp<X2>(x), d[1]);
+  x = wsel_ce(x, wsel_dpp<X1>(x), d[0]);
+  x = wsel_ce(x, wsel_x16p(wsel_dpp<M16>(x)), d[4]);  // mirror 32
+  x = wsel_ce(x, wsel_xrow<8>(x), d[3]);
+  x = wsel_ce(x, wsel_xrow<4>(x), d[2]);
+  x = wsel_ce(x, wsel_dpp<X2>(x), d[1]);
+  x = wsel_ce(x, wsel_dpp<X1>(x), d[0]);
+  x = wsel_ce(x, wsel_x32p(wsel_x16p(wsel_dpp<M16>(x))), d[5]);  // mirror 64
+  x = wsel_ce(x, wsel_x16p(x), d[4]);
+  x = wsel_ce(x, wsel_xrow<8>(x), d[3]);
+  x = wsel_ce(x, wsel_xrow<4>(x), d[2]);
+  x = wsel_ce(x, wsel_dpp<X2>(x), d[1]);
+  x = wsel_ce(x, wsel_dpp<X1>(x), d[0]);
+  return x;
+}
+
+#else
+// One compare-exchange stage of the sort below where the lower lanes of the
+// pairs are the even lanes (m = 1) or lanes 0-1 of each quad (m = 2): the
+// partner by DPP, folded into the compare and the select (2 VALU + 2 SALU):
+// the borrow of partner - x (v_sub_co: VOPC has no DPP form on gfx950) is vcc
+// = partner < x, flipped on the lanes that keep the minimum, then x = vcc ? x
+// : partner.  s_nop 1: the previous stage's VALU wrote x, which this DPP
+// reads (gfx9 needs 2 wait states).
+#define PCR_WSEL_VCC_STAGE(NAME, CTRL, LOW)                                        \
+  __device__ inline unsigned NAME(unsigned x) {                                    \
+    unsigned t;                                                                    \
+    asm volatile("s_nop 1\n\t"                                                     \
+                 "v_sub_co_u32_dpp %1, vcc, %0, %0 " CTRL " row_mask:0xf bank_mask:0xf\n\t" \
+                 "s_xor_b32 vcc_lo, vcc_lo, " LOW "\n\t"                           \
+                 "s_xor_b32 vcc_hi, vcc_hi, " LOW "\n\t"                           \
+                 "v_cndmask_b32_dpp %0, %0, %0, vcc " CTRL " row_mask:0xf bank_mask:0xf" \
+                 : "+v"(x), "=&v"(t)                                               \
+                 :                                                                 \
+                 : "vcc");                                                         \
+    return x;                                                                      \
+  }
+PCR_WSEL_VCC_STAGE(wsel_x1, "quad_perm:[1,0,3,2]", "0x55555555")
+PCR_WSEL_VCC_STAGE(wsel_x2, "quad_perm:[2,3,0,1]", "0x33333333")
+PCR_WSEL_VCC_STAGE(wsel_m4, "quad_perm:[3,2,1,0]", "0x33333333")
+#undef PCR_WSEL_VCC_STAGE
+// Stages whose lower lanes are whole 4-lane banks of a row (m = 4, 8) or whole
+// rows (m = 16, 32): the DPP bank / row masks pick the lanes, so the lower
+// lanes write min(partner, x) and the upper lanes max(partner, x) into a new
+// register with two masked VALU -- no VCC, no SALU.  LO / HI are the
+// partner's DPP controls for the lower / upper lanes, MLO / MHI their masks.
+#define PCR_WSEL_MINMAX_STAGE(NAME, LO, HI, MLO, MHI)                              \
+  __device__ inline unsigned NAME(unsigned x) {                                    \
+    unsigned a;                                                                    \
+    asm volatile("s_nop 1\n\t"                                                     \
+                 "v_min_u32_dpp %0, %1, %1 " LO " " MLO "\n\t"                     \
+                 "v_max_u32_dpp %0, %1, %1 " HI " " MHI                            \
+                 : "=&v"(a)                                                        \
+                 : "v"(x));                                                        \
+    return a;                                                                      \
+  }
+PCR_WSEL_MINMAX_STAGE(wsel_m8, "row_half_mirror", "row_half_mirror",
+                      "row_mask:0xf bank_mask:0x5", "row_mask:0xf bank_mask:0xa")
+PCR_WSEL_MINMAX_STAGE(wsel_m16, "row_mirror", "row_mirror",
+                      "row_mask:0xf bank_mask:0x3", "row_mask:0xf bank_mask:0xc")
+PCR_WSEL_MINMAX_STAGE(wsel_x4, "row_shl:4", "row_shr:4",
+                      "row_mask:0xf bank_mask:0x5", "row_mask:0xf bank_mask:0xa")
+PCR_WSEL_MINMAX_STAGE(wsel_x8, "row_shl:8", "row_shr:8",
+                      "row_mask:0xf bank_mask:0x3", "row_mask:0xf bank_mask:0xc")
+#undef PCR_WSEL_MINMAX_STAGE
+// Cross-row partners (FETCH into %2): lane ^ 16 / lane ^ 32 from gfx950's
+// v_permlane16_swap / v_permlane32_swap of a register with itself, the 32- and
+// 64-lane mirrors from a row mirror plus those swaps; then the row-masked
+// min / max (identity DPP: only its row mask matters).  No LDS round trip.
+#define PCR_WSEL_ROW_STAGE(NAME, FETCH, RLO, RHI)                                  \
+  __device__ inline unsigned NAME(unsigned x) {                                    \
+    unsigned a, p;                                                                 \
+    asm volatile("s_nop 1\n\t" FETCH                                               \
+                 "s_nop 1\n\t"                                                     \
+                 "v_min_u32_dpp %0, %1, %2 quad_perm:[0,1,2,3] row_mask:" RLO " bank_mask:0xf\n\t" \
+                 "v_max_u32_dpp %0, %1, %2 quad_perm:[0,1,2,3] row_mask:" RHI " bank_mask:0xf" \
+                 : "=&v"(a), "+v"(x), "=&v"(p)                                     \
+                 :);                                                               \
+    return a;                                                                      \
+  }
+PCR_WSEL_ROW_STAGE(wsel_x16,
+                   "v_mov_b32_e32 %2, %1\n\t"
+                   "s_nop 1\n\t"
+                   "v_permlane16_swap_b32 %2, %2\n\t",
+                   "0x5", "0xa")
+PCR_WSEL_ROW_STAGE(wsel_m32,
+                   "v_mov_b32_dpp %2, %1 row_mirror row_mask:0xf bank_mask:0xf\n\t"
+                   "s_nop 1\n\t"
+                   "v_permlane16_swap_b32 %2, %2\n\t",
+                   "0x5", "0xa")
+PCR_WSEL_ROW_STAGE(wsel_m64,
+                   "v_mov_b32_dpp %2, %1 row_mirror row_mask:0xf bank_mask:0xf\n\t"
+                   "s_nop 1\n\t"
+                   "v_permlane16_swap_b32 %2, %2\n\t"
+                   "s_nop 1\n\t"
+                   "v_permlane32_swap_b32 %2, %2\n\t",
+                   "0x3", "0xc")
+#undef PCR_WSEL_ROW_STAGE
+
+// ascending 64-lane bitonic sort ("mirror" form: the first stage of each
+// merge compares i with its mirror i ^ (kk - 1), so every block sorts
+// ascending and the lower lane of a pair always keeps the minimum)
+__device__ inline unsigned wsel_sort64(unsigned x, const int (&)[6]) {
+  x = wsel_x1(x);
+  x = wsel_m4(x);
+  x = wsel_x1(x);
+  x = wsel_m8(x);
+  x = wsel_x2(x);
+  x = wsel_x1(x);
+  x = wsel_m16(x);
+  x = wsel_x4(x);
+  x = wsel_x2(x);
+  x = wsel_x1(x);
+  x = wsel_m32(x);
+  x = wsel_x8(x);
+  x = wsel_x4(x);
+  x = wsel_x2(x);
+  x = wsel_x1(x);
+  x = wsel_m64(x);
+  x = wsel_x16(x);
+  x = wsel_x8(x);
+  x = wsel_x4(x);
+  x = wsel_x2(x);
+  x = wsel_x1(x);
+  // the caller's next DPP read of x follows a VALU write inside the asm above,
+  // which the compiler's hazard tracking does not see
+  asm volatile("s_nop 1");
+  return x;
+}
+#endif
+
+// the same on 64-bit keys (d bits << 32 | original index): exact, rare
+__device__ inline unsigned long long wsel_sort64_exact(unsigned long long x, int lane) {
+  for (int kk = 2; kk <= 64; kk <<= 1) {
+    for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+      const int m = jj == (kk >> 1) ? kk - 1 : jj;  // mirror first, then half-cleaners
+      const unsigned long long p = shfl_xor_u64(x, m);
+      const bool lower = (lane & jj) == 0;
+      x = lower ? (x < p ? x : p) : (x < p ? p : x);
+    }
+  }
+  return x;
+}
+
+// Appends the keys of the lanes in `m` (a ballot mask) to the wave's LDS
+// rows at slots base, base + 1, ...: d bits to kd, index to kd + 2048 bytes.
+// exec = m for three VALU (the slot: mbcnt lo / hi; the address) and two
+// ds_write, restored after: no per-lane condition is materialised.
+__device__ inline void wsel_append(unsigned long long m, unsigned addr, unsigned d, int j) {
+  unsigned t;
+  unsigned long long save;
+  asm volatile(
+      "s_mov_b64 %1, exec\n\t"
+      "s_mov_b64 exec, %2\n\t"
+      "v_mbcnt_lo_u32_b32 %0, %3, 0\n\t"
+      "v_mbcnt_hi_u32_b32 %0, %4, %0\n\t"
+      "v_lshl_add_u32 %0, %0, 2, %5\n\t"
+      "ds_write_b32 %0, %6\n\t"
+      "ds_write_b32 %0, %7 offset:2048\n\t"
+      "s_mov_b64 exec, %1"
+      : "=&v"(t), "=&s"(save)
+      : "s"(m), "s"((unsigned)m), "s"((unsigned)(m >> 32)), "s"(addr), "v"(d), "v"(j)
+      : "memory");
+}
+
+template <int R>
+__global__ __launch_bounds__(kWselWaves * 64) void knn_wsel_kernel(KnnSet s, int k) {
+  // [0][wave][slot] collected d bits, [1][wave][slot] their original indices
+  // (2048 bytes apart: wsel_append's ds_write offset)
+  __shared__ unsigned kbuf_s[2][kWselWaves][kWselCap];
+  __shared__ int tile_s[kBlk][kSortedK + 1];  // output ids [query][slot] (padded: no bank conflicts)
+  __shared__ int qnext_s;                     // the next chunk of the block's queries
+  static_assert(sizeof(kbuf_s[0]) == 2048, "wsel_append's offset");
+  const int b = blockIdx.y, qblk = blockIdx.x;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const size_t cb = (size_t)b * s.npad;
+  const int nr = s.npad / kBlk;  // candidate registers in use (<= R)
+#ifdef PCR_DIAG
+  if (threadIdx.x == 0 && PCR_WG_LINEAR < 1023) {
+    pcr_diag_stamps[PCR_WG_LINEAR][12] = __builtin_amdgcn_s_memrealtime();
+    pcr_diag_stamps[PCR_WG_LINEAR][0] = __builtin_amdgcn_s_memtime();
+  }
+#endif
+  typedef float pf2v __attribute__((ext_vector_type(2)));
+  // the whole cloud, one candidate per lane and register (NaN / -1 padding)
+  pf2v cx[R / 2], cy[R / 2], cz[R / 2];
+  int cj[R];
+#pragma unroll
+  for (int h = 0; h < R / 2; h++) {
+    float v[2][3];
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+      // unconditional loads (a register past the cloud re-reads its last
+      // block, then reads as NaN / -1): no branch, so all are in flight at once
+      const int r = 2 * h + e;
+      const bool ok = r < nr;
+      const size_t p = cb + (size_t)(ok ? r : nr - 1) * kBlk + lane;
+      const float x = s.x[p], y = s.y[p], z = s.z[p];
+      const int j = s.j[p];
+      v[e][0] = ok ? x : __builtin_nanf("");
+      v[e][1] = ok ? y : __builtin_nanf("");
+      v[e][2] = ok ? z : __builtin_nanf("");
+      cj[r] = ok ? j : -1;
+    }
+    cx[h] = pf2v{v[0][0], v[1][0]};
+    cy[h] = pf2v{v[0][1], v[1][1]};
+    cz[h] = pf2v{v[0][2], v[1][2]};
+  }
+  // the block's 64 queries, one per lane (every wave holds all of them: the
+  // waves take chunks of kWselChunk consecutive queries from an LDS counter,
+  // so a wave that drew expensive queries -- outliers, extra passes -- takes
+  // fewer chunks and the workgroup ends with its mean, not its slowest wave)
+  const size_t pq = cb + (size_t)qblk * kBlk + lane;
+  const float qxl = s.x[pq], qyl = s.y[pq], qzl = s.z[pq];
+  const int qjl = s.j[pq];
+  if (threadIdx.x == 0) qnext_s = 0;
+  __syncthreads();
+  auto grab = [&]() {
+    int v = 0;
+    if (lane == 0)
+      v = __hip_atomic_fetch_add(&qnext_s, kWselChunk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return v;
+  };
+  int q0 = __builtin_amdgcn_readfirstlane(grab());
+  // first guess: the largest distance from the wave's first query to its own
+  // block's box (>= the k-th when the block holds k points), else 10000-
+  int tb = kWselTmax;
+  if (q0 < kBlk) {
+    const float* bx = s.box + ((size_t)b * s.nblk + qblk) * 8;
+    const float qx = readlane_f(qxl, q0), qy = readlane_f(qyl, q0), qz = readlane_f(qzl, q0);
+    if (min(kBlk, s.n - qblk * kBlk) >= k) {
+      const float u = box_ub(qx, qy, qz, bx);
+      if (u < PCR_KNN_UNDEF) tb = (int)__float_as_uint(u);
+    }
+  }
+#ifdef PCR_DIAG
+  if (threadIdx.x == 0 && PCR_WG_LINEAR < 1023) pcr_diag_stamps[PCR_WG_LINEAR][1] = __builtin_amdgcn_s_memtime();
+  int dg_exact = 0, dg_slow = 0, dg_keys = 0, dg_pass = 0;
+#endif
+  unsigned* kd = kbuf_s[0][wv];
+  int* kj = (int*)kbuf_s[1][wv];
+  const unsigned kd_addr =  // LDS byte address of the wave's rows
+      (unsigned)(uintptr_t)((__attribute__((address_space(3))) unsigned*)kd);
+  const float tgt = 0.5f * (float)(k + kWselCap);
+  int sdir[6];  // the sort's lane directions: 0 where lane & 2^m is clear, else -1
+#pragma unroll
+  for (int m = 0; m < 6; m++) sdir[m] = (lane >> m) & 1 ? -1 : 0;
+#ifdef PCR_DIAG
+  unsigned long long ph[6] = {0, 0, 0, 0, 0, 0}, pt = 0;
+#define WSEL_PHASE(i)                                                    \
+  do {                                                                   \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime();        \
+    if ((i) > 0) ph[(i) - 1] += now_ - pt;                               \
+    pt = now_;                                                           \
+  } while (0)
+#else
+#define WSEL_PHASE(i) \
+  do {                \
+  } while (0)
+#endif
+#pragma unroll 1
+  for (int qi = q0; qi < kBlk;) {
+    WSEL_PHASE(0);
+    const int qj = __builtin_amdgcn_readlane(qjl, qi);
+    if (qj < 0) {
+      if (lane < kSortedK) tile_s[qi][lane] = 0;
+      if (++qi % kWselChunk == 0) qi = __builtin_amdgcn_readfirstlane(grab());
+      continue;
+    }
+    const float qx = readlane_f(qxl, qi), qy = readlane_f(qyl, qi), qz = readlane_f(qzl, qi);
+    const pf2v qx2 = {qx, qx}, qy2 = {qy, qy}, qz2 = {qz, qz};
+    // 1. distances, knn.cu:20-23's chain
+    unsigned db[R];
+#pragma unroll
+    for (int h = 0; h < R / 2; h++) {
+      const pf2v a = qx2 - cx[h], bq = qy2 - cy[h], c = qz2 - cz[h];
+      pf2v d = a * a;
+      d = __builtin_elementwise_fma(bq, bq, d);
+      d = __builtin_elementwise_fma(c, c, d);
+      db[2 * h] = __float_as_uint(d[0]);
+      db[2 * h + 1] = __float_as_uint(d[1]);
+    }
+    WSEL_PHASE(1);
+    // 2. threshold: count(d <= t) by ballots (NaN bits compare above every t)
+    unsigned long long msk[R];
+    auto count_le = [&](int bits) {
+      int c = 0;
+#pragma unroll
+      for (int r = 0; r < R; r++) {
+        msk[r] = __ballot(db[r] <= (unsigned)bits);
+        c += __popcll(msk[r]);
+      }
+      return c;
+    };
+    int lo = -1, hi = 0x7F800000, cnt_lo = 0, cnt = 0;
+    bool exact = false;
+#pragma unroll 1
+    for (int pass = 0;; pass++) {
+      cnt = count_le(tb);
+      if (cnt >= k && cnt <= kWselCap) break;
+#ifdef PCR_DIAG
+      dg_pass++;
+#endif
+      if (cnt < k) {
+        lo = tb;
+        cnt_lo = cnt;
+        if (tb >= kWselTmax) break;  // fewer than k candidates below 10000: all of them
+      } else {
+        hi = tb;
+      }
+      if (hi - lo <= 1) {  // more than 64 - cnt_lo keys tie at distance bits hi
+        exact = true;
+        break;
+      }
+      int nb;
+      if (pass < 3) {
+        // count ~ t^1.5 near the k-th distance (smooth clouds: ~1.6 passes)
+        const float f = __uint_as_float((unsigned)tb) *
+                        __builtin_exp2f(0.6666667f * __builtin_log2f(
+                                                         tgt * __builtin_amdgcn_rcpf((float)max(cnt, 1))));
+        nb = f < 1e30f ? (int)__float_as_uint(f) : kWselTmax;
+      } else {
+        // steep counts (an outlier facing the bulk): bisect the bracket's bits
+        nb = lo + ((hi - lo) >> 1);
+      }
+      nb = min(nb, kWselTmax);
+      if (nb <= lo || nb >= hi) nb = lo + ((hi - lo) >> 1);
+      tb = __builtin_amdgcn_readfirstlane(nb);
+    }
+    WSEL_PHASE(2);
+    int ntake;
+    if (!exact) {
+      // 3. compact the cnt <= 64 keys with d <= t (the last pass's ballots)
+      unsigned addr = kd_addr;
+#pragma unroll
+      for (int r = 0; r < R; r++) {
+        if (msk[r] != 0ull) {
+          wsel_append(msk[r], addr, db[r], cj[r]);
+          addr += 4u * (unsigned)__popcll(msk[r]);
+        }
+      }
+      ntake = cnt;
+    } else {
+      // 5. ties: every key below distance bits hi (cnt_lo < k of them), then
+      // the need = k - cnt_lo smallest indices among those at exactly hi
+      const int need = k - cnt_lo;
+      int jl = -1, jh = s.n - 1;
+#pragma unroll 1
+      while (jh - jl > 1) {
+        const int jm = jl + ((jh - jl) >> 1);
+        int c = 0;
+#pragma unroll
+        for (int r = 0; r < R; r++) c += __popcll(__ballot(db[r] == (unsigned)hi && cj[r] <= jm));
+        if (c >= need) jh = jm;
+        else jl = jm;
+      }
+      unsigned addr = kd_addr;
+#pragma unroll
+      for (int r = 0; r < R; r++) {
+        const unsigned long long m =
+            __ballot(db[r] < (unsigned)hi || (db[r] == (unsigned)hi && cj[r] <= jh));
+        if (m != 0ull) {
+          wsel_append(m, addr, db[r], cj[r]);
+          addr += 4u * (unsigned)__popcll(m);
+        }
+      }
+      ntake = k;
+    }
+    WSEL_PHASE(3);
+    // 4. sort 31-bit keys: d bits >> 6 (25 bits: d < 10000) and the slot as payload
+    const unsigned dl = lane < ntake ? kd[lane] : 0xFFFFFFFFu;
+    unsigned key = lane < ntake ? ((dl >> 6) << 6) | (unsigned)lane : 0x7FFFFFFFu;
+    key = wsel_sort64(key, sdir);
+    WSEL_PHASE(4);
+    // a truncated-distance tie among the first k (or at the k-th) needs the
+    // exact order (lane i sees lane i + 1: DPP wave_shl:1)
+    const unsigned nxt = (unsigned)__builtin_amdgcn_mov_dpp((int)key, 0x130, 0xF, 0xF, false);
+    const bool tie = lane < k && lane + 1 < ntake && (key >> 6) == (nxt >> 6);
+    const bool slow = __any(tie);
+#ifdef PCR_DIAG
+    dg_exact += exact ? 1 : 0;
+    dg_slow += slow ? 1 : 0;
+    dg_keys += ntake;
+#endif
+    if (!slow) {
+      const int jo = lane < ntake ? kj[key & 63u] : 0;
+      if (lane < k) tile_s[qi][lane] = jo;
+    } else {
+      unsigned long long skey = ~0ull;
+      if (lane < ntake) skey = ((unsigned long long)kd[lane] << 32) | (unsigned)kj[lane];
+      skey = wsel_sort64_exact(skey, lane);
+      if (lane < k) tile_s[qi][lane] = lane < ntake ? (int)(unsigned)(skey & 0xFFFFFFFFull) : 0;
+    }
+    // the rows are read before the next query's appends rewrite them (LDS
+    // operations of a wave complete in order; this keeps the compiler's order)
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    WSEL_PHASE(5);
+    if (++qi % kWselChunk == 0) qi = __builtin_amdgcn_readfirstlane(grab());
+  }
+#undef WSEL_PHASE
+#ifdef PCR_DIAG
+  if (lane == 0 && PCR_WG_LINEAR < 1023) pcr_diag_stamps[PCR_WG_LINEAR][4 + wv] = __builtin_amdgcn_s_memtime();
+  // per-wave path counts: (exact << 48 | slow << 32 | passes << 16 | keys / 8), read back by
+  // scripts/wsel_diag.py (no atomics: a shared counter would queue every wave's exit)
+  if (lane == 0 && PCR_WG_LINEAR < 1023)
+    pcr_diag_wave[PCR_WG_LINEAR][wv][0] = ((unsigned long long)dg_exact << 48) |
+                                          ((unsigned long long)dg_slow << 32) |
+                                          ((unsigned long long)dg_pass << 16) | (unsigned)(dg_keys / 8);
+  if (lane == 0 && PCR_WG_LINEAR < 1023)
+    for (int i = 0; i < 5; i++) pcr_diag_wave[PCR_WG_LINEAR][wv][1 + i] = ph[i];
+#endif
+  __syncthreads();
+#ifdef PCR_DIAG
+  if (threadIdx.x == 0 && PCR_WG_LINEAR < 1023)
+    pcr_diag_stamps[PCR_WG_LINEAR][13] = __builtin_amdgcn_s_memrealtime();
+#endif
+  for (int sl = wv; sl < k; sl += kWselWaves)
+    s.sidx[((size_t)b * kSortedK + sl) * s.npad + (size_t)qblk * kBlk + lane] = tile_s[lane][sl];
+}
+
 // Un-permutes the selection's sorted-order keys (qs.skey, sorted_emit 2)
 // into the reference's [b][k][n] outputs (knn/knn.cu:40-47 layout) and
 // computes the local PPF of every (query, slot) on the way
@@ -1921,6 +2425,11 @@ pcr_status knn_spatial(const float* xyz1, const float* xyz2, int b, int n, int m
     if (!self || ppf1 || dist1 || idx2 || k > kSortedK || k > kSelMaxK || s1.sidx == nullptr ||
         s1.npad > 2 * kSelCache)
       return PCR_ERR_UNSUPPORTED;
+    if (s1.npad <= 16 * kBlk && PCR_KNOB("PCR_KNN_WSEL", PCR_WSEL_DEFAULT)) {
+      hipLaunchKernelGGL((knn_wsel_kernel<16>), dim3(s1.nblk, b), dim3(kWselWaves * 64), 0, st, s1,
+                         k);
+      return PCR_OK;
+    }
     return launch_block<false>(s1, c1, b, k, nullptr, idx1, nullptr, nullptr, nullptr, nullptr,
                                0, nullptr, st, 1);
   }

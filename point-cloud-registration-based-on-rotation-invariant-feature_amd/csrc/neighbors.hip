@@ -893,8 +893,15 @@ extern "C" pcr_status pcr_knn_backward(const float* xyz1, const float* xyz2,
   return launch_status("knn_backward");
 }
 
+// clouds past the LDS counters (or empty ones) take the atomic kernel, which
+// needs no workspace
+static bool knn_bwd_sorted_applies(int n, int m, int k) {
+  return !(n > kKnnBwdMaxT || m > kKnnBwdMaxT || n == 0 || m == 0 ||
+           (size_t)k * (n > m ? n : m) >= (1u << 31));
+}
+
 extern "C" size_t pcr_knn_backward_workspace_size(int b, int n, int m, int k) {
-  if (b <= 0 || n < 0 || m < 0 || k <= 0) return 256;
+  if (b <= 0 || n < 0 || m < 0 || k <= 0 || !knn_bwd_sorted_applies(n, m, k)) return 256;
   return knn_bwd_ws_layout(b, n, m, k, nullptr, nullptr);
 }
 
@@ -908,8 +915,7 @@ extern "C" pcr_status pcr_knn_backward_ws(const float* xyz1, const float* xyz2,
               "knn_backward_ws: invalid sizes");
   if (b == 0) return PCR_OK;
   // clouds past the LDS counters: the atomic kernel (same contract)
-  if (n > kKnnBwdMaxT || m > kKnnBwdMaxT || n == 0 || m == 0 ||
-      (size_t)k * (n > m ? n : m) >= (1u << 31))
+  if (!knn_bwd_sorted_applies(n, m, k))
     return pcr_knn_backward(xyz1, xyz2, graddist1, graddist2, idx1, idx2, b, c, n, m, k,
                             gradxyz1, gradxyz2, stream);
   KnnBwdWs ws;

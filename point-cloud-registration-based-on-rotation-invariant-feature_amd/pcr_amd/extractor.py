@@ -152,12 +152,20 @@ class SphExtractor:
                 return
             if rs != -3:  # PCR_ERR_UNSUPPORTED: nothing launched
                 _lib.check(rs, "knn_select_sorted")
+            # the sorted path does not apply: the events are recorded again
+            # around the fallback below (its selection + PPF), so they never
+            # read ~0 for a launch that ran outside them
+            ev0.record(torch_stream)
+        else:
+            events = None
         if self.split_ppf and ppf and self.knn_dist is None:
             # selection in sorted query order + the PPF launch that writes
             # knn_idx and the PPF (pcr_knn_select_ppf)
             _lib.check(lib.pcr_knn_select_ppf(
                 _ptr(xyz), _ptr(normals), self.b, self.n, self.k, int(self.relative), _ptr(idx),
                 _ptr(ppf_out), _ptr(kws), kws.numel(), stream), "knn_select_ppf")
+            if events is not None:
+                events[1].record(torch_stream)
             return
         _lib.check(lib.pcr_knn_local_ppf_prepared(
             _ptr(xyz), _ptr(normals), self.b, self.n, self.k, int(self.relative),
@@ -338,7 +346,7 @@ class SphExtractor:
         else:
             self.voxel_devox(features, stream, desc, slot)
 
-    def pipelined_steps(self, steps, batch, consume, select_events=None):
+    def pipelined_steps(self, steps, batch, consume, select_events=None, prefetch=False):
         """`steps` train steps whose neighbour side runs one batch ahead.
 
         A batch's self-KNN + local PPF depend on its coordinates and normals
@@ -355,14 +363,21 @@ class SphExtractor:
         every step's neighbours, voxels and consume run once.
 
         batch(s) may make its tensors on the caller's stream (an H2D copy as
-        in train.py:140, an augmentation, the LRF change_coords): batch(s+1)
-        is called right after step s's neighbours are enqueued, before step
-        s's voxel side and consume, and s_nbr waits for an event recorded on
-        the caller's stream right after it, so batch s+1's neighbours are
-        ordered after its producers but neither after step s's voxel side
-        nor after consume(s) -- the overlap stays.  xyz and
-        normals are record_stream'ed to s_nbr, so the caching allocator does
-        not hand their blocks out while s_nbr still reads them.
+        in train.py:140, an augmentation, the LRF change_coords); s_nbr waits
+        for an event recorded on the caller's stream right after it, so a
+        batch's neighbours are ordered after its producers.  xyz and normals
+        are record_stream'ed to s_nbr, so the caching allocator does not hand
+        their blocks out while s_nbr still reads them.
+
+        prefetch=False (the default): batch(s+1) is called after consume(s),
+        as the reference's train loop fetches (train.py:138-153): a producer
+        may refill the same staging tensors in place and may read weights
+        that consume(s) updated.  prefetch=True calls batch(s+1) right after
+        step s's neighbours are enqueued, before step s's voxel side and
+        consume(s), so batch s+1's neighbours are not ordered after them
+        (more overlap; the c3 bench uses it).  It requires batch(s+1) to
+        return NEW storage (never a tensor step s still reads) and not to
+        depend on consume(s).
         select_events: optional list of (ev0, ev1) per step, recorded on s_nbr
         around that step's selection launch (its in-step duration)."""
         cur = torch.cuda.current_stream(self.device)
@@ -394,15 +409,18 @@ class SphExtractor:
             e_nbr = self.enqueue_neighbors(
                 xyz, normals, q, after=done[q],
                 events=select_events[s] if select_events is not None else None)
-            # the next batch is produced ahead of this step's voxel side and
-            # consume (its neighbours wait for its producers only)
-            nxt = fetch(s + 1) if s + 1 < steps else None
+            if prefetch:
+                # the next batch is produced ahead of this step's voxel side
+                # and consume (its neighbours wait for its producers only)
+                nxt = fetch(s + 1) if s + 1 < steps else None
             self.enqueue_voxels(xyz, features, cur.cuda_stream, q)
             cur.wait_event(e_nbr)
             consume(s, self.outputs(slot=q, idx_slot=q))
             ev = torch.cuda.Event()
             ev.record(cur)
             done[q] = ev
+            if not prefetch:
+                nxt = fetch(s + 1) if s + 1 < steps else None
         cur.wait_stream(self.s_nbr)
 
     def outputs(self, slot=0, idx_slot=0):

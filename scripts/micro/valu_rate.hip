@@ -109,6 +109,62 @@ __global__ __launch_bounds__(256) void k_cmp_cnd(float* out, Stamp* st, float s)
   out[blockIdx.x * 256 + threadIdx.x] = t;
 }
 
+// one 32-bit-register instruction "OP %0, %0, %1" in 16 independent chains
+#define K32(NAME, ASM)                                                              \
+  __global__ __launch_bounds__(256) void NAME(float* out, Stamp* st, float s) {    \
+    float a[NCH];                                                                   \
+    for (int i = 0; i < NCH; i++) a[i] = s + i;                                     \
+    STAMP_BEGIN                                                                     \
+    for (int it = 0; it < ITER; it++) {                                             \
+      _Pragma("unroll") for (int r = 0; r < 64 / NCH; r++)                          \
+      _Pragma("unroll") for (int i = 0; i < NCH; i++)                               \
+        asm volatile(ASM : "+v"(a[i]) : "v"(s));                                    \
+    }                                                                               \
+    STAMP_END(st)                                                                   \
+    float t = 0;                                                                    \
+    for (int i = 0; i < NCH; i++) t += a[i];                                        \
+    out[blockIdx.x * 256 + threadIdx.x] = t;                                        \
+  }
+// the same on 64-bit register pairs
+#define K64(NAME, ASM)                                                              \
+  __global__ __launch_bounds__(256) void NAME(float* out, Stamp* st, float s) {    \
+    double a[NCH];                                                                  \
+    const double m = (double)s;                                                     \
+    for (int i = 0; i < NCH; i++) a[i] = m + i;                                     \
+    STAMP_BEGIN                                                                     \
+    for (int it = 0; it < ITER; it++) {                                             \
+      _Pragma("unroll") for (int r = 0; r < 64 / NCH; r++)                          \
+      _Pragma("unroll") for (int i = 0; i < NCH; i++)                               \
+        asm volatile(ASM : "+v"(a[i]) : "v"(m));                                    \
+    }                                                                               \
+    STAMP_END(st)                                                                   \
+    double t = 0;                                                                   \
+    for (int i = 0; i < NCH; i++) t += a[i];                                        \
+    out[blockIdx.x * 256 + threadIdx.x] = (float)t;                                 \
+  }
+K32(k_add_f32, "v_add_f32 %0, %0, %1")
+K32(k_mul_f32, "v_mul_f32 %0, %0, %1")
+K32(k_min_f32, "v_min_f32 %0, %0, %1")
+K32(k_lshr, "v_lshrrev_b32 %0, 3, %0")
+K32(k_med3, "v_med3_i32 %0, %0, %1, 7")
+K32(k_mbcnt, "v_mbcnt_lo_u32_b32 %0, -1, %0")
+K32(k_dpp, "v_mov_b32_dpp %0, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf")
+K32(k_dpp_add, "v_add_u32_dpp %0, %1, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf")
+K32(k_cmpu, "v_cmp_lt_u32 vcc, %0, %1")
+K32(k_min_u32, "v_min_u32 %0, %0, %1")
+K32(k_max_u32, "v_max_u32 %0, %0, %1")
+K32(k_min_dpp, "v_min_u32_dpp %0, %1, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf")
+K32(k_lshl_add, "v_lshl_add_u32 %0, %0, 2, %1")
+K32(k_and, "v_and_b32 %0, %0, %1")
+K32(k_bfe, "v_bfe_u32 %0, %0, 3, 5")
+K32(k_sub_f32, "v_sub_f32 %0, %1, %0")
+K32(k_cnd_s, "v_cndmask_b32_e64 %0, %0, %1, s[4:5]")
+K32(k_cmp_s, "v_cmp_le_u32_e64 s[4:5], %0, %1")
+K64(k_pk_add, "v_pk_add_f32 %0, %0, %1")
+K64(k_pk_mul, "v_pk_mul_f32 %0, %0, %1")
+K64(k_min_f64, "v_min_f64 %0, %0, %1")
+K64(k_cmp_u64, "v_cmp_lt_u64 vcc, %0, %1")
+
 template <typename K>
 void run(const char* name, K kern, float* d, Stamp* st, int W) {
   const int wgs = 256 * W;
@@ -152,11 +208,34 @@ int main() {
   const int maxw = 8;
   (void)hipMalloc(&d, (size_t)256 * maxw * 256 * 4);
   (void)hipMalloc(&st, (size_t)256 * maxw * 4 * sizeof(Stamp));
-  for (int W : {1, 2, 4, 8}) {
+  for (int W : {4}) {
     run("fma", k_fma, d, st, W);
     run("pk_fma", k_pk_fma, d, st, W);
     run("add_u32", k_add_u32, d, st, W);
     run("cmp+cnd", k_cmp_cnd, d, st, W);
+    if (W < 2) continue;
+    run("add_f32", k_add_f32, d, st, W);
+    run("mul_f32", k_mul_f32, d, st, W);
+    run("min_f32", k_min_f32, d, st, W);
+    run("lshr", k_lshr, d, st, W);
+    run("med3_i32", k_med3, d, st, W);
+    run("mbcnt_lo", k_mbcnt, d, st, W);
+    run("mov_dpp", k_dpp, d, st, W);
+    run("add_dpp", k_dpp_add, d, st, W);
+    run("cmp_u32", k_cmpu, d, st, W);
+    run("min_u32", k_min_u32, d, st, W);
+    run("max_u32", k_max_u32, d, st, W);
+    run("min_dpp", k_min_dpp, d, st, W);
+    run("lshl_add", k_lshl_add, d, st, W);
+    run("and_b32", k_and, d, st, W);
+    run("bfe_u32", k_bfe, d, st, W);
+    run("sub_f32", k_sub_f32, d, st, W);
+    run("cnd_sgpr", k_cnd_s, d, st, W);
+    run("cmp_sgpr", k_cmp_s, d, st, W);
+    run("pk_add", k_pk_add, d, st, W);
+    run("pk_mul", k_pk_mul, d, st, W);
+    run("min_f64", k_min_f64, d, st, W);
+    run("cmp_u64", k_cmp_u64, d, st, W);
   }
   (void)hipFree(d);
   (void)hipFree(st);

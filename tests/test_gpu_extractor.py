@@ -294,9 +294,10 @@ def test_extractor_ind_vs_reference_fp32_normalisation(dev, seed):
     assert total <= b * n // 1000
 
 
+@pytest.mark.parametrize("prefetch", [False, True])
 @pytest.mark.parametrize("b,n,c,k,r", [(4, 1024, 16, 32, 16), (2, 2048, 32, 32, 32),
                                        (3, 1500, 7, 16, 16)])
-def test_extractor_pipelined_steps(dev, b, n, c, k, r):
+def test_extractor_pipelined_steps(dev, b, n, c, k, r, prefetch):
     """SphExtractor.pipelined_steps (bench.py c3: each batch's KNN + local
     PPF on s_nbr one batch ahead of the caller's voxel side and backwards):
     every step sees exactly its own batch's outputs, equal to the oracle,
@@ -314,7 +315,7 @@ def test_extractor_pipelined_steps(dev, b, n, c, k, r):
         gg = ops.spherical_trilinear_devoxelize_backward(gy, out["dinds"], out["dwgts"], r)
         got.append(({kk: v.clone() for kk, v in out.items()}, gg))
 
-    ex.pipelined_steps(4, lambda s: tb[s], consume)
+    ex.pipelined_steps(4, lambda s: tb[s], consume, prefetch=prefetch)
     torch.cuda.synchronize()
     assert len(got) == 4
     for s, (out, gg) in enumerate(got):
@@ -359,6 +360,32 @@ def test_extractor_pipelined_batches_made_in_loop(dev):
             t.div_(2.0)
             out.append(t)
         return tuple(out)
+
+    ex.pipelined_steps(steps, batch, lambda s, out: got.append(
+        {kk: v.clone() for kk, v in out.items()}))
+    torch.cuda.synchronize()
+    _check_steps(got, batches, k, r)
+
+
+def test_extractor_pipelined_in_place_producer(dev):
+    """The default pipelined_steps (prefetch=False) with a producer that
+    refills ONE staging buffer in place each step (xyz.copy_(host), as a
+    loader with a pinned staging tensor does), after a GPU-side delay: step
+    s+1's copy must not overwrite step s's inputs while its voxel side or
+    KNN still read them.  Every step against the oracle."""
+    from pcr_amd.extractor import SphExtractor
+    b, n, c, k, r, steps = 4, 1024, 16, 32, 32, 5
+    batches = [gaussian_clouds(b, n, seed=80 + s, c=c) for s in range(steps)]
+    src = [[T(a, dev) for a in bt] for bt in batches]
+    stage = [torch.empty_like(t) for t in src[0]]
+    ex = SphExtractor(b, n, c, k, r, device=dev)
+    got = []
+
+    def batch(s):
+        torch.cuda._sleep(2_000_000)  # the producer lags behind the host
+        for dst, t in zip(stage, src[s]):
+            dst.copy_(t)
+        return tuple(stage)
 
     ex.pipelined_steps(steps, batch, lambda s, out: got.append(
         {kk: v.clone() for kk, v in out.items()}))

@@ -20,6 +20,29 @@ def N(t):
     return t.detach().cpu().numpy()
 
 
+def check_sorted(dev, xyz, nrm, k, exp_idx):
+    """The extractor's selection (pcr_knn_prepare + pcr_knn_select_ppf: ids
+    in sorted query order, clouds of <= 1024 points through the transposed
+    knn_wsel_kernel) on the same cloud, every output poisoned first."""
+    import torch
+    from pcr_amd import _lib
+    from pcr_amd.ops import _ptr, _stream
+    b, _, n = xyz.shape
+    tx, tn = T(xyz, dev), T(nrm, dev)
+    lib = _lib.load()
+    ws = torch.full((lib.pcr_knn_workspace_size(b, n, n),), 0xA5, dtype=torch.uint8, device=dev)
+    idx = torch.full((b, k, n), -7, dtype=torch.int32, device=dev)
+    ppf = torch.full((b, 4, k, n), float("nan"), device=dev)
+    _lib.check(lib.pcr_knn_prepare(_ptr(tx), b, n, _ptr(ws), ws.numel(), _stream()), "prepare")
+    _lib.check(lib.pcr_knn_select_ppf(_ptr(tx), _ptr(tn), b, n, k, 1, _ptr(idx), _ptr(ppf),
+                                      _ptr(ws), ws.numel(), _stream()), "select_ppf")
+    torch.cuda.synchronize()
+    got = N(idx)
+    bad = np.argwhere(got != exp_idx)
+    assert bad.size == 0, "sorted-path idx differs at %d places, first %s: got %s exp %s" % (
+        len(bad), bad[:3].tolist(), got[tuple(bad[0])], exp_idx[tuple(bad[0])])
+
+
 def check_self(dev, xyz, k):
     """knn_forward_cuda(xyz, xyz, k) and the fused knn_local_ppf vs the oracle."""
     from pcr_amd import ops
@@ -34,6 +57,8 @@ def check_self(dev, xyz, k):
     assert np.array_equal(N(dist), e[0])
     ep = oracle.local_ppf(xyz, nrm, xyz, nrm, e[2], kmajor=True, relative=True)
     assert np.array_equal(N(ppf), ep, equal_nan=True)
+    if k <= 32 and xyz.shape[2] <= 2048:
+        check_sorted(dev, xyz, nrm, k, e[2])
 
 
 @pytest.mark.parametrize("k", [1, 7, 16, 31, 32])
