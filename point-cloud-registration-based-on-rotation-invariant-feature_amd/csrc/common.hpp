@@ -95,11 +95,7 @@ static __device__ unsigned long long pcr_diag_stamps[1024][16];  // one copy per
 // Issue priority of the latency-bound per-cloud kernels (prep, Morton sort):
 // they share CUs with the other stream's throughput kernels, whose waves
 // would otherwise take most issue slots and stretch them several-fold.
-__device__ inline void latency_kernel_priority() {
-#if !(defined(KNN_EXP) && KNN_EXP == 12)
-  __builtin_amdgcn_s_setprio(3);
-#endif
-}
+__device__ inline void latency_kernel_priority() { __builtin_amdgcn_s_setprio(3); }
 
 // Diagnostic builds: per-kernel issue priorities from the environment
 // (PCR_PRIO_<slot>=0..3, slot 0 sort, 1 select, 2 PPF, 3 prep, 4 means,
@@ -282,6 +278,90 @@ __device__ inline void block_bitonic(unsigned long long (&v)[kMaxE], int E,
       }
     }
   }
+}
+
+// Stable LSD radix sort of m ints inside ONE workgroup of NT threads, 8-bit
+// digits of key(v) (bits [0, kbits)), ping-pong between `a` and `b` (global
+// memory; a holds the input).  Each pass: a digit histogram (LDS atomics:
+// order-free), its exclusive scan, then the elements in tiles of NT, in
+// order: a wave ranks its 64 elements among the same digit with 8 ballots
+// (the lanes that agree on every bit; rank = those below the lane), the
+// per-wave digit counts are scanned over the waves in wave order, and each
+// element goes to base[digit] + earlier waves + its rank -- equal keys keep
+// their input order.  O(m) per pass.  Returns the array holding the result.
+// lds: (2 + NT / 64) * 256 ints.
+template <int NT, typename KeyF>
+__device__ int* wg_radix_sort(int* a, int* b, int m, int kbits, KeyF key, int* lds) {
+  constexpr int NW = NT / kWave;
+  static_assert(NT >= 256 && NT % kWave == 0, "one thread per digit");
+  int* base = lds;             // [256] running bucket offsets
+  int* tot = lds + 256;        // [256] this tile's digit totals
+  int* wtab = lds + 512;       // [NW][256] per-wave digit counts, then their prefixes
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  for (int sh = 0; sh < kbits; sh += 8) {
+    for (int i = tid; i < 256 + NW * 256; i += NT) (i < 256 ? base[i] : wtab[i - 256]) = 0;
+    __syncthreads();
+    for (int e = tid; e < m; e += NT) atomicAdd(&base[(key(a[e]) >> sh) & 255], 1);
+    __syncthreads();
+    {
+      // exclusive scan of the 256 counts: wave scans, then the wave sums
+      int c = tid < 256 ? base[tid] : 0;
+      const int own = c;
+#pragma unroll
+      for (int off = 1; off < kWave; off <<= 1) {
+        const int t = __shfl_up(c, off, kWave);
+        if (lane >= off) c += t;
+      }
+      if (tid < 256 && lane == 63) tot[wv] = c;
+      __syncthreads();
+      int add = 0;
+      if (tid < 256)
+        for (int w = 0; w < wv; w++) add += tot[w];
+      __syncthreads();
+      if (tid < 256) base[tid] = add + c - own;
+      __syncthreads();
+    }
+    for (int t0 = 0; t0 < m; t0 += NT) {
+      const int e = t0 + tid;
+      const bool ok = e < m;
+      const int v = ok ? a[e] : 0;
+      const int dg = ok ? (key(v) >> sh) & 255 : 0;
+      unsigned long long peers = __ballot(ok);
+#pragma unroll
+      for (int bit = 0; bit < 8; bit++) {
+        const bool one = (dg >> bit) & 1;
+        const unsigned long long bb = __ballot(ok && one);
+        peers &= one ? bb : ~bb;
+      }
+      const int rank = __popcll(peers & lt);
+      if (ok && rank == 0) wtab[wv * 256 + dg] = __popcll(peers);
+      __syncthreads();
+      if (tid < 256) {
+        int run = 0;
+        for (int w = 0; w < NW; w++) {
+          const int c = wtab[w * 256 + tid];
+          wtab[w * 256 + tid] = run;
+          run += c;
+        }
+        tot[tid] = run;
+      }
+      __syncthreads();
+      if (ok) b[base[dg] + wtab[wv * 256 + dg] + rank] = v;
+      __syncthreads();
+      if (tid < 256) {
+        base[tid] += tot[tid];
+        for (int w = 0; w < NW; w++) wtab[w * 256 + tid] = 0;
+      }
+      __syncthreads();
+    }
+    __threadfence_block();  // b's global writes are read by other threads next pass
+    __syncthreads();
+    int* t = a;
+    a = b;
+    b = t;
+  }
+  return a;
 }
 
 }  // namespace pcr

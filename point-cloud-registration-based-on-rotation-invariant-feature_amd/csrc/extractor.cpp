@@ -161,23 +161,13 @@ extern "C" pcr_status pcr_runner_create(int timed_steps, pcr_runner** out) {
   // measured no better than the default.  The caller's stream is joined
   // after the run with these events, and the host synchronises through its
   // own (system-scope) events.
-#if defined(KNN_EXP) && KNN_EXP == 26
-  const unsigned scope = hipEventReleaseToDevice;
-#elif defined(KNN_EXP) && KNN_EXP == 27
-  const unsigned scope = 0;
-#else
   const unsigned scope = hipEventDisableSystemFence;
-#endif
   for (int i = 0; i < kSyncEvents; i++)
     ok = ok && hipEventCreateWithFlags(&rn->sync[i], hipEventDisableTiming | scope) == hipSuccess;
   // timing events: device-scope release (hipEventReleaseToDevice: more
   // precise timings, no system-scope write-back inside the timed kernel's
-  // bracket); the experiment build 28 keeps the default
-#if defined(KNN_EXP) && KNN_EXP == 28
-  const unsigned tscope = 0;
-#else
+  // bracket)
   const unsigned tscope = hipEventReleaseToDevice;
-#endif
   if (ok && timed_steps > 0) {
     rn->t0 = new hipEvent_t[timed_steps]();
     rn->t1 = new hipEvent_t[timed_steps]();

@@ -1906,11 +1906,12 @@ __device__ inline void wsel_append(unsigned long long m, unsigned addr, unsigned
 
 template <int R>
 __global__ __launch_bounds__(kWselWaves * 64) void knn_wsel_kernel(KnnSet s, int k) {
-  // [0][wave][slot] collected d bits, [1][wave][slot] their original indices
+  // [0][wave][slot] collected d bits, [1][wave][slot] their sorted positions
   // (2048 bytes apart: wsel_append's ds_write offset)
   __shared__ unsigned kbuf_s[2][kWselWaves][kWselCap];
   __shared__ int tile_s[kBlk][kSortedK + 1];  // output ids [query][slot] (padded: no bank conflicts)
   __shared__ int qnext_s;                     // the next chunk of the block's queries
+  __shared__ int cj_s[R * kBlk];              // original index of each sorted position
   static_assert(sizeof(kbuf_s[0]) == 2048, "wsel_append's offset");
   const int b = blockIdx.y, qblk = blockIdx.x;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1924,9 +1925,12 @@ __global__ __launch_bounds__(kWselWaves * 64) void knn_wsel_kernel(KnnSet s, int
   }
 #endif
   typedef float pf2v __attribute__((ext_vector_type(2)));
-  // the whole cloud, one candidate per lane and register (NaN / -1 padding)
+  // the whole cloud, one candidate per lane and register (NaN padding); the
+  // candidates' original indices in LDS (cj_s[p], p = 64 r + lane: the
+  // compaction stores positions, the output looks the index up)
   pf2v cx[R / 2], cy[R / 2], cz[R / 2];
-  int cj[R];
+  for (int i = threadIdx.x; i < R * kBlk; i += kWselWaves * kBlk)
+    cj_s[i] = i < s.npad ? s.j[cb + i] : -1;
 #pragma unroll
   for (int h = 0; h < R / 2; h++) {
     float v[2][3];
@@ -1938,11 +1942,9 @@ __global__ __launch_bounds__(kWselWaves * 64) void knn_wsel_kernel(KnnSet s, int
       const bool ok = r < nr;
       const size_t p = cb + (size_t)(ok ? r : nr - 1) * kBlk + lane;
       const float x = s.x[p], y = s.y[p], z = s.z[p];
-      const int j = s.j[p];
       v[e][0] = ok ? x : __builtin_nanf("");
       v[e][1] = ok ? y : __builtin_nanf("");
       v[e][2] = ok ? z : __builtin_nanf("");
-      cj[r] = ok ? j : -1;
     }
     cx[h] = pf2v{v[0][0], v[1][0]};
     cy[h] = pf2v{v[0][1], v[1][1]};
@@ -2024,15 +2026,20 @@ __global__ __launch_bounds__(kWselWaves * 64) void knn_wsel_kernel(KnnSet s, int
     }
     WSEL_PHASE(1);
     // 2. threshold: count(d <= t) by ballots (NaN bits compare above every t)
-    unsigned long long msk[R];
+    // the last pass's ballots are kept for the compaction when they fit in
+    // SGPRs (R = 16: 32 of them); R = 32 ballots again there
+    constexpr bool kKeep = R <= 16;
+    unsigned long long msk[kKeep ? R : 1];
     auto count_le = [&](int bits) {
-      int c = 0;
+      // four running popcount sums: a dependency chain a quarter as long
+      int pc[4] = {0, 0, 0, 0};
 #pragma unroll
       for (int r = 0; r < R; r++) {
-        msk[r] = __ballot(db[r] <= (unsigned)bits);
-        c += __popcll(msk[r]);
+        const unsigned long long m = __ballot(db[r] <= (unsigned)bits);
+        if (kKeep) msk[kKeep ? r : 0] = m;
+        pc[r & 3] += __popcll(m);
       }
-      return c;
+      return (pc[0] + pc[1]) + (pc[2] + pc[3]);
     };
     int lo = -1, hi = 0x7F800000, cnt_lo = 0, cnt = 0;
     bool exact = false;
@@ -2076,9 +2083,10 @@ __global__ __launch_bounds__(kWselWaves * 64) void knn_wsel_kernel(KnnSet s, int
       unsigned addr = kd_addr;
 #pragma unroll
       for (int r = 0; r < R; r++) {
-        if (msk[r] != 0ull) {
-          wsel_append(msk[r], addr, db[r], cj[r]);
-          addr += 4u * (unsigned)__popcll(msk[r]);
+        const unsigned long long m = kKeep ? msk[kKeep ? r : 0] : __ballot(db[r] <= (unsigned)tb);
+        if (m != 0ull) {
+          wsel_append(m, addr, db[r], 64 * r + lane);
+          addr += 4u * (unsigned)__popcll(m);
         }
       }
       ntake = cnt;
@@ -2086,13 +2094,15 @@ __global__ __launch_bounds__(kWselWaves * 64) void knn_wsel_kernel(KnnSet s, int
       // 5. ties: every key below distance bits hi (cnt_lo < k of them), then
       // the need = k - cnt_lo smallest indices among those at exactly hi
       const int need = k - cnt_lo;
+      // (rare: the indices are read from LDS where used, no registers held)
+      auto cj = [&](int r) { return cj_s[64 * r + lane]; };
       int jl = -1, jh = s.n - 1;
 #pragma unroll 1
       while (jh - jl > 1) {
         const int jm = jl + ((jh - jl) >> 1);
         int c = 0;
 #pragma unroll
-        for (int r = 0; r < R; r++) c += __popcll(__ballot(db[r] == (unsigned)hi && cj[r] <= jm));
+        for (int r = 0; r < R; r++) c += __popcll(__ballot(db[r] == (unsigned)hi && cj(r) <= jm));
         if (c >= need) jh = jm;
         else jl = jm;
       }
@@ -2100,9 +2110,9 @@ __global__ __launch_bounds__(kWselWaves * 64) void knn_wsel_kernel(KnnSet s, int
 #pragma unroll
       for (int r = 0; r < R; r++) {
         const unsigned long long m =
-            __ballot(db[r] < (unsigned)hi || (db[r] == (unsigned)hi && cj[r] <= jh));
+            __ballot(db[r] < (unsigned)hi || (db[r] == (unsigned)hi && cj(r) <= jh));
         if (m != 0ull) {
-          wsel_append(m, addr, db[r], cj[r]);
+          wsel_append(m, addr, db[r], 64 * r + lane);
           addr += 4u * (unsigned)__popcll(m);
         }
       }
@@ -2125,11 +2135,11 @@ __global__ __launch_bounds__(kWselWaves * 64) void knn_wsel_kernel(KnnSet s, int
     dg_keys += ntake;
 #endif
     if (!slow) {
-      const int jo = lane < ntake ? kj[key & 63u] : 0;
+      const int jo = lane < ntake ? cj_s[kj[key & 63u]] : 0;
       if (lane < k) tile_s[qi][lane] = jo;
     } else {
       unsigned long long skey = ~0ull;
-      if (lane < ntake) skey = ((unsigned long long)kd[lane] << 32) | (unsigned)kj[lane];
+      if (lane < ntake) skey = ((unsigned long long)kd[lane] << 32) | (unsigned)cj_s[kj[lane]];
       skey = wsel_sort64_exact(skey, lane);
       if (lane < k) tile_s[qi][lane] = lane < ntake ? (int)(unsigned)(skey & 0xFFFFFFFFull) : 0;
     }
@@ -2425,9 +2435,13 @@ pcr_status knn_spatial(const float* xyz1, const float* xyz2, int b, int n, int m
     if (!self || ppf1 || dist1 || idx2 || k > kSortedK || k > kSelMaxK || s1.sidx == nullptr ||
         s1.npad > 2 * kSelCache)
       return PCR_ERR_UNSUPPORTED;
+    // clouds of <= 1024 points: the transposed selection (c2: 31.0 us alone
+    // against 32.8 for knn_select_kernel).  At 2048 points its R = 32
+    // registers per coordinate leave 2 waves per SIMD and it lost (928 us
+    // against 600 at c3), so those keep the per-lane kernel.
     if (s1.npad <= 16 * kBlk && PCR_KNOB("PCR_KNN_WSEL", PCR_WSEL_DEFAULT)) {
-      hipLaunchKernelGGL((knn_wsel_kernel<16>), dim3(s1.nblk, b), dim3(kWselWaves * 64), 0, st, s1,
-                         k);
+      hipLaunchKernelGGL((knn_wsel_kernel<16>), dim3(s1.nblk, b), dim3(kWselWaves * 64), 0, st,
+                         s1, k);
       return PCR_OK;
     }
     return launch_block<false>(s1, c1, b, k, nullptr, idx1, nullptr, nullptr, nullptr, nullptr,

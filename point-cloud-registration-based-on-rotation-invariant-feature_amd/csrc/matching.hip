@@ -50,21 +50,29 @@ __global__ __launch_bounds__(256) void match_sqnorm_cm_kernel(const float* __res
 }
 
 constexpr int kMT = 128;  // tile rows (f1) and columns (f2)
-constexpr int kKC = 32;   // channels per LDS stage
+// channels per LDS stage: 16 (two double-buffered stages of A and B take
+// 34 KB, four workgroups per CU) measured 0.417 -> 0.350 ms at c4 (128 pairs
+// x 1024 points, C = 64) and 1.59 -> 1.47 ms at C = 512 against 32 (68 KB,
+// two per CU: the epilogue of one workgroup had too few MFMAs beside it)
+#ifndef PCR_MATCH_KC
+#define PCR_MATCH_KC 16
+#endif
+constexpr int kKC = PCR_MATCH_KC;
 constexpr int kMPad = kMT + 4;
+constexpr int kE = kKC * kMT / 256;  // channels of one row each thread stages per stage
 
-// One stage of the operands: thread t holds 16 consecutive channels of row
+// One stage of the operands: thread t holds kE consecutive channels of row
 // t / 2 of A and of B (float4 loads when the stage is full and c % 4 == 0).
 __device__ inline void match_load_stage(const float* __restrict__ A, const float* __restrict__ B,
                                         int i0, int j0, int n1, int n2, int c, int k0, int lr,
-                                        int lk, float (&va)[16], float (&vb)[16]) {
+                                        int lk, float (&va)[kE], float (&vb)[kE]) {
   const int ka = k0 + lk;
   const bool ra = i0 + lr < n1, rb = j0 + lr < n2;
-  if (ka + 16 <= c && (c & 3) == 0) {
+  if (ka + kE <= c && (c & 3) == 0) {
     const float4* pa = reinterpret_cast<const float4*>(A + (size_t)(i0 + lr) * c + ka);
     const float4* pb = reinterpret_cast<const float4*>(B + (size_t)(j0 + lr) * c + ka);
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
+    for (int q = 0; q < kE / 4; q++) {
       const float4 x = ra ? pa[q] : make_float4(0.f, 0.f, 0.f, 0.f);
       const float4 y = rb ? pb[q] : make_float4(0.f, 0.f, 0.f, 0.f);
       va[4 * q] = x.x;
@@ -78,7 +86,7 @@ __device__ inline void match_load_stage(const float* __restrict__ A, const float
     }
   } else {
 #pragma unroll
-    for (int e = 0; e < 16; e++) {
+    for (int e = 0; e < kE; e++) {
       const int k = ka + e;
       va[e] = (ra && k < c) ? A[(size_t)(i0 + lr) * c + k] : 0.0f;
       vb[e] = (rb && k < c) ? B[(size_t)(j0 + lr) * c + k] : 0.0f;
@@ -87,16 +95,16 @@ __device__ inline void match_load_stage(const float* __restrict__ A, const float
 }
 
 // Channel-major operands ([c][rows] per pair): thread t holds row t % 128
-// of A and of B, channels 16 (t / 128) .. +15 of the stage, so each channel
-// row is read as 128 consecutive floats.
+// of A and of B, channels kE (t / 128) .. + kE - 1 of the stage, so each
+// channel row is read as 128 consecutive floats.
 __device__ inline void match_load_stage_cm(const float* __restrict__ A,
                                            const float* __restrict__ B, int i0, int j0, int n1,
-                                           int n2, int c, int k0, int lr, int lk, float (&va)[16],
-                                           float (&vb)[16]) {
+                                           int n2, int c, int k0, int lr, int lk, float (&va)[kE],
+                                           float (&vb)[kE]) {
   const int ka = k0 + lk;
   const bool ra = i0 + lr < n1, rb = j0 + lr < n2;
 #pragma unroll
-  for (int e = 0; e < 16; e++) {
+  for (int e = 0; e < kE; e++) {
     const int k = ka + e;
     va[e] = (ra && k < c) ? A[(size_t)k * n1 + i0 + lr] : 0.0f;
     vb[e] = (rb && k < c) ? B[(size_t)k * n2 + j0 + lr] : 0.0f;
@@ -128,8 +136,8 @@ __global__ __launch_bounds__(256) void match_tile_kernel(
 #pragma unroll
       for (int v = 0; v < 16; v++) acc[ti][tj][v] = 0.0f;
   const int lr = CM ? (tid & (kMT - 1)) : (tid >> 1);
-  const int lk = CM ? (tid / kMT) * 16 : (tid & 1) * 16;
-  float va[16], vb[16];
+  const int lk = CM ? (tid / kMT) * kE : (tid & 1) * kE;
+  float va[kE], vb[kE];
   auto load = [&](int k0) {
     if (CM)
       match_load_stage_cm(A, B, i0, j0, n1, n2, c, k0, lr, lk, va, vb);
@@ -140,7 +148,7 @@ __global__ __launch_bounds__(256) void match_tile_kernel(
   int buf = 0;
   for (int k0 = 0; k0 < c; k0 += kKC, buf ^= 1) {
 #pragma unroll
-    for (int e = 0; e < 16; e++) {
+    for (int e = 0; e < kE; e++) {
       a_s[buf][lk + e][lr] = va[e];
       b_s[buf][lk + e][lr] = vb[e];
     }

@@ -216,17 +216,18 @@ __global__ __launch_bounds__(256) void knn_grad_kernel(const float* __restrict__
 //         of g(q,i') (xB[i'] - xA[i])                         as a neighbour
 // with g = 2 graddist skipped at >= 20000, every term the reference's own
 // product.  The second sum needs, per target point, the list of pairs that
-// name it: knn_bwd_sort_kernel counting-sorts each direction's pairs by
-// target (one workgroup per (cloud, direction), LDS counters), then orders
-// each target's segment by pair id (the arrival order of the placement is
-// not deterministic), and knn_bwd_gather_kernel sums, one thread per point.
+// name it: knn_bwd_sort_kernel counts each direction's pairs per target (one
+// workgroup per (cloud, direction), LDS counters: the segment starts) and
+// orders them by target, ascending pair id within a target, with a stable
+// workgroup radix sort (O(P) per pass), and knn_bwd_gather_kernel sums, one
+// thread per point.
 constexpr int kKnnBwdThreads = 1024;
 constexpr int kKnnBwdMaxT = 16384;  // targets per cloud the LDS counters hold
 
 struct KnnBwdWs {
   int* start[2];  // [b][T_d + 1] segment starts of direction d (by target)
   int* list[2];   // [b][k N_d] pair ids (q N_d + i) by target, ascending within a target
-  int* tmp[2];    // [b][k N_d] the same in arrival order
+  int* tmp[2];    // [b][k N_d] the radix sort's second buffer
 };
 
 static size_t knn_bwd_ws_layout(int b, int n, int m, int k, KnnBwdWs* w, char* base) {
@@ -255,6 +256,7 @@ __global__ __launch_bounds__(kKnnBwdThreads) void knn_bwd_sort_kernel(
     const int* __restrict__ idx1, int n, int m, int k, KnnBwdWs ws) {
   extern __shared__ int cnt_s[];  // [T]
   __shared__ int scan_s[kKnnBwdThreads / kWave + 1];
+  __shared__ int rs_lds[(2 + kKnnBwdThreads / kWave) * 256];  // wg_radix_sort
   const int b = blockIdx.x, d = blockIdx.y, tid = threadIdx.x;
   const int N = d ? m : n, T = d ? n : m;
   const size_t P = (size_t)k * N;
@@ -285,27 +287,29 @@ __global__ __launch_bounds__(kKnnBwdThreads) void knn_bwd_sort_kernel(
     for (int t = t0; t < t1; t++) {
       const int c = cnt_s[t];
       start[t] = run;
-      cnt_s[t] = run;  // placement cursor
       run += c;
     }
     if (tid == kKnnBwdThreads - 1) start[T] = incl;
   }
   __syncthreads();
-  for (size_t p = tid; p < P; p += kKnnBwdThreads) {
-    const int j = target(p);
-    if (j >= 0) tmp[atomicAdd(&cnt_s[j], 1)] = (int)p;
-  }
+  // the pairs by target, ascending pair id within a target: a stable LSD
+  // radix sort of the pair ids keyed by target (invalid pairs key T: last).
+  // O(P) per pass, whatever the targets' multiplicities (a hub neighbour
+  // named by thousands of pairs costs no more than any other target)
+  for (size_t p = tid; p < P; p += kKnnBwdThreads) list[p] = (int)p;
   __threadfence_block();
   __syncthreads();
-  // every pair's final place: its rank by pair id within its target's segment
-  const int total = start[T];
-  for (int e = tid; e < total; e += kKnnBwdThreads) {
-    const int p = tmp[e];
-    const int j = idx[p];
-    const int s0 = start[j], s1 = start[j + 1];
-    int rank = 0;
-    for (int x = s0; x < s1; x++) rank += tmp[x] < p ? 1 : 0;
-    list[s0 + rank] = p;
+  const int kbits = 32 - __clz(T);  // keys 0 .. T
+  int* res = wg_radix_sort<kKnnBwdThreads>(
+      list, tmp, (int)P, kbits,
+      [&](int p) {
+        const int j = target((size_t)p);
+        return j >= 0 ? j : T;
+      },
+      rs_lds);
+  if (res != list) {
+    const int total = start[T];
+    for (int e = tid; e < total; e += kKnnBwdThreads) list[e] = res[e];
   }
 }
 
@@ -344,7 +348,29 @@ __global__ __launch_bounds__(256) void knn_bwd_gather_kernel(
       for (int p = 0; p < CG; p++)
         if (c0 + p < c) acc[p] += g * (xi[p] - xb[(size_t)(c0 + p) * Nb + j]);
     }
-    for (int e = s0; e < s1; e++) {
+    // the pairs naming this point, ascending: four at a time with their
+    // loads issued ahead of the in-order sums (a hub point named by
+    // thousands of pairs waits a quarter of the load round trips)
+    int e = s0;
+    for (; e + 4 <= s1; e += 4) {
+      int pp[4];
+      float g[4], xv[4][CG];
+#pragma unroll
+      for (int u = 0; u < 4; u++) pp[u] = lst[e + u];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int i2 = pp[u] % Nb;
+        g[u] = gdt[pp[u]] * 2.0f;
+#pragma unroll
+        for (int p = 0; p < CG; p++) xv[u][p] = c0 + p < c ? xb[(size_t)(c0 + p) * Nb + i2] : 0.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++)
+#pragma unroll
+        for (int p = 0; p < CG; p++)
+          if (c0 + p < c) acc[p] += -(g[u] * (xv[u][p] - xi[p]));
+    }
+    for (; e < s1; e++) {
       const int pp = lst[e];
       const int i2 = pp % Nb;
       const float g = gdt[pp] * 2.0f;
@@ -495,39 +521,6 @@ __global__ __launch_bounds__(NT) void local_ppf_self_kernel(const float* __restr
   }
 }
 
-// Local PPF on the hardware's approximate reciprocal square root / square
-// root (v_rsq_f32, v_sqrt_f32, ~1 ulp) instead of IEEE divisions and
-// correctly rounded square roots: experiment build KNN_EXP == 21 only (the
-// product keeps pcr_local_ppf, bit-identical to the oracle)
-__device__ inline float acosf_hw(float x) {
-  const float pio2_hi = 1.57079637e+00f, pio2_lo = -4.37113883e-08f;
-  const float pi_hi = 3.14159274e+00f, pi_lo = -8.74227766e-08f;
-  const float ax = __builtin_fabsf(x);
-  const bool mid = ax <= 0.5f;
-  const float s = mid ? x : __builtin_amdgcn_sqrtf((1.0f - ax) * 0.5f);
-  const float p = pcr_asinf_core(s);
-  return mid ? pio2_hi - (p - pio2_lo) : (x > 0.0f ? 2.0f * p : pi_hi - (2.0f * p - pi_lo));
-}
-__device__ inline void local_ppf_hw(float cx, float cy, float cz, float cnx, float cny,
-                                    float cnz, float px, float py, float pz, float pnx,
-                                    float pny, float pnz, int relative, float out[4]) {
-  const float gx = relative ? px - cx : px;
-  const float gy = relative ? py - cy : py;
-  const float gz = relative ? pz - cz : pz;
-  const float dx = cx - gx, dy = cy - gy, dz = cz - gz;
-  const float d2 = pcr_sumsq3f(dx, dy, dz);
-  const float rn = __builtin_amdgcn_rsqf(d2);
-  const float ux = dx * rn, uy = dy * rn, uz = dz * rn;
-  out[0] = acosf_hw(pcr_clamp1f(pcr_dot3f(pnx, pny, pnz, ux, uy, uz)));
-  out[1] = acosf_hw(pcr_clamp1f(pcr_dot3f(cnx, cny, cnz, ux, uy, uz)));
-  out[2] = acosf_hw(pcr_clamp1f(pcr_dot3f(pnx, pny, pnz, cnx, cny, cnz)));
-  out[3] = __builtin_amdgcn_sqrtf(d2);
-}
-#if defined(KNN_EXP) && KNN_EXP == 21
-#define PCR_LOCAL_PPF_CLOUD local_ppf_hw
-#else
-#define PCR_LOCAL_PPF_CLOUD pcr_local_ppf
-#endif
 
 // The same local PPF from the selection's sorted-order id rows
 // (pcr_knn_select_ppf), one workgroup per (cloud, SL slots) covering every
@@ -549,7 +542,8 @@ __global__ __launch_bounds__(NT) void local_ppf_cloud_kernel(const float* __rest
                                                               float* __restrict__ out,
                                                               const int* __restrict__ sidx,
                                                               const int* __restrict__ inv,
-                                                              int npad, int* __restrict__ idx_out) {
+                                                              int npad, int* __restrict__ idx_out,
+                                                              int pr) {
   extern __shared__ __align__(16) float cl_s[];  // [6][n] x y z nx ny nz, then [SL][npad] ids
   int* id_s = (int*)(cl_s + 6 * n);
   constexpr int PT = kPpfSelfMaxN / NT;  // points per thread at most
@@ -557,16 +551,21 @@ __global__ __launch_bounds__(NT) void local_ppf_cloud_kernel(const float* __rest
   const int U = gridDim.x;
   const int id = blockIdx.x;
   const int u = (U % 8 == 0) ? (id % 8) * (U / 8) + id / 8 : id;
-  const int b = u / G;
-  const int q0 = (u - b * G) * SL;
+  // unit u = (cloud, slot group, point range): a cloud's units are
+  // consecutive, so the XCD-aware order keeps them on one XCD
+  const int b = u / (G * pr);
+  const int rem = u - b * G * pr;
+  const int q0 = (rem / pr) * SL;
+  const int span = (n + pr - 1) / pr;  // points of this workgroup's range
+  const int j0 = (rem % pr) * span, j1 = min(n, j0 + span);
   const int sl = min(SL, k - q0);
   const int tid = threadIdx.x;
   // this thread's points' rows in sorted order, loaded before the staging
   int p[PT];
 #pragma unroll
   for (int e = 0; e < PT; e++) {
-    const int j = e * NT + tid;
-    p[e] = j < n ? inv[(size_t)b * n + j] : 0;
+    const int j = j0 + e * NT + tid;
+    p[e] = j < j1 ? inv[(size_t)b * n + j] : 0;
   }
   const float* P = xyz + (size_t)b * 3 * n;
   const float* Nn = nrm + (size_t)b * 3 * n;
@@ -581,8 +580,8 @@ __global__ __launch_bounds__(NT) void local_ppf_cloud_kernel(const float* __rest
   int* I = idx_out + (size_t)b * k * n;
 #pragma unroll
   for (int e = 0; e < PT; e++) {
-    const int j = e * NT + tid;
-    if (j >= n) break;
+    const int j = j0 + e * NT + tid;
+    if (j >= j1) break;
     const float cx = cl_s[j], cy = cl_s[n + j], cz = cl_s[2 * n + j];
     const float cnx = cl_s[3 * n + j], cny = cl_s[4 * n + j], cnz = cl_s[5 * n + j];
 #pragma unroll
@@ -593,7 +592,7 @@ __global__ __launch_bounds__(NT) void local_ppf_cloud_kernel(const float* __rest
       I[(size_t)q * n + j] = jd;
       const unsigned si = (jd < 0 || jd >= n) ? 0u : (unsigned)jd;
       float o[4];
-      PCR_LOCAL_PPF_CLOUD(cx, cy, cz, cnx, cny, cnz, cl_s[si], cl_s[n + si], cl_s[2 * n + si],
+      pcr_local_ppf(cx, cy, cz, cnx, cny, cnz, cl_s[si], cl_s[n + si], cl_s[2 * n + si],
                           cl_s[3 * n + si], cl_s[4 * n + si], cl_s[5 * n + si], relative, o);
       // nontemporal: the PPF rows are streamed out
 #pragma unroll
@@ -1023,25 +1022,19 @@ extern "C" pcr_status pcr_knn_ppf_sorted(const float* xyz, const float* normals,
   PCR_REQUIRE(workspace != nullptr && workspace_bytes >= pcr_knn_workspace_size(b, n, n) &&
                   knn_sorted_views(const_cast<void*>(workspace), b, n, &sidx, &inv, &npad),
               "knn_ppf_sorted: workspace without sorted neighbour rows");
-#if defined(KNN_EXP) && KNN_EXP == 22
-  // A/B build: the per-256-point workgroups of local_ppf_self_kernel
-  hipLaunchKernelGGL((local_ppf_self_kernel<8>), dim3(ceil_div(n, 256), ceil_div(k, 8), b),
-                     dim3(256), (size_t)6 * n * 4, as_stream(stream), xyz, normals, nullptr, n, k,
-                     relative, ppf, sidx, inv, npad, idx);
-#elif defined(KNN_EXP) && KNN_EXP == 23
-  // A/B build: two slots per workgroup (LDS 64 KB at 2048 points)
-  constexpr int SL = 2;
-  const size_t lds = ((size_t)6 * n + (size_t)SL * npad) * 4;
-  allow_big_lds(local_ppf_cloud_kernel<SL>, lds);
-  hipLaunchKernelGGL((local_ppf_cloud_kernel<SL>), dim3(b * ceil_div(k, SL)), dim3(512), lds,
-                     as_stream(stream), xyz, normals, n, k, relative, ppf, sidx, inv, npad, idx);
-#else
+  // clouds of <= 1024 points: one workgroup per (cloud, 4 slots, 512
+  // points), a thread per point, so a c2 launch has 4096 waves to hide the
+  // staging and the LDS gathers behind each other's arithmetic (13.9 ->
+  // 13.0 us alone).  At 2048 points every workgroup already has 4 points per
+  // thread, and splitting it re-stages the 48 KB cloud per range (c3: 100 ->
+  // 160 us), so those keep one workgroup per (cloud, 4 slots).
   constexpr int SL = 4;
+  const int pr = PCR_KNOB("PCR_PPF_RANGES", n <= 1024 ? ceil_div(n, 512) : 1);
   const size_t lds = ((size_t)6 * n + (size_t)SL * npad) * 4;
   allow_big_lds(local_ppf_cloud_kernel<SL>, lds);
-  hipLaunchKernelGGL((local_ppf_cloud_kernel<SL>), dim3(b * ceil_div(k, SL)), dim3(512), lds,
-                     as_stream(stream), xyz, normals, n, k, relative, ppf, sidx, inv, npad, idx);
-#endif
+  hipLaunchKernelGGL((local_ppf_cloud_kernel<SL>), dim3(b * ceil_div(k, SL) * pr), dim3(512), lds,
+                     as_stream(stream), xyz, normals, n, k, relative, ppf, sidx, inv, npad, idx,
+                     pr);
   return launch_status("knn_ppf_sorted");
 }
 

@@ -1294,9 +1294,10 @@ __global__ __launch_bounds__(kPrepThreads) void sph_normalize_kernel(
 // slot in its voxel; (2) a per-cloud exclusive scan of the counts (tile sums,
 // then each tile scans itself after the sum of the tiles before it) locates
 // every voxel's segment; (3) each point lands at start + slot (arrival
-// order); (4) each point of a segment of m > 1 takes its rank by point id
-// among the segment (m reads), so every voxel's points end up in ascending
-// point order -- the order the oracle sums in; (5) one thread per voxel sums
+// order); (4) each point of a segment of 1 < m <= 64 takes its rank by point
+// id among the segment (m reads), a larger segment is sorted by a stable
+// workgroup radix sort, so every voxel's points end up in ascending point
+// order -- the order the oracle sums in; (5) one thread per voxel sums
 // its segment in that order and writes all C channels, so the dense grid is
 // written once, coalesced, zeros included.  The reference scatters C fp32
 // atomics per point (spherical_vox.cu:103-123, one cache line each).
@@ -1306,9 +1307,14 @@ struct BigVoxWs {
   int* perm;      // [b][n] points by voxel, ascending within a voxel
   int* start;     // [b][r3] segment start of each voxel (relative to its cloud)
   int* tsum;      // [b][ntile] counts per scan tile
+  int* big;       // [1 + b n / (kRankScan + 1)]: count, then voxels of > kRankScan points
   float* featT;   // [b][n][c] point-major copy of the features (nullptr: c == 0)
   int ntile;
 };
+
+// segments of up to this many points take their rank by a scan of the
+// segment (m reads per point); larger ones are sorted by vox_seg_sort_kernel
+constexpr int kRankScan = 64;
 
 constexpr int kBigScanThreads = 256;
 constexpr int kBigScanPer = 16;
@@ -1330,6 +1336,7 @@ static size_t big_ws_layout(int b, int n, int r, BigVoxWs* ws, void* base, int c
   int* perm = (int*)take(nk * 4);
   int* start = (int*)take(nr * 4);
   int* tsum = (int*)take((size_t)b * ntile * 4);
+  int* big = (int*)take((1 + nk / (kRankScan + 1)) * 4);
   float* ft = c > 0 ? (float*)take(nk * (size_t)c * 4) : nullptr;
   if (ws) {
     ws->slot = slot;
@@ -1337,6 +1344,7 @@ static size_t big_ws_layout(int b, int n, int r, BigVoxWs* ws, void* base, int c
     ws->perm = perm;
     ws->start = start;
     ws->tsum = tsum;
+    ws->big = big;
     ws->featT = ft;
     ws->ntile = ntile;
   }
@@ -1440,24 +1448,94 @@ __global__ __launch_bounds__(256) void vox_place_big_kernel(const int* __restric
 }
 
 // every point's final place: its rank by point id within its voxel's segment
-// (m reads for a voxel of m points; one-point voxels copy)
+// (m reads for a voxel of m <= kRankScan points; one-point voxels copy).  A
+// larger segment (duplicated points, a cloud padded by repeating a point) is
+// listed once, by its first arrival, for vox_seg_sort_kernel: the scan would
+// cost m^2 reads there.
 __global__ __launch_bounds__(256) void vox_rank_big_kernel(const int* __restrict__ ind,
                                                            const int* __restrict__ slot, int n,
                                                            int r3, const int* __restrict__ cnt,
                                                            const int* __restrict__ start,
                                                            const int* __restrict__ perm_u,
-                                                           int* __restrict__ perm) {
+                                                           int* __restrict__ perm,
+                                                           int* __restrict__ big) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   const int b = blockIdx.y;
   if (i >= n) return;
-  if (slot[(size_t)b * n + i] < 0) return;
+  const int sl = slot[(size_t)b * n + i];
+  if (sl < 0) return;
   const int v = ind[(size_t)b * n + i];
   const size_t vi = (size_t)b * r3 + v;
   const int m = cnt[vi];
+  if (m > kRankScan) {
+    if (sl == 0) big[1 + atomicAdd(&big[0], 1)] = (int)vi;
+    return;
+  }
   const int* seg = perm_u + (size_t)b * n + start[vi];
   int rank = 0;
   for (int x = 0; x < m; x++) rank += seg[x] < i ? 1 : 0;
   perm[(size_t)b * n + start[vi] + rank] = i;
+}
+
+// the listed large segments: one workgroup per segment (grid-stride over the
+// list), its point ids sorted ascending by a stable workgroup radix sort
+// (O(m) per 8-bit pass) from the arrival order (perm_u) into perm
+constexpr int kSegSortThreads = 1024;
+__global__ __launch_bounds__(kSegSortThreads) void vox_seg_sort_kernel(
+    const int* __restrict__ big, const int* __restrict__ cnt, const int* __restrict__ start,
+    int n, int r3, int kbits, int* __restrict__ perm_u, int* __restrict__ perm) {
+  __shared__ int rs_lds[(2 + kSegSortThreads / kWave) * 256];
+  const int nb = big[0];
+  for (int e = blockIdx.x; e < nb; e += gridDim.x) {
+    const int vi = big[1 + e];
+    const int m = cnt[vi];
+    const size_t off = (size_t)(vi / r3) * n + start[vi];
+    int* res = wg_radix_sort<kSegSortThreads>(perm_u + off, perm + off, m, kbits,
+                                              [](int v) { return v; }, rs_lds);
+    if (res != perm + off)
+      for (int t = threadIdx.x; t < m; t += kSegSortThreads) perm[off + t] = res[t];
+    __syncthreads();
+  }
+}
+
+// the listed large segments' means: one workgroup per segment (grid-stride
+// over the list), a thread per channel summing the segment's points in
+// ascending order (the order of the thread-per-voxel kernels, which skip
+// these voxels), eight point ids and their values loaded ahead of the sums.
+// FT: point-major features [b][n][c] (else channel-major [b][c][n]).
+template <bool FT>
+__global__ __launch_bounds__(256) void vox_seg_gather_kernel(
+    const int* __restrict__ big, const float* __restrict__ feat, const int* __restrict__ cnt,
+    const int* __restrict__ start, const int* __restrict__ perm, int c, int n, int r3,
+    float* __restrict__ out) {
+  constexpr int kB = 8;
+  const int nb = big[0];
+  for (int e = blockIdx.x; e < nb; e += gridDim.x) {
+    const int vi = big[1 + e];
+    const int b = vi / r3, v = vi - b * r3;
+    const int m = cnt[vi];
+    const int* P = perm + (size_t)b * n + start[vi];
+    const float inv = pcr_inv_count(m);
+    for (int ch = threadIdx.x; ch < c; ch += blockDim.x) {
+      auto val = [&](int i) {
+        return FT ? feat[((size_t)b * n + i) * c + ch] : feat[((size_t)b * c + ch) * n + i];
+      };
+      float acc = 0.0f;
+      int s = 0;
+      for (; s + kB <= m; s += kB) {
+        int pi[kB];
+        float x[kB];
+#pragma unroll
+        for (int u = 0; u < kB; u++) pi[u] = P[s + u];
+#pragma unroll
+        for (int u = 0; u < kB; u++) x[u] = val(pi[u]);
+#pragma unroll
+        for (int u = 0; u < kB; u++) acc += x[u] * inv;
+      }
+      for (; s < m; s++) acc += val(P[s]) * inv;
+      __builtin_nontemporal_store(acc, &out[((size_t)b * c + ch) * r3 + v]);
+    }
+  }
 }
 
 // one thread per voxel: its segment of the sorted points, summed per channel
@@ -1470,6 +1548,7 @@ __global__ __launch_bounds__(256) void vox_gather_big_kernel(
   if (v >= r3) return;
   const size_t vi = (size_t)b * r3 + v;
   const int m = cnt[vi];
+  if (m > kRankScan) return;  // vox_seg_gather_kernel
   const int* P = perm + (size_t)b * n + start[vi];
   const float* F = feat + (size_t)b * c * n;
   float* O = out + (size_t)b * c * r3 + v;
@@ -1579,6 +1658,7 @@ __global__ __launch_bounds__(256) void vox_gather_big_t_kernel(
   if (v >= r3) return;
   const size_t vi = (size_t)b * r3 + v;
   const int m = cnt[vi];
+  if (m > kRankScan) return;  // vox_seg_gather_kernel
   float* O = out + (size_t)b * c * r3 + v;
   const int* P = perm + (size_t)b * n + (m > 0 ? start[vi] : 0);
   const float* FT = featT + (size_t)b * n * c;
@@ -1650,7 +1730,8 @@ static pcr_status run_voxelize_big(const float* features, const float* coords_f,
   if (workspace == nullptr || ws_bytes < need) need = big_ws_layout(b, n, r, &ws, workspace, 0);
   PCR_REQUIRE(workspace != nullptr && ws_bytes >= need, "%s: workspace too small (%zu < %zu)",
               name, ws_bytes, need);
-  if (hipMemsetAsync(cnt, 0, (size_t)b * r3 * sizeof(int), stream) != hipSuccess) {
+  if (hipMemsetAsync(cnt, 0, (size_t)b * r3 * sizeof(int), stream) != hipSuccess ||
+      hipMemsetAsync(ws.big, 0, sizeof(int), stream) != hipSuccess) {
     set_error("%s: memset failed", name);
     return PCR_ERR_LAUNCH;
   }
@@ -1666,14 +1747,21 @@ static pcr_status run_voxelize_big(const float* features, const float* coords_f,
     hipLaunchKernelGGL(vox_place_big_kernel, pts, dim3(256), 0, stream, ind, ws.slot, n, r3,
                        ws.start, ws.perm_u);
     hipLaunchKernelGGL(vox_rank_big_kernel, pts, dim3(256), 0, stream, ind, ws.slot, n, r3, cnt,
-                       ws.start, ws.perm_u, ws.perm);
+                       ws.start, ws.perm_u, ws.perm, ws.big);
+    const int kbits = n > 1 ? 32 - __builtin_clz((unsigned)(n - 1)) : 1;
+    hipLaunchKernelGGL(vox_seg_sort_kernel, dim3(64), dim3(kSegSortThreads), 0, stream, ws.big,
+                       cnt, ws.start, n, r3, kbits, ws.perm_u, ws.perm);
     if (ws.featT) {
       hipLaunchKernelGGL(feat_transpose_kernel, dim3(ceil_div(n, 64), ceil_div(c, 64), b),
                          dim3(256), 0, stream, features, c, n, ws.featT);
       hipLaunchKernelGGL(vox_gather_big_t_kernel<32>, dim3(ceil_div(r3, 256), b), dim3(256), 0,
                          stream, ws.featT, cnt, ws.start, ws.perm, c, n, r3, out);
+      hipLaunchKernelGGL(vox_seg_gather_kernel<true>, dim3(64), dim3(256), 0, stream, ws.big,
+                         ws.featT, cnt, ws.start, ws.perm, c, n, r3, out);
     } else {
       hipLaunchKernelGGL(vox_gather_big_kernel, dim3(ceil_div(r3, 256), b), dim3(256), 0, stream,
+                         features, cnt, ws.start, ws.perm, c, n, r3, out);
+      hipLaunchKernelGGL(vox_seg_gather_kernel<false>, dim3(64), dim3(256), 0, stream, ws.big,
                          features, cnt, ws.start, ws.perm, c, n, r3, out);
     }
   }

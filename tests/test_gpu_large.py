@@ -3,8 +3,9 @@
 voxelisation on the global-atomic path, devoxelisation and KNN, against the
 oracle at sizes it finishes in seconds, plus size-independent properties at
 the full c5 cloud size.  The large-cloud voxelisers sort the points by voxel
-(hipCUB radix sort) and sum each voxel in ascending point order, the oracle's
-order, so their grids are bit-exact."""
+(a hand-written counting sort; voxels of more than 64 points by a stable
+workgroup radix sort) and sum each voxel in ascending point order, the
+oracle's order, so their grids are bit-exact."""
 import numpy as np
 import pytest
 
@@ -40,6 +41,39 @@ def test_sph_vox_large(dev):
     nc = oracle.normalize_sph(xyz)
     out, ind, cnt = ops.spherical_avg_voxelize_forward(T(feat, dev), T(nc, dev), 64)
     eo, ei, ec = oracle.spherical_avg_voxelize_forward(feat, nc, 64)
+    assert np.array_equal(N(ind), ei)
+    assert np.array_equal(N(cnt), ec.reshape(N(cnt).shape))
+    assert np.array_equal(N(out).reshape(eo.shape), eo)
+
+
+@pytest.mark.parametrize("kind", ["one_voxel_20pct", "many_heavy_voxels"])
+def test_sph_vox_large_heavy_voxels(dev, kind):
+    """A 65,536-point cloud (BASELINE c5 size, r = 64) whose points pile into
+    few voxels: 20% of them duplicated at one location, or 100 locations
+    with 300 copies each.  Segments past 64 points are sorted by the stable
+    workgroup radix sort (vox_seg_sort_kernel) instead of the O(m^2) rank
+    scan; ind / cnt / grid bit-exact vs the oracle, time printed."""
+    import torch
+    from pcr_amd import ops
+    b, n, c, r = 2, 65536, 8, 64
+    xyz, _, feat = gaussian_clouds(b, n, seed=44, c=c)
+    if kind == "one_voxel_20pct":
+        xyz[:, :, 1000:1000 + n // 5] = xyz[:, :, 7:8]
+    else:
+        for h in range(100):
+            xyz[:, :, 2000 + h * 300:2000 + (h + 1) * 300] = xyz[:, :, h:h + 1]
+    nc = oracle.normalize_sph(xyz)
+    tf, tn = T(feat, dev), T(nc, dev)
+    out, ind, cnt = ops.spherical_avg_voxelize_forward(tf, tn, r)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    ops.spherical_avg_voxelize_forward(tf, tn, r)
+    e1.record()
+    torch.cuda.synchronize()
+    print("%s: sph voxelize %.3f ms, largest voxel %d points" %
+          (kind, e0.elapsed_time(e1), int(N(cnt).max())))
+    eo, ei, ec = oracle.spherical_avg_voxelize_forward(feat, nc, r)
     assert np.array_equal(N(ind), ei)
     assert np.array_equal(N(cnt), ec.reshape(N(cnt).shape))
     assert np.array_equal(N(out).reshape(eo.shape), eo)

@@ -227,6 +227,39 @@ def test_knn_backward_c2_shape(dev, self_knn):
     assert_within_sum_order(N(g2), e2, b2)
 
 
+def test_knn_backward_hub_neighbour(dev):
+    """A hub neighbour: point 0 is the first neighbour of every point of
+    both clouds (8,192 points, k = 8), so its pair list holds 8,192 pairs.
+    The stable radix sort by target orders it in O(P) (the old rank scan
+    read the whole segment per pair: 6.7e7 reads).  Within the sum-order
+    bound of the oracle, bit-repeatable, time printed."""
+    from pcr_amd import ops
+    b, n, k = 2, 8192, 8
+    rng = np.random.default_rng(27)
+    x1 = rng.standard_normal((b, 3, n)).astype(np.float32)
+    x2 = rng.standard_normal((b, 3, n)).astype(np.float32)
+    i1 = rng.integers(0, n, size=(b, k, n)).astype(np.int32)
+    i2 = rng.integers(0, n, size=(b, k, n)).astype(np.int32)
+    i1[:, 0, :] = 0
+    i2[:, 0, :] = 0
+    gd1 = rng.standard_normal((b, k, n)).astype(np.float32)
+    gd2 = rng.standard_normal((b, k, n)).astype(np.float32)
+    args = [T(a, dev) for a in (x1, x2, gd1, gd2, i1, i2)]
+    g1, g2 = ops.knn_backward_cuda(*args)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    r1, r2 = ops.knn_backward_cuda(*args)
+    e1.record()
+    torch.cuda.synchronize()
+    print("hub neighbour: knn backward %.3f ms" % e0.elapsed_time(e1))
+    assert torch.equal(g1, r1) and torch.equal(g2, r2)
+    e1_, e2_ = oracle.knn_backward(x1, x2, gd1, gd2, i1, i2)
+    b1, b2 = knn_backward_bound(x1, x2, gd1, gd2, i1, i2)
+    assert_within_sum_order(N(g1), e1_, b1)
+    assert_within_sum_order(N(g2), e2_, b2)
+
+
 def test_knn_backward_gather_repeatable_and_entry_points(dev):
     """The atomics-free KNN backward (pcr_knn_backward_ws: pairs counting-
     sorted by neighbour, one gather per point) is bit-identical run to run,
