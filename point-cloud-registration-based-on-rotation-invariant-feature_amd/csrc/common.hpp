@@ -160,6 +160,45 @@ __device__ inline void lds_only_barrier() {
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
 
+typedef __attribute__((address_space(3))) void* lds_void_p;
+typedef __attribute__((address_space(1))) void* gbl_void_p;
+
+// s_waitcnt vmcnt(N) only (gfx9 encoding: expcnt / lgkmcnt at their maxima)
+template <int N>
+__device__ inline void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);  // compiler-only (the builtin is IntrNoMem)
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
+// Workgroup copy of `nbytes` (a multiple of V) from global memory straight
+// into LDS by LDS-DMA (global_load_lds_dword / _dwordx4, V = 4 / 16 bytes per
+// lane): the waves of the workgroup take pieces of 64 V bytes in turn and
+// issue them all without waiting, so the whole copy is one round trip, and no
+// staging registers are held.  Lanes of the last piece past the end re-read
+// the last V bytes (in bounds) into the destination's tail, which must be
+// padded to a whole piece (lds_dma_pad).  The caller waits with
+// wait_vmcnt<0>() before the barrier that publishes the data.
+__host__ __device__ inline int lds_dma_pad(int nbytes, int v) {
+  return (nbytes + 64 * v - 1) / (64 * v) * (64 * v);
+}
+template <int V>
+__device__ inline void lds_dma_copy(void* lds_dst, const void* gsrc, int nbytes) {
+  static_assert(V == 4 || V == 16, "LDS-DMA width");
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int np = (nbytes + 64 * V - 1) / (64 * V);
+  for (int p = wv; p < np; p += nw) {
+    const int off = min(p * 64 * V + lane * V, nbytes - V);
+    const gbl_void_p src = (gbl_void_p)((const char*)gsrc + off);
+    const lds_void_p dst = (lds_void_p)((char*)lds_dst + p * 64 * V);
+    if constexpr (V == 16)
+      __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
+    else
+      __builtin_amdgcn_global_load_lds(src, dst, 4, 0, 0);
+  }
+}
+
 // Inclusive block-wide scan of one int per thread (blockDim.x threads,
 // multiple of 64, <= 1024).  `smem` needs blockDim.x/64 + 1 ints.  Its
 // barriers order LDS only (lds_barrier).

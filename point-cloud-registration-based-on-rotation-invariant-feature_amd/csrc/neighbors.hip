@@ -535,7 +535,117 @@ __global__ __launch_bounds__(NT) void local_ppf_self_kernel(const float* __restr
 // (profiles/r03_pmc_traffic.json).  XCD-aware: the dispatcher deals
 // workgroups round-robin over the 8 XCDs, so unit (id % 8) * (U / 8) + id / 8
 // puts a cloud's slot groups on one XCD (its cloud is fetched into one L2).
-template <int SL, int NT = 512>
+// pcr_local_ppf (include/pcr_math.h) with the same bits, in fewer gfx950
+// instructions:
+//  - the three IEEE divisions by |d| share one refined reciprocal.  The
+//    compiler's f32 division is v_div_scale, v_rcp, two FMA refining the
+//    reciprocal, five FMA for the quotient, v_div_fmas and v_div_fixup; with
+//    |d| and every nonzero numerator in [2^-60, 2^60] the scales are 1, fmas
+//    is a plain FMA and fixup passes the quotient through, so the unscaled
+//    sequence below yields the same bits (a zero numerator keeps its signed
+//    zero, as fixup does).  A wave with any lane outside that range (|d| = 0
+//    for the self pair, NaN, extreme scales) takes the plain divisions.
+//  - the acos tails are selects, not branches.
+__device__ inline float ppf_acos_sel(float x) {
+  const float pio2_hi = 1.57079637e+00f, pio2_lo = -4.37113883e-08f;
+  const float pi_hi = 3.14159274e+00f, pi_lo = -8.74227766e-08f;
+  const float ax = __builtin_fabsf(x);
+  const bool mid = ax <= 0.5f;
+  const float s = mid ? x : __builtin_sqrtf((1.0f - ax) * 0.5f);
+  const float p = pcr_asinf_core(s);
+  const float t2 = 2.0f * p;
+  const float rm = pio2_hi - (p - pio2_lo);
+  const float rn = pi_hi - (t2 - pi_lo);
+  const float rt = x > 0.0f ? t2 : rn;
+  return mid ? rm : rt;
+}
+// |v| in [2^-60, 2^60] (NaN / inf excluded) by one unsigned range test on
+// the bits; `zero_ok` also accepts +-0.  Bitwise, so no short-circuit branches.
+__device__ inline bool ppf_div_safe(float v, bool zero_ok) {
+  const unsigned a = __float_as_uint(v) & 0x7FFFFFFFu;
+  constexpr unsigned lo = 0x21800000u, hi = 0x5D800000u;  // 2^-60, 2^60
+  return ((a - lo) <= (hi - lo)) | (zero_ok & (a == 0u));
+}
+__device__ inline float ppf_div_shared(float a, float b, float y) {
+  float q = a * y;
+  float r = __builtin_fmaf(-b, q, a);
+  q = __builtin_fmaf(r, y, q);
+  r = __builtin_fmaf(-b, q, a);
+  q = __builtin_fmaf(r, y, q);
+  return a == 0.0f ? a : q;
+}
+// M pairs of one centre in lockstep (every step written for all M before the
+// next), so their dependent chains interleave: the scheduler does not
+// interleave whole calls by itself.  c[m] / p[m] = {x, y, z, nx, ny, nz} of
+// pair m's centre / neighbour.
+template <int M>
+__device__ inline void ppf_local_dev(const float (&c)[M][6], const float (&p)[M][6], int relative,
+                                     float (&out)[M][4]) {
+  float dx[M], dy[M], dz[M], dn[M];
+  bool safe = true;
+#pragma unroll
+  for (int m = 0; m < M; m++) {
+    const float gx = relative ? p[m][0] - c[m][0] : p[m][0];
+    const float gy = relative ? p[m][1] - c[m][1] : p[m][1];
+    const float gz = relative ? p[m][2] - c[m][2] : p[m][2];
+    dx[m] = c[m][0] - gx;
+    dy[m] = c[m][1] - gy;
+    dz[m] = c[m][2] - gz;
+  }
+#pragma unroll
+  for (int m = 0; m < M; m++) dn[m] = __builtin_sqrtf(pcr_sumsq3f(dx[m], dy[m], dz[m]));
+#pragma unroll
+  for (int m = 0; m < M; m++)
+    safe = safe & ppf_div_safe(dn[m], false) & ppf_div_safe(dx[m], true) &
+           ppf_div_safe(dy[m], true) & ppf_div_safe(dz[m], true);
+  float ux[M], uy[M], uz[M];
+  if (__builtin_expect(__all(safe), 1)) {
+    float y[M];
+#pragma unroll
+    for (int m = 0; m < M; m++) y[m] = __builtin_amdgcn_rcpf(dn[m]);
+#pragma unroll
+    for (int m = 0; m < M; m++) y[m] = __builtin_fmaf(__builtin_fmaf(-dn[m], y[m], 1.0f), y[m], y[m]);
+#pragma unroll
+    for (int m = 0; m < M; m++) {
+      ux[m] = ppf_div_shared(dx[m], dn[m], y[m]);
+      uy[m] = ppf_div_shared(dy[m], dn[m], y[m]);
+      uz[m] = ppf_div_shared(dz[m], dn[m], y[m]);
+    }
+  } else {
+#pragma unroll
+    for (int m = 0; m < M; m++) {
+      ux[m] = dx[m] / dn[m];
+      uy[m] = dy[m] / dn[m];
+      uz[m] = dz[m] / dn[m];
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < M; m++) {
+    out[m][0] = pcr_clamp1f(pcr_dot3f(p[m][3], p[m][4], p[m][5], ux[m], uy[m], uz[m]));
+    out[m][1] = pcr_clamp1f(pcr_dot3f(c[m][3], c[m][4], c[m][5], ux[m], uy[m], uz[m]));
+    out[m][2] = pcr_clamp1f(pcr_dot3f(p[m][3], p[m][4], p[m][5], c[m][3], c[m][4], c[m][5]));
+    out[m][3] = dn[m];
+  }
+#pragma unroll
+  for (int a = 0; a < 3; a++)
+#pragma unroll
+    for (int m = 0; m < M; m++) out[m][a] = ppf_acos_sel(out[m][a]);
+}
+
+// LDS layout of local_ppf_cloud_kernel: [3][n] coordinates, [3][n] normals,
+// [SL][npad] id rows, each region padded to whole LDS-DMA pieces of width V
+struct PpfLds {
+  int nrm_off, ids_off, bytes;  // byte offsets / total
+};
+__host__ __device__ inline PpfLds ppf_lds_layout(int n, int sl, int npad, int v) {
+  PpfLds l;
+  l.nrm_off = lds_dma_pad(12 * n, v);
+  l.ids_off = 2 * l.nrm_off;
+  l.bytes = l.ids_off + lds_dma_pad(4 * sl * npad, v);
+  return l;
+}
+
+template <int SL, int V, int NT = 512>
 __global__ __launch_bounds__(NT) void local_ppf_cloud_kernel(const float* __restrict__ xyz,
                                                               const float* __restrict__ nrm, int n,
                                                               int k, int relative,
@@ -544,8 +654,7 @@ __global__ __launch_bounds__(NT) void local_ppf_cloud_kernel(const float* __rest
                                                               const int* __restrict__ inv,
                                                               int npad, int* __restrict__ idx_out,
                                                               int pr) {
-  extern __shared__ __align__(16) float cl_s[];  // [6][n] x y z nx ny nz, then [SL][npad] ids
-  int* id_s = (int*)(cl_s + 6 * n);
+  extern __shared__ __align__(16) float cl_s[];  // PpfLds: x y z | nx ny nz | id rows
   constexpr int PT = kPpfSelfMaxN / NT;  // points per thread at most
   const int G = (k + SL - 1) / SL;
   const int U = gridDim.x;
@@ -567,14 +676,16 @@ __global__ __launch_bounds__(NT) void local_ppf_cloud_kernel(const float* __rest
     const int j = j0 + e * NT + tid;
     p[e] = j < j1 ? inv[(size_t)b * n + j] : 0;
   }
-  const float* P = xyz + (size_t)b * 3 * n;
-  const float* Nn = nrm + (size_t)b * 3 * n;
-  for (int i = tid; i < 3 * n; i += NT) {
-    cl_s[i] = P[i];
-    cl_s[3 * n + i] = Nn[i];
-  }
-  const int* rows = sidx + ((size_t)b * kKnnSortedK + q0) * npad;
-  for (int i = tid; i < sl * npad; i += NT) id_s[i] = rows[i];
+  // the cloud and the id rows straight into LDS (LDS-DMA: every piece in
+  // flight at once, one round trip; a loop of loads and LDS stores waited for
+  // each of its ~14 trips in turn)
+  const PpfLds L = ppf_lds_layout(n, SL, npad, V);
+  const float* nl_s = cl_s + L.nrm_off / 4;
+  const int* id_s = (const int*)(cl_s + L.ids_off / 4);
+  lds_dma_copy<V>(cl_s, xyz + (size_t)b * 3 * n, 12 * n);
+  lds_dma_copy<V>((float*)nl_s, nrm + (size_t)b * 3 * n, 12 * n);
+  lds_dma_copy<V>((int*)id_s, sidx + ((size_t)b * kKnnSortedK + q0) * npad, 4 * sl * npad);
+  wait_vmcnt<0>();
   __syncthreads();
   float* O = out + (size_t)b * 4 * k * n;
   int* I = idx_out + (size_t)b * k * n;
@@ -583,22 +694,122 @@ __global__ __launch_bounds__(NT) void local_ppf_cloud_kernel(const float* __rest
     const int j = j0 + e * NT + tid;
     if (j >= j1) break;
     const float cx = cl_s[j], cy = cl_s[n + j], cz = cl_s[2 * n + j];
-    const float cnx = cl_s[3 * n + j], cny = cl_s[4 * n + j], cnz = cl_s[5 * n + j];
+    const float cnx = nl_s[j], cny = nl_s[n + j], cnz = nl_s[2 * n + j];
+    // the SL slots in lockstep (slots past sl compute on neighbour 0 and are
+    // not stored)
+    float nb[SL][6];
 #pragma unroll
     for (int s = 0; s < SL; s++) {
-      if (s >= sl) break;
-      const int q = q0 + s;
-      const int jd = id_s[s * npad + p[e]];
-      I[(size_t)q * n + j] = jd;
+      const int jd = s < sl ? id_s[s * npad + p[e]] : 0;
+      if (s < sl) I[(size_t)(q0 + s) * n + j] = jd;
       const unsigned si = (jd < 0 || jd >= n) ? 0u : (unsigned)jd;
-      float o[4];
-      pcr_local_ppf(cx, cy, cz, cnx, cny, cnz, cl_s[si], cl_s[n + si], cl_s[2 * n + si],
-                          cl_s[3 * n + si], cl_s[4 * n + si], cl_s[5 * n + si], relative, o);
-      // nontemporal: the PPF rows are streamed out
-#pragma unroll
-      for (int ch = 0; ch < 4; ch++)
-        __builtin_nontemporal_store(o[ch], &O[((size_t)ch * k + q) * n + j]);
+      nb[s][0] = cl_s[si];
+      nb[s][1] = cl_s[n + si];
+      nb[s][2] = cl_s[2 * n + si];
+      nb[s][3] = nl_s[si];
+      nb[s][4] = nl_s[n + si];
+      nb[s][5] = nl_s[2 * n + si];
     }
+    float ce[SL][6], o[SL][4];
+#pragma unroll
+    for (int s = 0; s < SL; s++) {
+      ce[s][0] = cx;
+      ce[s][1] = cy;
+      ce[s][2] = cz;
+      ce[s][3] = cnx;
+      ce[s][4] = cny;
+      ce[s][5] = cnz;
+    }
+    ppf_local_dev<SL>(ce, nb, relative, o);
+    // nontemporal: the PPF rows are streamed out
+#pragma unroll
+    for (int s = 0; s < SL; s++)
+      if (s < sl)
+#pragma unroll
+        for (int ch = 0; ch < 4; ch++)
+          __builtin_nontemporal_store(o[s][ch], &O[((size_t)ch * k + q0 + s) * n + j]);
+  }
+}
+
+// The same with four consecutive points per thread and one slot (needs n %
+// 4 == 0 and 16-byte aligned rows): every output store is a 16-byte vector
+// (five per thread instead of twenty 4-byte stores, the id row included), and
+// the four pairs run in lockstep.  Work item f = (slot s, quad qd) of the
+// workgroup's SL slots x span / 4 quads, taken in turn by its threads.
+typedef float ppf_f4 __attribute__((ext_vector_type(4)));
+typedef int ppf_i4 __attribute__((ext_vector_type(4)));
+template <int SL, int NT = 512>
+__global__ __launch_bounds__(NT) void local_ppf_quad_kernel(const float* __restrict__ xyz,
+                                                             const float* __restrict__ nrm, int n,
+                                                             int k, int relative,
+                                                             float* __restrict__ out,
+                                                             const int* __restrict__ sidx,
+                                                             const int* __restrict__ inv,
+                                                             int npad, int* __restrict__ idx_out,
+                                                             int pr) {
+  extern __shared__ __align__(16) float cl_s[];  // PpfLds: x y z | nx ny nz | id rows
+  const int G = (k + SL - 1) / SL;
+  const int U = gridDim.x;
+  const int id = blockIdx.x;
+  const int u = (U % 8 == 0) ? (id % 8) * (U / 8) + id / 8 : id;
+  const int b = u / (G * pr);
+  const int rem = u - b * G * pr;
+  const int q0 = (rem / pr) * SL;
+  const int span = ((n + pr - 1) / pr + 3) & ~3;  // whole quads
+  const int j0 = (rem % pr) * span, j1 = min(n, j0 + span);
+  const int nq = (j1 - j0) >> 2;
+  const int sl = min(SL, k - q0);
+  const int tid = threadIdx.x;
+  const PpfLds L = ppf_lds_layout(n, SL, npad, 16);
+  const float* nl_s = cl_s + L.nrm_off / 4;
+  const int* id_s = (const int*)(cl_s + L.ids_off / 4);
+  lds_dma_copy<16>(cl_s, xyz + (size_t)b * 3 * n, 12 * n);
+  lds_dma_copy<16>((float*)nl_s, nrm + (size_t)b * 3 * n, 12 * n);
+  lds_dma_copy<16>((int*)id_s, sidx + ((size_t)b * kKnnSortedK + q0) * npad, 4 * sl * npad);
+  wait_vmcnt<0>();
+  __syncthreads();
+  float* O = out + (size_t)b * 4 * k * n;
+  int* I = idx_out + (size_t)b * k * n;
+  const int* pinv = inv + (size_t)b * n;
+  for (int f = tid; f < sl * nq; f += NT) {
+    const int s = f / nq;
+    const int j = j0 + 4 * (f - s * nq);
+    const int q = q0 + s;
+    // the quad's rows in sorted order (inv), its ids, centres and neighbours
+    const int4 pv = *(const int4*)(pinv + j);
+    const int pp[4] = {pv.x, pv.y, pv.z, pv.w};
+    int jd[4];
+    float ce[4][6], nb[4][6], o[4][4];
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+      jd[m] = id_s[s * npad + pp[m]];
+      const unsigned si = (jd[m] < 0 || jd[m] >= n) ? 0u : (unsigned)jd[m];
+      nb[m][0] = cl_s[si];
+      nb[m][1] = cl_s[n + si];
+      nb[m][2] = cl_s[2 * n + si];
+      nb[m][3] = nl_s[si];
+      nb[m][4] = nl_s[n + si];
+      nb[m][5] = nl_s[2 * n + si];
+    }
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+      const float4 cv = *(const float4*)(cl_s + a * n + j);
+      const float4 nv = *(const float4*)(nl_s + a * n + j);
+      ce[0][a] = cv.x;
+      ce[1][a] = cv.y;
+      ce[2][a] = cv.z;
+      ce[3][a] = cv.w;
+      ce[0][3 + a] = nv.x;
+      ce[1][3 + a] = nv.y;
+      ce[2][3 + a] = nv.z;
+      ce[3][3 + a] = nv.w;
+    }
+    __builtin_nontemporal_store(ppf_i4{jd[0], jd[1], jd[2], jd[3]}, (ppf_i4*)(I + (size_t)q * n + j));
+    ppf_local_dev<4>(ce, nb, relative, o);
+#pragma unroll
+    for (int ch = 0; ch < 4; ch++)
+      __builtin_nontemporal_store(ppf_f4{o[0][ch], o[1][ch], o[2][ch], o[3][ch]},
+                                  (ppf_f4*)(O + ((size_t)ch * k + q) * n + j));
   }
 }
 
@@ -1030,11 +1241,23 @@ extern "C" pcr_status pcr_knn_ppf_sorted(const float* xyz, const float* normals,
   // 160 us), so those keep one workgroup per (cloud, 4 slots).
   constexpr int SL = 4;
   const int pr = PCR_KNOB("PCR_PPF_RANGES", n <= 1024 ? ceil_div(n, 512) : 1);
-  const size_t lds = ((size_t)6 * n + (size_t)SL * npad) * 4;
-  allow_big_lds(local_ppf_cloud_kernel<SL>, lds);
-  hipLaunchKernelGGL((local_ppf_cloud_kernel<SL>), dim3(b * ceil_div(k, SL) * pr), dim3(512), lds,
-                     as_stream(stream), xyz, normals, n, k, relative, ppf, sidx, inv, npad, idx,
-                     pr);
+  // 16-byte LDS-DMA pieces and output vectors when every row is 16-byte
+  // aligned: four points per thread (local_ppf_quad_kernel)
+  const bool v16 = n % 4 == 0 && npad % 4 == 0 &&
+                   (((uintptr_t)xyz | (uintptr_t)normals | (uintptr_t)sidx | (uintptr_t)inv |
+                     (uintptr_t)idx | (uintptr_t)ppf) & 15) == 0;
+  const dim3 grid(b * ceil_div(k, SL) * pr);
+  if (v16) {
+    const size_t lds = ppf_lds_layout(n, SL, npad, 16).bytes;
+    allow_big_lds(local_ppf_quad_kernel<SL>, lds);
+    hipLaunchKernelGGL((local_ppf_quad_kernel<SL>), grid, dim3(512), lds, as_stream(stream),
+                       xyz, normals, n, k, relative, ppf, sidx, inv, npad, idx, pr);
+  } else {
+    const size_t lds = ppf_lds_layout(n, SL, npad, 4).bytes;
+    allow_big_lds(local_ppf_cloud_kernel<SL, 4>, lds);
+    hipLaunchKernelGGL((local_ppf_cloud_kernel<SL, 4>), grid, dim3(512), lds, as_stream(stream),
+                       xyz, normals, n, k, relative, ppf, sidx, inv, npad, idx, pr);
+  }
   return launch_status("knn_ppf_sorted");
 }
 

@@ -887,18 +887,6 @@ constexpr int kStreamNB = 3;     // means buffers (item t streams, t+1 ready, t+
 constexpr int kStreamMaxN = 2048;  // two rows of ms <= 2052 floats: 17 pieces past 1024 points
 constexpr int kStreamMaxW = 1024;  // occupancy words (r^3 <= 32768)
 
-typedef __attribute__((address_space(3))) void* lds_void_p;
-typedef __attribute__((address_space(1))) void* gbl_void_p;
-
-// s_waitcnt vmcnt(N) only (gfx9 encoding: expcnt / lgkmcnt at their maxima)
-template <int N>
-__device__ inline void wait_vmcnt() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);  // compiler-only (the builtin is IntrNoMem)
-  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
-}
-
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 template <int NS, int NB, int U, int AUX, int G = kStreamG, int NG = kStreamNG>
 __global__ __launch_bounds__((NS + 1) * 64) void vox_stream_kernel(int c, int n, int r3, VoxWs ws,
