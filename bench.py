@@ -78,13 +78,8 @@ def parse(argv=None):
     ap.add_argument("--kernel-iters", type=int, default=50, help="(kept for old command lines)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--schedule", type=int, choices=(1, 2, 3, 4, 5, 6, 7), default=None,
-                    help="pcr_extractor_run schedule (include/pcr_amd.h): 1 = three streams "
-                         "(sort+select+PPF / prep+means+devox / dense-grid stream), 2 = as 1 "
-                         "with the Morton sort on the prep stream, 3 = as 1 with the local PPF "
-                         "on a fourth stream beside the next step's sort + selection, 4 = as 1 "
-                         "with three voxel workspaces and the grid stream alternating between "
-                         "two queues, 5 = as 4 with the local PPF on the grid queues, 6 = two "
+    ap.add_argument("--schedule", type=int, choices=(6, 7), default=None,
+                    help="pcr_extractor_run schedule (include/pcr_amd.h): 6 = two "
                          "independent pipelines per chain (voxel chain on s_vox / origin, KNN "
                          "chain on s_nbr / s_pre by step parity), no cross-queue events, 7 = as 6 "
                          "with three voxel queues (s_vox / origin / s_pre) and one KNN queue; default "
@@ -98,6 +93,10 @@ def parse(argv=None):
                          "batch ahead, overlapping the previous step's backwards "
                          "(SphExtractor.pipelined_steps); serial = forward (joined), then "
                          "the backwards")
+    ap.add_argument("--cu-split", type=float, default=0.0,
+                    help="extract diagnostic: the KNN queues on this fraction of the CUs, the "
+                         "voxel queues (s_vox and the caller's stream) on the rest (CU-masked "
+                         "HIP streams); 0 = off")
     ap.add_argument("--c3-cu-split", type=float, default=0.0,
                     help="c3 diagnostic: run the neighbour stream on this fraction of the CUs "
                          "and the caller's chain on the rest (CU-masked HIP streams); 0 = off")
@@ -315,6 +314,10 @@ class ExtractWorkload:
             self.ex = PairExtractor(b // 2, n, c, k, r, device=dev)
         else:
             self.ex = SphExtractor(b, n, c, k, r, device=dev)
+        self.origin = None
+        if args.cu_split > 0:
+            sx = self.ex.ex if args.workload == "pairs" else self.ex
+            sx.s_nbr, sx.s_pre, sx.s_vox, self.origin = cu_masked_streams(args.cu_split, dev, 2)
         self.S = max(1, args.steps_per_launch)
         self.next_set = 0
         self.desc_steps = {}
@@ -403,7 +406,13 @@ class ExtractWorkload:
             self.next_set = (self.next_set + m) % self.R
             return self.desc_steps[m]
 
-        return run_pipelined(steps, self.S, launch, self.pipe)
+        if self.origin is None:
+            return run_pipelined(steps, self.S, launch, self.pipe)
+        self.origin.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(self.origin):
+            out = run_pipelined(steps, self.S, launch, self.pipe)
+        torch.cuda.current_stream(self.dev).wait_stream(self.origin)
+        return out
 
     def kernel_report(self):
         ms = self.ex.grid_kernel_times()
@@ -443,6 +452,7 @@ class ExtractWorkload:
                 "global_batch": b * self.world,
                 "parallelism": "dp%d (clouds sharded, descriptor all-gather)" % self.world,
                 "schedule": a.schedule,
+                "cu_split": a.cu_split or None,
                 "runner_calls": [len(self.chunks(a.warmup)), len(self.chunks(a.steps))],
                 "steps_per_launch": self.S,
                 "distinct_batches": self.R}
@@ -623,12 +633,14 @@ def c3_selection_timed(ms):
     return bool(ms) and all(t > 0 for t in ms)
 
 
-def cu_masked_streams(frac, dev):
-    """Two HIP streams on complementary CU masks (hipExtStreamCreateWithCUMask
-    of the runtime torch loaded): `frac` of every 8 consecutive CU bits for
-    the first.  Returns torch ExternalStreams (diagnostic)."""
+def cu_masked_streams(frac, dev, copies=1):
+    """HIP streams on complementary CU masks (pcr_stream_create_cu_mask):
+    `frac` of every 8 consecutive CU bits for the first `copies` streams, the
+    rest for the next `copies`.  Returns torch ExternalStreams (diagnostic;
+    the streams live for the process)."""
     import ctypes
-    hip = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"))
+    from pcr_amd import _lib
+    lib = _lib.load()
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
     words = (ncu + 31) // 32
     take = max(1, min(7, int(round(frac * 8))))
@@ -641,11 +653,11 @@ def cu_masked_streams(frac, dev):
             bm[cu // 32] |= 1 << (cu % 32)
     out = []
     for mask in (a, bm):
-        st = ctypes.c_void_p()
-        rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(st), ctypes.c_uint32(words), mask)
-        if rc != 0:
-            raise SystemExit("bench: hipExtStreamCreateWithCUMask failed (%d)" % rc)
-        out.append(torch.cuda.ExternalStream(st.value, device=dev))
+        for _ in range(copies):
+            st = ctypes.c_void_p()
+            _lib.check(lib.pcr_stream_create_cu_mask(mask, words, ctypes.byref(st)),
+                       "stream_create_cu_mask")
+            out.append(torch.cuda.ExternalStream(st.value, device=dev))
     return out
 
 

@@ -42,6 +42,12 @@ typedef int pcr_status;
 const char *pcr_last_error(void);
 /* Library version string. */
 const char *pcr_version(void);
+/* A HIP stream restricted to the CUs set in mask (nwords 32-bit words, bit
+ * i = CU i of the runtime's numbering; hipExtStreamCreateWithCUMask), and its
+ * release.  No reference counterpart: a scheduling tool for the runner's
+ * queues. */
+pcr_status pcr_stream_create_cu_mask(const unsigned *mask, int nwords, void **stream);
+pcr_status pcr_stream_destroy(void *stream);
 
 /* ---------------------------------------------------------------- KNN ----
  * knn_forward_cuda (modules/functional/src/knn/knn.cpp:6-25, kernel
@@ -390,26 +396,11 @@ pcr_status pcr_read_xyzn_txt(const char *path, float *out, long long rows, int c
  * measures), enqueued from native code: every launch and cross-stream event
  * of every step is issued here, so the host enqueue rate never limits the
  * step rate.  Forked from and joined back into `origin`.
- *   schedule 0: two streams -- s_nbr: Morton sort, KNN selection, local PPF;
- *               s_vox: prep + the fused grid / devox / descriptor kernel.
- *   schedule 1: three streams -- s_nbr as above; s_pre: prep + means / devox
- *               / descriptor of step s into buffer set s % 2 (after the grid
- *               stream of step s-2 read it); s_vox: the grid stream of step s.
- *   schedule 2: as 1, with the Morton sort moved to s_pre (ahead of prep, into
- *               KNN workspace s % 2 after the selection of step s-2 read it),
- *               so s_nbr only selects and computes the local PPF.
- *   schedule 3: as 1, with the local PPF of step s on `origin` (a fourth
- *               stream) after the selection of step s, beside the sort +
- *               selection of step s+1 on s_nbr (KNN workspace s % 2, reused
- *               by step s+2 after that PPF read it).
- *   schedule 4: as 1, with three voxel workspaces (step s in s % 3, reused
- *               by step s+3) and the grid-stream kernels of even steps on
- *               s_vox, of odd steps on `origin`: a stream kernel's completion
- *               (its write stream drained, ~10 us after its last wave) is no
- *               longer on the next step's path.
- *   schedule 5: as 4, with the local PPF of step s on step s's grid queue,
- *               ahead of its grid stream (s_nbr only sorts and selects; KNN
- *               workspace s % 2, reused by step s+2 after that PPF).
+ *   schedule 0: serial, two streams -- s_nbr: Morton sort, KNN selection,
+ *               local PPF; s_vox: prep + the fused grid / devox / descriptor
+ *               kernel; the single set of buffers (or ring set s).
+ *   (schedules 1-5, single-queue-per-stage variants measured in rounds 2-4,
+ *   were removed: DESIGN.md 4.)
  *   schedule 6: two independent pipelines per chain and no cross-queue event
  *               inside the run: the voxel chain (prep, means / devox /
  *               descriptor, matching, grid stream) of step s on s_vox (even
@@ -428,7 +419,8 @@ pcr_status pcr_read_xyzn_txt(const char *path, float *out, long long rows, int c
  *               ring size is not a multiple of 3.  Schedules 6 / 7 with
  *               match_pairs: each voxel queue matches in its own part (half
  *               / third) of match_ws.
- * Buffers with two entries are the alternating sets (schedule 0 uses set 0).
+ * Buffers with two entries: schedule 0 uses entry 0; schedules 6 / 7 use
+ * knn_ws[q] / vox_ws[q] (+ vox_ws3) as the queue's workspace.
  * desc_steps: [steps][b][c] per-step descriptors, or NULL (then desc).
  *
  * `runner` holds the run's cross-stream events, created once by
@@ -440,12 +432,12 @@ pcr_status pcr_read_xyzn_txt(const char *path, float *out, long long rows, int c
  * pcr_runner_grid_times waits for them and returns the per-step durations
  * (ms) of the last run -- the dominant kernel's in-step duration.
  *
- * Batch ring (nsets > 0, schedules 1 to 6): step s of a call reads its clouds
+ * Batch ring (nsets > 0; required by schedules 6 and 7): step s of a call reads its clouds
  * from, and writes every output into, sets[(set0 + s) % nsets] -- a fresh
  * batch per step, as the reference's loaders hand one over per iteration
  * (datasets/deepgmr_mn40.py:71-97, train.py:138-153) -- and the single-set
  * input / output pointers of pcr_extractor_args are ignored (the workspaces
- * stay the alternating scratch pair).  With steps <= nsets every step of a
+ * stay per queue).  With steps <= nsets every step of a
  * call writes its own set, so after the call (all streams joined back into
  * `origin`) the outputs of every step are readable on `origin`; the next
  * call forks from `origin` after whatever the caller enqueued there, so a
@@ -493,14 +485,15 @@ typedef struct pcr_extractor_args {
   int match_pairs;
   int *corr12, *corr21, *idx1, *idx2, *match_count;
   void *match_ws;                         /* pcr_mutual_nn_workspace_size(P, n, n);
-                                             schedule 6: twice that + 512 B (one
-                                             half per voxel queue) */
+                                             schedules 6 / 7: two / three times
+                                             that + 512 B (one part per voxel
+                                             queue) */
   size_t match_ws_bytes;
   /* batch ring (see above): nsets sets, step s of the call uses set
    * (set0 + s) % nsets; nsets = 0: the single set above */
   int nsets, set0;
   const pcr_extractor_set *sets;
-  /* schedule 4: the third voxel workspace (vox_ws_bytes) */
+  /* schedule 7: the third voxel workspace (vox_ws_bytes) */
   void *vox_ws3;
 } pcr_extractor_args;
 pcr_status pcr_extractor_run(pcr_runner *runner, const pcr_extractor_args *args, int steps,

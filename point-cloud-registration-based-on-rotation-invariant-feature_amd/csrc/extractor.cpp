@@ -17,7 +17,7 @@ namespace {
 // every pcr_extractor_run call.  A wait captures the event's most recent
 // record at the time it is enqueued, so re-recording across steps and calls
 // keeps the same ordering as fresh events.
-constexpr int kSyncEvents = 14;
+constexpr int kSyncEvents = 8;
 }  // namespace
 }  // namespace pcr
 
@@ -209,8 +209,8 @@ extern "C" pcr_status pcr_runner_grid_times(pcr_runner* rn, float* ms, int cap, 
 extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_args* a,
                                         int steps, int schedule, float* desc_steps, void* origin,
                                         void* s_nbr_p, void* s_pre_p, void* s_vox_p) {
-  PCR_REQUIRE(a != nullptr && steps >= 0 && schedule >= 0 && schedule <= 7,
-              "extractor_run: invalid arguments");
+  PCR_REQUIRE(a != nullptr && steps >= 0 && (schedule == 0 || schedule == 6 || schedule == 7),
+              "extractor_run: invalid arguments (schedule 0, 6 or 7)");
   PCR_REQUIRE(a->b >= 0 && a->n >= 1 && a->c >= 1 && a->k >= 1 && a->r >= 1,
               "extractor_run: invalid sizes");
   PCR_REQUIRE(a->match_pairs <= 0 || a->b == 2 * a->match_pairs,
@@ -219,13 +219,13 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
   if (steps == 0 || a->b == 0) return PCR_OK;
   const hipStream_t org = as_stream(origin), sn = as_stream(s_nbr_p), sp = as_stream(s_pre_p),
                     sv = as_stream(s_vox_p);
-  const int nslots = schedule >= 1 ? 2 : 1;
-  PCR_REQUIRE(a->nsets >= 0 && (a->nsets == 0 || (a->sets && schedule >= 1 && a->set0 >= 0)),
-              "extractor_run: a batch ring needs sets, set0 >= 0 and schedule >= 1");
+  PCR_REQUIRE(a->nsets >= 0 && (a->nsets == 0 || (a->sets && a->set0 >= 0)),
+              "extractor_run: a batch ring needs sets and set0 >= 0");
   // schedules 6 / 7: nvq voxel queues and nkq KNN queues, each running a
   // whole chain of every nvq-th / nkq-th step
   const int nvq = schedule == 7 ? 3 : 2, nkq = schedule == 7 ? 1 : 2;
   const bool multi = schedule >= 6;
+  const int nvws = multi ? nvq : 1, nkws = multi ? nkq : 1;  // workspaces in use
   // consecutive steps are written from different queues: they need distinct
   // output sets (the c5 voxel path counts into cnt with atomics)
   PCR_REQUIRE(!multi || a->nsets >= nvq,
@@ -238,12 +238,15 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
                       pcr_mutual_nn_workspace_size(a->match_pairs, a->n, a->n),
               "extractor_run: schedule %d with match_pairs needs a matching workspace of "
               "%d x pcr_mutual_nn_workspace_size (plus 512 B)", schedule, nvq);
-  PCR_REQUIRE(schedule < 4 || schedule == 6 || a->vox_ws3 != nullptr,
-              "extractor_run: schedules 4, 5 and 7 need the third voxel workspace (vox_ws3)");
-  for (int q = 0; q < nslots; q++)
-    PCR_REQUIRE(a->vox_ws[q] && a->knn_ws[schedule >= 2 ? q : 0] &&
-                    (a->nsets > 0 || (a->dinds[q] && a->dwgts[q])),
-                "extractor_run: buffer set %d missing", q);
+  PCR_REQUIRE(schedule != 7 || a->vox_ws3 != nullptr,
+              "extractor_run: schedule 7 needs the third voxel workspace (vox_ws3)");
+  void* const vws[3] = {a->vox_ws[0], a->vox_ws[1], a->vox_ws3};
+  for (int q = 0; q < nvws; q++)
+    PCR_REQUIRE(vws[q] != nullptr, "extractor_run: voxel workspace %d missing", q);
+  for (int q = 0; q < nkws; q++)
+    PCR_REQUIRE(a->knn_ws[q] != nullptr, "extractor_run: KNN workspace %d missing", q);
+  PCR_REQUIRE(a->nsets > 0 || (a->dinds[0] && a->dwgts[0]),
+              "extractor_run: devox corner buffers missing");
   for (int t = 0; t < a->nsets; t++)
     PCR_REQUIRE(a->sets[t].xyz && a->sets[t].normals && a->sets[t].features &&
                     a->sets[t].knn_idx && a->sets[t].local_ppf && a->sets[t].grid &&
@@ -261,19 +264,13 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
     ~Owned() { delete p; }
   } owned{tmp};
   pcr_runner* const rn = runner;
-  rn->timed_last = schedule == 0 ? 0 : steps < rn->timed_want ? steps : rn->timed_want;
+  rn->timed_last = !multi ? 0 : steps < rn->timed_want ? steps : rn->timed_want;
   // the timed_last steps in the MIDDLE of the run are timed: the pipeline
   // is full there (the last steps' grid kernels run beside a draining
   // pipeline: at c2 under schedule 6 ~64 us against ~102 us in steady state)
   const int t_first = (steps - rn->timed_last) / 2;
   hipEvent_t* e = rn->sync;
-  hipEvent_t fork = e[0], means_done[3] = {e[1], e[2], e[8]},
-             stream_done[3] = {e[3], e[4], e[9]}, join[3] = {e[5], e[6], e[7]},
-             sort_done[2] = {e[8], e[9]}, sel_done[2] = {e[10], e[11]},
-             ppf_done[2] = {e[12], e[13]};
-  // schedule 4: three voxel workspaces (step s in s % 3) and the grid-stream
-  // kernels of consecutive steps on alternating queues (s_vox, origin)
-  void* const vws[3] = {a->vox_ws[0], a->vox_ws[1], a->vox_ws3};
+  hipEvent_t fork = e[0], means_done[2] = {e[1], e[2]}, join[3] = {e[5], e[6], e[7]};
   // schedules 6 / 7 over a ring that one call wraps onto other queues
   // (nsets not a multiple of the queue count): per-set events, made once
   // per ring size (the first call, outside any timed region)
@@ -290,8 +287,7 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
   for (hipStream_t st : {sn, sp, sv}) PCR_HIP(hipStreamWaitEvent(st, fork, 0), "fork wait");
   const size_t dstride = (size_t)a->b * a->c;
   for (int s = 0; s < steps; s++) {
-    const int q = schedule >= 1 ? (s & 1) : 0;  // scratch slot
-    const StepIO io = step_io(a, s, q);
+    const StepIO io = step_io(a, s, 0);
     float* desc = desc_steps ? desc_steps + (size_t)s * dstride : io.desc;
     bool sorted = false;
     if (schedule == 0) {
@@ -304,137 +300,51 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
       PCR_TRY(match_pairs(a, io, sv));
       continue;
     }
-    if (multi) {
-      // independent pipelines per chain, no cross-queue events: the voxel
-      // chain (prep, means / devox, match, grid stream) of step s on voxel
-      // queue s % nvq with voxel workspace s % nvq, the KNN chain (sort,
-      // selection, local PPF) on KNN queue s % nkq with KNN workspace s % nkq;
-      // every workspace is reused only by its own queue.  Schedule 6: voxel
-      // queues {s_vox, origin}, KNN queues {s_nbr, s_pre}; schedule 7: voxel
-      // queues {s_vox, origin, s_pre}, KNN queue s_nbr
-      const hipStream_t vqs[3] = {sv, org, sp}, kqs[2] = {sn, sp};
-      const int iv = s % nvq, ik = s % nkq;
-      const hipStream_t vq = vqs[iv], kq = kqs[ik];
-      void* const vw6 = vws[iv];
-      const int t = a->nsets > 0 ? (a->set0 + s) % a->nsets : 0;
-      hipEvent_t* const rv = ring_wait ? rn->ring_ev.data() : nullptr;
-      if (rv && s >= a->nsets) {  // set t last written on the other queues
-        PCR_HIP(hipStreamWaitEvent(vq, rv[2 * t], 0), "ring wait");
-        PCR_HIP(hipStreamWaitEvent(kq, rv[2 * t + 1], 0), "ring wait");
-      }
-      auto knn_part = [&]() -> pcr_status {
-        PCR_TRY(knn_sort(a, io, ik, kq, &sorted));
-        return knn_select_ppf(a, io, ik, sorted, kq);
-      };
-      auto vox_part = [&]() -> pcr_status {
-        // voxel queue i > 0 starts after step i - 1's means, so the queues'
-        // grid streams take turns rather than coincide (aligned, they fight
-        // for HBM and then leave it idle together)
-        if (s >= 1 && s < nvq) PCR_HIP(hipStreamWaitEvent(vq, means_done[s - 1], 0), "offset wait");
-        PCR_TRY(pcr_extractor_voxel_prep(io.xyz, a->b, a->n, a->r, io.norm_coords, io.ind,
-                                         io.dinds, io.dwgts, vw6, a->vox_ws_bytes, vq));
-        PCR_TRY(pcr_extractor_voxel_means_devox(io.features, a->b, a->c, a->n, a->r, io.devox,
-                                                io.dinds, io.dwgts, desc, vw6, a->vox_ws_bytes,
-                                                vq));
-        if (s < nvq - 1) PCR_HIP(hipEventRecord(means_done[s], vq), "offset record");
-        PCR_TRY(match_pairs(a, io, vq, iv, nvq));
-        const bool timed = s >= t_first && s < t_first + rn->timed_last;
-        if (timed) PCR_HIP(hipEventRecord(rn->t0[s - t_first], vq), "timing record");
-        PCR_TRY(pcr_extractor_voxel_stream(a->b, a->c, a->n, a->r, io.cnt, io.grid, vw6,
-                                           a->vox_ws_bytes, vq));
-        if (timed) PCR_HIP(hipEventRecord(rn->t1[s - t_first], vq), "timing record");
-        return PCR_OK;
-      };
-      PCR_TRY(knn_part());
-      PCR_TRY(vox_part());
-      if (rv && s + a->nsets < steps) {
-        PCR_HIP(hipEventRecord(rv[2 * t], vq), "ring record");
-        PCR_HIP(hipEventRecord(rv[2 * t + 1], kq), "ring record");
-      }
-      continue;
+    // independent pipelines per chain, no cross-queue events: the voxel
+    // chain (prep, means / devox, match, grid stream) of step s on voxel
+    // queue s % nvq with voxel workspace s % nvq, the KNN chain (sort,
+    // selection, local PPF) on KNN queue s % nkq with KNN workspace s % nkq;
+    // every workspace is reused only by its own queue.  Schedule 6: voxel
+    // queues {s_vox, origin}, KNN queues {s_nbr, s_pre}; schedule 7: voxel
+    // queues {s_vox, origin, s_pre}, KNN queue s_nbr
+    const hipStream_t vqs[3] = {sv, org, sp}, kqs[2] = {sn, sp};
+    const int iv = s % nvq, ik = s % nkq;
+    const hipStream_t vq = vqs[iv], kq = kqs[ik];
+    void* const vw6 = vws[iv];
+    const int t = a->nsets > 0 ? (a->set0 + s) % a->nsets : 0;
+    hipEvent_t* const rv = ring_wait ? rn->ring_ev.data() : nullptr;
+    if (rv && s >= a->nsets) {  // set t last written on the other queues
+      PCR_HIP(hipStreamWaitEvent(vq, rv[2 * t], 0), "ring wait");
+      PCR_HIP(hipStreamWaitEvent(kq, rv[2 * t + 1], 0), "ring wait");
     }
-    if (schedule == 2) {
-      if (s >= 2) PCR_HIP(hipStreamWaitEvent(sp, sel_done[q], 0), "knn slot wait");
-      PCR_TRY(knn_sort(a, io, q, sp, &sorted));
-      PCR_HIP(hipEventRecord(sort_done[q], sp), "sort record");
-    }
-    // voxel workspace slot and the queue of this step's grid stream
-    const int nv = schedule >= 4 ? 3 : 2;
-    const int qv = s % nv;
-    void* const vw = vws[qv];
-    const hipStream_t sg = (schedule >= 4 && (s & 1)) ? org : sv;
-    if (schedule == 5) {
-      // sort + selection of step s on s_nbr into KNN workspace q; the local
-      // PPF of step s on this step's grid queue, ahead of its grid stream
-      // (each grid queue runs every other step, so it has the time)
-      if (s >= 2) PCR_HIP(hipStreamWaitEvent(sn, ppf_done[q], 0), "knn slot wait");
-      PCR_TRY(knn_sort(a, io, q, sn, &sorted));
-      pcr_status rs = PCR_ERR_UNSUPPORTED;
-      if (sorted && !io.knn_dist)
-        rs = pcr_knn_select_sorted(io.xyz, a->b, a->n, a->k, a->knn_ws[q], a->knn_ws_bytes, sn);
-      if (rs == PCR_OK) {
-        PCR_HIP(hipEventRecord(sel_done[q], sn), "select record");
-        PCR_HIP(hipStreamWaitEvent(sg, sel_done[q], 0), "select wait");
-        PCR_TRY(pcr_knn_ppf_sorted(io.xyz, io.normals, a->b, a->n, a->k, a->relative,
-                                   io.knn_idx, io.local_ppf, a->knn_ws[q], a->knn_ws_bytes, sg));
-        PCR_HIP(hipEventRecord(ppf_done[q], sg), "ppf record");
-      } else {
-        if (rs != PCR_ERR_UNSUPPORTED) return rs;
-        PCR_TRY(knn_select_ppf(a, io, q, sorted, sn));
-        PCR_HIP(hipEventRecord(ppf_done[q], sn), "ppf record");
-      }
-    }
-    if (s >= nv) PCR_HIP(hipStreamWaitEvent(sp, stream_done[qv], 0), "slot wait");
-    PCR_TRY(pcr_extractor_voxel_prep(io.xyz, a->b, a->n, a->r, io.norm_coords, io.ind, io.dinds,
-                                       io.dwgts, vw, a->vox_ws_bytes, sp));
-    PCR_TRY(pcr_extractor_voxel_means_devox(io.features, a->b, a->c, a->n, a->r, io.devox,
-                                            io.dinds, io.dwgts, desc, vw, a->vox_ws_bytes, sp));
-    PCR_HIP(hipEventRecord(means_done[qv], sp), "means record");
-    PCR_TRY(match_pairs(a, io, sp));
-    PCR_HIP(hipStreamWaitEvent(sg, means_done[qv], 0), "means wait");
-    const bool timed = s >= t_first && s < t_first + rn->timed_last;
-    if (timed) PCR_HIP(hipEventRecord(rn->t0[s - t_first], sg), "timing record");
-    PCR_TRY(pcr_extractor_voxel_stream(a->b, a->c, a->n, a->r, io.cnt, io.grid, vw,
-                                       a->vox_ws_bytes, sg));
-    if (timed) PCR_HIP(hipEventRecord(rn->t1[s - t_first], sg), "timing record");
-    PCR_HIP(hipEventRecord(stream_done[qv], sg), "stream record");
-    if (schedule == 2) {
-      PCR_HIP(hipStreamWaitEvent(sn, sort_done[q], 0), "sort wait");
-      // (the PPF launch reads the workspace too: the slot is free after it)
-      PCR_TRY(knn_select_ppf(a, io, q, sorted, sn));
-      PCR_HIP(hipEventRecord(sel_done[q], sn), "select record");
-    } else if (schedule == 3) {
-      // sort + selection of step s on s_nbr into KNN workspace q, the local
-      // PPF of step s on `origin` (the fourth stream) after it, so the PPF of
-      // step s runs beside the sort + selection of step s + 1; workspace q
-      // is rewritten by step s + 2 only after the PPF of step s read it
-      if (s == 0) PCR_HIP(hipStreamWaitEvent(sn, means_done[q], 0), "head wait");
-      if (s >= 2) PCR_HIP(hipStreamWaitEvent(sn, ppf_done[q], 0), "knn slot wait");
-      PCR_TRY(knn_sort(a, io, q, sn, &sorted));
-      pcr_status rs = PCR_ERR_UNSUPPORTED;
-      if (sorted && !io.knn_dist)
-        rs = pcr_knn_select_sorted(io.xyz, a->b, a->n, a->k, a->knn_ws[q], a->knn_ws_bytes, sn);
-      if (rs == PCR_OK) {
-        PCR_HIP(hipEventRecord(sel_done[q], sn), "select record");
-        PCR_HIP(hipStreamWaitEvent(org, sel_done[q], 0), "select wait");
-        PCR_TRY(pcr_knn_ppf_sorted(io.xyz, io.normals, a->b, a->n, a->k, a->relative,
-                                   io.knn_idx, io.local_ppf, a->knn_ws[q], a->knn_ws_bytes, org));
-        PCR_HIP(hipEventRecord(ppf_done[q], org), "ppf record");
-      } else {
-        if (rs != PCR_ERR_UNSUPPORTED) return rs;
-        // no sorted rows (k > 32, clouds past 2048 points, distances
-        // requested): selection + PPF on s_nbr as schedule 1
-        PCR_TRY(knn_select_ppf(a, io, q, sorted, sn));
-        PCR_HIP(hipEventRecord(ppf_done[q], sn), "ppf record");
-      }
-    } else if (schedule != 5) {
-      // the first step's neighbour stream starts after that step's voxel
-      // means: prep + means (the grid stream's chain) get the chip first, so
-      // the grid stream starts ~1/3 sooner (a 20-step call: 289k -> 298k
-      // clouds/s; long runs unchanged)
-      if (s == 0) PCR_HIP(hipStreamWaitEvent(sn, means_done[q], 0), "head wait");
-      PCR_TRY(knn_sort(a, io, 0, sn, &sorted));
-      PCR_TRY(knn_select_ppf(a, io, 0, sorted, sn));
+    auto knn_part = [&]() -> pcr_status {
+      PCR_TRY(knn_sort(a, io, ik, kq, &sorted));
+      return knn_select_ppf(a, io, ik, sorted, kq);
+    };
+    auto vox_part = [&]() -> pcr_status {
+      // voxel queue i > 0 starts after step i - 1's means, so the queues'
+      // grid streams take turns rather than coincide (aligned, they fight
+      // for HBM and then leave it idle together)
+      if (s >= 1 && s < nvq) PCR_HIP(hipStreamWaitEvent(vq, means_done[s - 1], 0), "offset wait");
+      PCR_TRY(pcr_extractor_voxel_prep(io.xyz, a->b, a->n, a->r, io.norm_coords, io.ind,
+                                       io.dinds, io.dwgts, vw6, a->vox_ws_bytes, vq));
+      PCR_TRY(pcr_extractor_voxel_means_devox(io.features, a->b, a->c, a->n, a->r, io.devox,
+                                              io.dinds, io.dwgts, desc, vw6, a->vox_ws_bytes,
+                                              vq));
+      if (s < nvq - 1) PCR_HIP(hipEventRecord(means_done[s], vq), "offset record");
+      PCR_TRY(match_pairs(a, io, vq, iv, nvq));
+      const bool timed = s >= t_first && s < t_first + rn->timed_last;
+      if (timed) PCR_HIP(hipEventRecord(rn->t0[s - t_first], vq), "timing record");
+      PCR_TRY(pcr_extractor_voxel_stream(a->b, a->c, a->n, a->r, io.cnt, io.grid, vw6,
+                                         a->vox_ws_bytes, vq));
+      if (timed) PCR_HIP(hipEventRecord(rn->t1[s - t_first], vq), "timing record");
+      return PCR_OK;
+    };
+    PCR_TRY(knn_part());
+    PCR_TRY(vox_part());
+    if (rv && s + a->nsets < steps) {
+      PCR_HIP(hipEventRecord(rv[2 * t], vq), "ring record");
+      PCR_HIP(hipEventRecord(rv[2 * t + 1], kq), "ring record");
     }
   }
   int i = 0;

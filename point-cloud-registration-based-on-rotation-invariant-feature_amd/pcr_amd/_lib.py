@@ -22,6 +22,8 @@ ST = ctypes.c_int
 SIGNATURES = {
     "pcr_last_error": (ctypes.c_char_p, []),
     "pcr_version": (ctypes.c_char_p, []),
+    "pcr_stream_create_cu_mask": (ST, [P, I, ctypes.POINTER(P)]),
+    "pcr_stream_destroy": (ST, [P]),
     "pcr_knn_forward": (ST, [P, P, I, I, I, I, I, P, P, P, P, P, SZ, P]),
     "pcr_knn_workspace_size": (SZ, [I, I, I]),
     "pcr_knn_backward": (ST, [P, P, P, P, P, P, I, I, I, I, I, P, P, P]),

@@ -495,7 +495,7 @@ class SphExtractor:
         a.vox_ws[0], a.vox_ws[1] = _ptr(self.ws), _ptr(s1[1])
         a.vox_ws_bytes = self.ws.numel()
         if getattr(self, "_ws3", None) is None:
-            # the third voxel workspace of runner schedule 4
+            # the third voxel workspace of runner schedule 7
             self._ws3 = torch.empty_like(self.ws)
             self._order_new_buffers()
         a.vox_ws3 = _ptr(self._ws3)
@@ -510,20 +510,14 @@ class SphExtractor:
             a.match_ws, a.match_ws_bytes = _ptr(match.ws), match.ws.numel()
         return a
 
-    def run_native(self, xyz, normals, features, steps, desc_steps=None, schedule=1,
+    def run_native(self, xyz, normals, features, steps, desc_steps=None, schedule=0,
                    timed=False, match=None):
-        """`steps` pipelined steps enqueued by the library's native runner
-        (pcr_extractor_run): schedule 4 = as 1 with three voxel workspaces and
-        the grid-stream kernels alternating between s_vox and the caller's
-        stream; schedule 3 = as 1 with the local PPF of each step
-        on the caller's stream beside the next step's sort + selection;
-        schedule 1 = three streams (prep + means / devox
-        on s_pre, the grid stream on s_vox, sort + select + PPF on s_nbr,
-        voxel buffer sets alternating), 2 = as 1 with the Morton sort on
-        s_pre, 0 = two streams with the fused grid kernel.  One ctypes call
-        for all steps.  timed: bracket the grid-stream kernel of every step
-        (True) or of N steps in the middle of the run (an int N) with timing events (read
-        back with grid_kernel_times()).  match: a
+        """`steps` steps over the extractor's single buffer set, enqueued by
+        the library's native runner (pcr_extractor_run schedule 0: sort +
+        selection + PPF on s_nbr, prep + the fused grid kernel on s_vox).
+        One ctypes call for all steps.  The pipelined schedules 6 / 7 need
+        distinct output sets per step: run_ring.  timed: only schedules 6 /
+        7 bracket grid-stream kernels (grid_kernel_times()).  match: a
         registration.PairMatch whose buffers receive, every step, the
         mutual-NN matching of clouds [0, B/2) against [B/2, B)."""
         self._check_inputs(xyz, normals, features)
@@ -546,8 +540,7 @@ class SphExtractor:
             runner, ctypes.byref(a), steps, schedule, _ptr(desc_steps), cur.cuda_stream,
             self.s_nbr.cuda_stream, self.s_pre.cuda_stream, self.s_vox.cuda_stream),
             "extractor_run")
-        last = (steps - 1) & 1 if schedule >= 1 else 0
-        return self.outputs(slot=last)
+        return self.outputs(slot=0)
 
     # ------------------------------------------------------------ batch ring
     def ring_outputs(self, nsets, match_pairs=0):
@@ -579,18 +572,22 @@ class SphExtractor:
         self._order_new_buffers()
         return ring
 
-    def run_ring(self, batches, steps, set0=0, desc_steps=None, schedule=1, timed=False,
+    def run_ring(self, batches, steps, set0=0, desc_steps=None, schedule=6, timed=False,
                  match=None):
         """`steps` pipelined steps of the native runner over a batch ring
         (pcr_extractor_run with nsets = len(batches)): step s reads the
         clouds of batches[(set0 + s) % R] = (xyz, normals, features) and
         writes every output into ring_outputs(R)[(set0 + s) % R], so with
         steps <= R each step's outputs survive the call and are readable on
-        the current stream after it.  match: a
+        the current stream after it.  schedule 6: two voxel
+        and two KNN queues, 7: three voxel queues and one KNN queue, 0:
+        serial.  timed: bracket the grid-stream kernel of every step (True)
+        or of N steps in the middle of the run (an int N) with timing events
+        (grid_kernel_times()).  match: a
         registration.PairMatch (its workspace; the matching outputs go to
         the ring sets).  Returns the ring's output sets."""
-        if schedule not in (1, 2, 3, 4, 5, 6, 7):
-            raise RuntimeError("run_ring needs schedule 1 to 7")
+        if schedule not in (0, 6, 7):
+            raise RuntimeError("run_ring needs schedule 0, 6 or 7")
         if schedule >= 6 and len(batches) < schedule - 4:
             raise RuntimeError("run_ring schedule %d needs at least %d batches"
                                % (schedule, schedule - 4))

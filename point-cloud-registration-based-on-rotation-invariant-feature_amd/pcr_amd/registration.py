@@ -73,17 +73,17 @@ class PairExtractor:
         out.update(zip(("corr12", "corr21", "idx1", "idx2", "count"), got))
         return out
 
-    def run_native(self, xyz, normals, features, steps, desc_steps=None, schedule=1,
+    def run_native(self, xyz, normals, features, steps, desc_steps=None, schedule=0,
                    timed=False):
-        """`steps` pipelined steps of extraction + matching from one native
-        runner call; the matching outputs of the last step stay in
-        self.match."""
+        """`steps` serial steps of extraction + matching from one native
+        runner call (schedule 0); the matching outputs of the last step stay
+        in self.match."""
         out = dict(self.ex.run_native(xyz, normals, features, steps, desc_steps,
                                       schedule=schedule, timed=timed, match=self.match))
         out.update(self.match.outputs())
         return out
 
-    def run_ring(self, batches, steps, set0=0, desc_steps=None, schedule=1, timed=False):
+    def run_ring(self, batches, steps, set0=0, desc_steps=None, schedule=7, timed=False):
         """`steps` pipelined steps of extraction + matching over a batch ring
         of packed [2P, ...] batches (SphExtractor.run_ring): step s matches
         the pairs of batches[(set0 + s) % R] into that ring set's corr12 /

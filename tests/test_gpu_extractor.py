@@ -72,10 +72,11 @@ def poison(ex):
         t.view(-1).view(torch.uint8).fill_(0xFF)
 
 
-@pytest.mark.parametrize("schedule", [0, 1, 2, 3, 4, 5])
-def test_extractor_native_runner(dev, schedule):
-    """pcr_extractor_run (the bench's native multi-step enqueue): every
-    step's descriptor and the final outputs equal the single-step results."""
+def test_extractor_native_runner(dev):
+    """pcr_extractor_run schedule 0 over the single buffer set (the native
+    multi-step enqueue): every step's descriptor and the final outputs equal
+    the single-step results; the removed schedules 1-5 are refused."""
+    schedule = 0
     from pcr_amd.extractor import SphExtractor
     b, n, c, k, r = 8, 1024, 64, 32, 32
     xyz, nrm, feat = gaussian_clouds(b, n, seed=3, c=c)
@@ -101,9 +102,12 @@ def test_extractor_native_runner(dev, schedule):
             ms = ex.grid_kernel_times()
             assert len(ms) == (0 if schedule == 0 else steps if timed is True else min(steps, timed))
             assert all(0 < t < 100 for t in ms)
+    for gone in (1, 2, 3, 4, 5, 8):
+        with pytest.raises(RuntimeError):
+            ex.run_native(tx, tn, tf, 2, schedule=gone)
 
 
-@pytest.mark.parametrize("schedule", [1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("schedule", [0, 6, 7])
 def test_extractor_runner_batch_ring(dev, schedule):
     """pcr_extractor_run over a batch ring of 3 distinct batches (each with
     its own output set): one call of 3 steps, then a call of 5 steps that

@@ -57,7 +57,7 @@ def test_pair_step_matches_oracle(dev, p, n, c, k, r):
         assert np.array_equal(N(g), e), name
     # the native runner's per-step matching gives the same, every step
     from test_gpu_extractor import poison
-    for schedule in (0, 1, 2, 3, 4, 5):
+    for schedule in (0,):
         desc_steps = torch.empty((4, 2 * p, c), device=dev)
         poison(pe.ex)
         for t in (pe.match.corr12, pe.match.corr21, pe.match.idx1, pe.match.idx2,
@@ -96,7 +96,7 @@ def _pair_batch(p, n, c, seed):
     return xyz.astype(np.float32), nrm.astype(np.float32), feat
 
 
-@pytest.mark.parametrize("schedule", [1, 6, 7])
+@pytest.mark.parametrize("schedule", [0, 6, 7])
 def test_pair_runner_batch_ring(dev, schedule):
     """BASELINE c4 over distinct pair batches (datasets/deepgmr_mn40.py:71-97,
     a new pair per item): the native runner's batch ring, 4 batches of 2
