@@ -14,10 +14,10 @@ for r in csv.DictReader(open(sys.argv[1])):
     rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short, r["Queue_Id"]))
 rows.sort()
 per_call = int(sys.argv[2]) if len(sys.argv) > 2 else 40
-st = [r for r in rows if r[2] == "vox_stream_kernel"][-per_call:]
+st = [r for r in rows if r[2] in ("vox_stream_kernel", "vox_blocks_kernel")][-per_call:]
 t0, t1 = st[5][0], st[-5][1]
 win = [r for r in rows if r[0] >= t0 and r[1] <= t1]
-nsteps = sum(1 for r in win if r[2] == "vox_stream_kernel")
+nsteps = sum(1 for r in win if r[2] in ("vox_stream_kernel", "vox_blocks_kernel"))
 print("steady steps %d, wall per step %.1f us" % (nsteps, (t1 - t0) / 1e3 / nsteps))
 busy, kb, cnt = defaultdict(float), defaultdict(float), defaultdict(int)
 for s, e, n, q in win:
