@@ -10,6 +10,13 @@
 
 #include "common.hpp"
 
+#ifndef PCR_S6_HEAD
+// the KNN chains of a call's first PCR_S6_HEAD steps wait for step 0's voxel
+// means: 20-step calls 366k -> 375k clouds/s (3 interleaved rounds,
+// profiles/r05_ab_head_wait.log), 200 steps unchanged; A/B builds: 0 = none
+#define PCR_S6_HEAD 2
+#endif
+
 namespace pcr {
 namespace {
 
@@ -340,8 +347,23 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
       if (timed) PCR_HIP(hipEventRecord(rn->t1[s - t_first], vq), "timing record");
       return PCR_OK;
     };
+#if PCR_S6_HEAD
+    // the head of a call: the KNN chains of the first PCR_S6_HEAD steps wait
+    // for step 0's voxel means, so prep + means of step 0 get the chip first
+    // and its grid stream starts sooner (the call's fill)
+    if (s < PCR_S6_HEAD) {
+      if (s == 0) PCR_TRY(vox_part());
+      PCR_HIP(hipStreamWaitEvent(kq, means_done[0], 0), "head wait");
+      PCR_TRY(knn_part());
+      if (s != 0) PCR_TRY(vox_part());
+    } else {
+      PCR_TRY(knn_part());
+      PCR_TRY(vox_part());
+    }
+#else
     PCR_TRY(knn_part());
     PCR_TRY(vox_part());
+#endif
     if (rv && s + a->nsets < steps) {
       PCR_HIP(hipEventRecord(rv[2 * t], vq), "ring record");
       PCR_HIP(hipEventRecord(rv[2 * t + 1], kq), "ring record");
