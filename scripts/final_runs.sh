@@ -1,7 +1,7 @@
 #!/bin/bash
-# round-4 final state: smoke, GPU suite, bench lines (c2 default and driver
-# flags, pairs, c3, c5), rocprofv3 kernel traces + stats of the c2 / c3 / c5
-# bench commands, then the c2 PMC passes
+# a round's final state: smoke, GPU suite, bench lines (c2 default and driver
+# flags, pairs, c3, c5), rocprofv3 kernel traces + stats of the c2 / c3 / c5 /
+# pairs bench commands, then the c2 PMC passes (scripts/pmc_c2.sh)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
@@ -22,5 +22,6 @@ run bench_c5 300 python bench.py --workload c5
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 run prof_c2 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c2 -o run --output-format csv -- python3 bench.py --steps 80 --warmup 40 --no-cpu-baseline --no-verify
 run prof_c3 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c3 -o run --output-format csv -- python3 bench.py --workload c3 --steps 10 --no-cpu-baseline
+run prof_pairs 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_pairs -o run --output-format csv -- python3 bench.py --workload pairs --steps 40 --warmup 20 --no-cpu-baseline --no-verify
 run prof_c5 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c5 -o run --output-format csv -- python3 bench.py --workload c5 --steps 5 --no-cpu-baseline
-bash scripts/r04_pmc.sh
+bash scripts/pmc_c2.sh

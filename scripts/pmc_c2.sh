@@ -1,5 +1,5 @@
 #!/bin/bash
-# round-4 PMC passes over a short c2 bench (one pass per counter group, each
+# PMC passes over a short c2 bench (one pass per counter group, each
 # its own run): FETCH_SIZE, WRITE_SIZE, fabric read / write request counts
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Turn the two rocprofv3 --pmc passes of scripts/gpu_steps.sh (FETCH_SIZE,
+"""Turn the rocprofv3 --pmc passes of scripts/pmc_c2.sh (FETCH_SIZE,
 WRITE_SIZE; separate passes, TCC slots) into profiles/pmc_traffic.json, the
 per-launch HBM bytes of the dominant kernel (bench.py roofline.kernel.traffic)
 and of the whole step, summed over the step's kernels (roofline.traffic).
@@ -22,7 +22,7 @@ KERNEL = os.environ.get("PCR_PMC_KERNEL", "vox_stream_kernel")
 
 
 # the kernels of one bench step (schedule 1): one launch each per step
-STEP_KERNELS = ("knn_sort_kernel", "knn_select_kernel", "local_ppf_cloud_kernel",
+STEP_KERNELS = ("knn_sort_kernel", "knn_wsel_kernel", "local_ppf_quad_kernel",
                 "vox_prep_kernel", "vox_means_kernel", "vox_stream_kernel")
 
 
