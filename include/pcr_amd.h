@@ -309,6 +309,21 @@ pcr_status pcr_extractor_voxel_means_devox(const float *features, int b, int c, 
                                            void *stream);
 pcr_status pcr_extractor_voxel_stream(int b, int c, int n, int r, int *cnt, float *grid,
                                       void *workspace, size_t workspace_bytes, void *stream);
+/* The same back half with the spherical devox moved into the grid stream:
+ * pcr_extractor_voxel_means writes only the compact means rows (no devox,
+ * no descriptor), then pcr_extractor_voxel_stream_devox writes grid + cnt,
+ * devox [b,c,n] (from dwgts and prep's corner segments) and desc [b,c]
+ * (NULL: none) -- the outputs of means_devox + stream, bit for bit, with the
+ * cloud's corner data read once per grid workgroup instead of once per
+ * channel pair.  pcr_extractor_stream_devox_ok(n, c, r) is nonzero where it
+ * applies (n <= 1024, r^3 <= 32768). */
+int pcr_extractor_stream_devox_ok(int n, int c, int r);
+pcr_status pcr_extractor_voxel_means(const float *features, int b, int c, int n, int r,
+                                     void *workspace, size_t workspace_bytes, void *stream);
+pcr_status pcr_extractor_voxel_stream_devox(int b, int c, int n, int r, int *cnt, float *grid,
+                                            float *devox, const float *dwgts, float *desc,
+                                            void *workspace, size_t workspace_bytes,
+                                            void *stream);
 
 /* ------------------------------------------- mutual-NN matching (8f f1) ----
  * datasets/deepgmr_mn40.py:232-244 find_correspondence_one_pair, for p pairs:

@@ -10,6 +10,11 @@
 
 #include "common.hpp"
 
+#ifndef PCR_STREAM_DEVOX
+#define PCR_STREAM_DEVOX 1  // A/B builds: 0 = the means launch keeps the devox
+#endif
+constexpr bool kStreamDevox = PCR_STREAM_DEVOX != 0;
+
 #ifndef PCR_S6_HEAD
 // the KNN chains of a call's first PCR_S6_HEAD steps wait for step 0's voxel
 // means: 20-step calls 366k -> 375k clouds/s (3 interleaved rounds,
@@ -335,16 +340,30 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
       if (s >= 1 && s < nvq) PCR_HIP(hipStreamWaitEvent(vq, means_done[s - 1], 0), "offset wait");
       PCR_TRY(pcr_extractor_voxel_prep(io.xyz, a->b, a->n, a->r, io.norm_coords, io.ind,
                                        io.dinds, io.dwgts, vw6, a->vox_ws_bytes, vq));
-      PCR_TRY(pcr_extractor_voxel_means_devox(io.features, a->b, a->c, a->n, a->r, io.devox,
-                                              io.dinds, io.dwgts, desc, vw6, a->vox_ws_bytes,
-                                              vq));
+      // c2-sized clouds: the devox + descriptor ride in the grid stream (its
+      // means are in LDS there), so the means launch reads no corner data;
+      // the matching reads devox, so it follows the stream then
+      const bool dv = kStreamDevox && pcr_extractor_stream_devox_ok(a->n, a->c, a->r);
+      if (dv)
+        PCR_TRY(pcr_extractor_voxel_means(io.features, a->b, a->c, a->n, a->r, vw6,
+                                          a->vox_ws_bytes, vq));
+      else
+        PCR_TRY(pcr_extractor_voxel_means_devox(io.features, a->b, a->c, a->n, a->r, io.devox,
+                                                io.dinds, io.dwgts, desc, vw6, a->vox_ws_bytes,
+                                                vq));
       if (s < nvq - 1) PCR_HIP(hipEventRecord(means_done[s], vq), "offset record");
-      PCR_TRY(match_pairs(a, io, vq, iv, nvq));
+      if (!dv) PCR_TRY(match_pairs(a, io, vq, iv, nvq));
       const bool timed = s >= t_first && s < t_first + rn->timed_last;
       if (timed) PCR_HIP(hipEventRecord(rn->t0[s - t_first], vq), "timing record");
-      PCR_TRY(pcr_extractor_voxel_stream(a->b, a->c, a->n, a->r, io.cnt, io.grid, vw6,
-                                         a->vox_ws_bytes, vq));
+      if (dv)
+        PCR_TRY(pcr_extractor_voxel_stream_devox(a->b, a->c, a->n, a->r, io.cnt, io.grid,
+                                                 io.devox, io.dwgts, desc, vw6,
+                                                 a->vox_ws_bytes, vq));
+      else
+        PCR_TRY(pcr_extractor_voxel_stream(a->b, a->c, a->n, a->r, io.cnt, io.grid, vw6,
+                                           a->vox_ws_bytes, vq));
       if (timed) PCR_HIP(hipEventRecord(rn->t1[s - t_first], vq), "timing record");
+      if (dv) PCR_TRY(match_pairs(a, io, vq, iv, nvq));
       return PCR_OK;
     };
 #if PCR_S6_HEAD

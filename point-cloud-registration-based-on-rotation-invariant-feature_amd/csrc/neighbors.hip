@@ -582,7 +582,7 @@ template <int M>
 __device__ inline void ppf_local_dev(const float (&c)[M][6], const float (&p)[M][6], int relative,
                                      float (&out)[M][4]) {
   float dx[M], dy[M], dz[M], dn[M];
-  bool safe = true;
+  int safe = 1;  // bitwise ANDs of the range tests: no short-circuit branches
 #pragma unroll
   for (int m = 0; m < M; m++) {
     const float gx = relative ? p[m][0] - c[m][0] : p[m][0];
@@ -596,10 +596,10 @@ __device__ inline void ppf_local_dev(const float (&c)[M][6], const float (&p)[M]
   for (int m = 0; m < M; m++) dn[m] = __builtin_sqrtf(pcr_sumsq3f(dx[m], dy[m], dz[m]));
 #pragma unroll
   for (int m = 0; m < M; m++)
-    safe = safe & ppf_div_safe(dn[m], false) & ppf_div_safe(dx[m], true) &
-           ppf_div_safe(dy[m], true) & ppf_div_safe(dz[m], true);
+    safe &= (int)ppf_div_safe(dn[m], false) & (int)ppf_div_safe(dx[m], true) &
+            (int)ppf_div_safe(dy[m], true) & (int)ppf_div_safe(dz[m], true);
   float ux[M], uy[M], uz[M];
-  if (__builtin_expect(__all(safe), 1)) {
+  if (__builtin_expect(__all(safe != 0), 1)) {
     float y[M];
 #pragma unroll
     for (int m = 0; m < M; m++) y[m] = __builtin_amdgcn_rcpf(dn[m]);

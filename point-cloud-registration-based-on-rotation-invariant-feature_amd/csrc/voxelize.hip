@@ -730,7 +730,7 @@ __global__ __launch_bounds__(NT) void vox_grid_kernel(
 constexpr int kMeansNT = 256;
 constexpr int kMeansPB = 4;  // points per thread: clouds of <= 4 NT points
 constexpr int kMeansMaxN = 2 * kMeansPB * kMeansNT;  // NT = 512 past 4 kMeansNT points (c3)
-template <int G, int NT>
+template <int G, int NT, bool DEVOX = true>
 __global__ __launch_bounds__(NT) void vox_means_kernel(
     const float* __restrict__ feat, int c, int n, VoxWs ws, const float* __restrict__ dwgts,
     float* __restrict__ devox, float* __restrict__ desc, int ngrp) {
@@ -780,8 +780,8 @@ __global__ __launch_bounds__(NT) void vox_means_kernel(
     const int i = e * NT + tid;
 #pragma unroll
     for (int q = 0; q < 8; q++) {
-      dw[e][q] = i < n ? Wt[i + (size_t)q * n] : 0.0f;
-      const int sg = i < n ? Dg[i + (size_t)q * n] : -1;
+      dw[e][q] = (DEVOX && i < n) ? Wt[i + (size_t)q * n] : 0.0f;
+      const int sg = (DEVOX && i < n) ? Dg[i + (size_t)q * n] : -1;
       ds[e][q] = sg >= 0 ? sg : n;  // empty corner -> the zero slot
     }
   }
@@ -827,7 +827,9 @@ __global__ __launch_bounds__(NT) void vox_means_kernel(
   if (tid < gcount) mo[(size_t)tid * ws.ms + n] = 0.0f;  // the empty-cell slot
   lds_barrier();
 
-  // ---- devox of the G channels + descriptor
+  // ---- devox of the G channels + descriptor (DEVOX = false: the grid
+  // stream's DV role does it)
+  if (!DEVOX) return;
   float vmax[G];
 #pragma unroll
   for (int g = 0; g < G; g++) vmax[g] = -__builtin_inff();
@@ -888,11 +890,23 @@ constexpr int kStreamMaxN = 2048;  // two rows of ms <= 2052 floats: 17 pieces p
 constexpr int kStreamMaxW = 1024;  // occupancy words (r^3 <= 32768)
 
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-template <int NS, int NB, int U, int AUX, int G = kStreamG, int NG = kStreamNG>
+// DV (round 5): the streamer waves also evaluate the spherical devox of each
+// item's channels from the means already in LDS (spherical_trilinear_devox.cu
+// :127-134, vox_means_kernel's arithmetic: the same pcr_wsum8 of the same
+// means) and the per-cloud descriptor max, so the means launch no longer
+// reads the cloud's corner data once per channel pair: the corners of a
+// streamer thread's points (n <= 1024: 1024 / NTS points) are loaded once per
+// workgroup into registers.  Measured: the means launch without its devox ran
+// the c2 step 382k -> 418k clouds/s (the same as with no means launch at all).
+constexpr int kStreamDvMaxN = 1024;
+template <int NS, int NB, int U, int AUX, int G = kStreamG, int NG = kStreamNG, bool DV = false>
 __global__ __launch_bounds__((NS + 1) * 64) void vox_stream_kernel(int c, int n, int r3, VoxWs ws,
                                                                   float* __restrict__ out,
                                                                   int* __restrict__ cnt_out,
-                                                                  int ngrp, int wpc, int per) {
+                                                                  int ngrp, int wpc, int per,
+                                                                  const float* __restrict__ dwgts,
+                                                                  float* __restrict__ devox,
+                                                                  float* __restrict__ desc) {
   constexpr int D = NB - 1;     // prefetch distance in items
   constexpr int NTS = NS * 64;  // streamer threads
   constexpr int BUFB = NG * 1024;
@@ -1034,6 +1048,26 @@ __global__ __launch_bounds__((NS + 1) * 64) void vox_stream_kernel(int c, int n,
       }
     }
   };
+  // DV: this thread's points i = tid + e NTS, their 8 corners' segments
+  // (empty corner -> slot n, whose mean is 0) and weights, for every item
+  constexpr int PBS = DV ? kStreamDvMaxN / NTS : 1;
+  int dsg[PBS][8];
+  float dwt[PBS][8];
+  __shared__ float dred_s[2][DV ? NS : 1][G];  // per-wave descriptor partials, by item parity
+  if (DV) {
+    const float* Wt = dwgts + (size_t)b * 8 * n;
+    const int* Dg = ws.dseg + (size_t)b * 8 * n;
+#pragma unroll
+    for (int e = 0; e < PBS; e++) {
+      const int i = e * NTS + tid;
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        dwt[e][q] = i < n ? Wt[i + (size_t)q * n] : 0.0f;
+        const int sg = i < n ? Dg[i + (size_t)q * n] : -1;
+        dsg[e][q] = sg >= 0 ? sg : n;
+      }
+    }
+  }
   lds_only_barrier();
   PCR_STAMP(1);
   // the sweep starts at a workgroup-dependent step of the item and wraps, so
@@ -1051,9 +1085,47 @@ __global__ __launch_bounds__((NS + 1) * 64) void vox_stream_kernel(int c, int n,
       const int sp = st + rot < nstep ? st + rot : st + rot - nstep;
       stream_u(sp * NTS * 4 * U + tid * 4, ob, 0, gcount, ms0, cb);
     }
+    if (DV) {
+      // devox of the item's channels (vox_means_kernel's loop) + descriptor partials
+      float vmax[G];
+#pragma unroll
+      for (int g = 0; g < G; g++) vmax[g] = -__builtin_inff();
+      float* ov = devox + ((size_t)b * c + c0) * n;
+#pragma unroll
+      for (int e = 0; e < PBS; e++) {
+        const int i = e * NTS + tid;
+        if (i < n) {
+#pragma unroll
+          for (int g = 0; g < G; g++) {
+            if (g < gcount) {
+              float fq[8];
+#pragma unroll
+              for (int q = 0; q < 8; q++) fq[q] = ms0[(size_t)g * ms + dsg[e][q]];
+              const float v = pcr_wsum8(dwt[e], fq);
+              ov[(size_t)g * n + i] = v;
+              vmax[g] = fmaxf(vmax[g], v);
+            }
+          }
+        }
+      }
+      if (desc) {
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+          const float m = wave_max(vmax[g]);
+          if (lt == 0) dred_s[it & 1][tid >> 6][g] = m;
+        }
+      }
+    }
     if (it < 4) PCR_STAMP(2 + it);
     lds_only_barrier();
     if (it < 4) PCR_STAMP(8 + it);
+    if (DV && desc && tid < gcount) {
+      // (dred_s[it & 1] is rewritten two items later, after the next barrier)
+      float m = dred_s[it & 1][0][tid];
+#pragma unroll
+      for (int w = 1; w < NS; w++) m = fmaxf(m, dred_s[it & 1][w][tid]);
+      desc[(size_t)b * c + c0 + tid] = m;
+    }
   }
 }
 
@@ -2084,7 +2156,7 @@ extern "C" pcr_status pcr_extractor_voxel_stream(int b, int c, int n, int r, int
     allow_big_lds(vox_stream_kernel<NSV, NBV, UV, AV, GV, NGV>, smem);                        \
     hipLaunchKernelGGL((vox_stream_kernel<NSV, NBV, UV, AV, GV, NGV>), dim3(b * wpc),         \
                        dim3((NSV + 1) * 64), smem, as_stream(stream), c, n, r3, ws, grid, cnt, \
-                       ngrp, wpc, per);                                                       \
+                       ngrp, wpc, per, nullptr, nullptr, nullptr);                            \
   } while (0)
   if (wide) PCR_LAUNCH_STREAM(4, kStreamNB, 2, 16, kStreamG, 17);
   else
@@ -2100,6 +2172,68 @@ extern "C" pcr_status pcr_extractor_voxel_stream(int b, int c, int n, int r, int
 #endif
     PCR_LAUNCH_STREAM(4, kStreamNB, 2, 16, kStreamG, kStreamNG);
 #undef PCR_LAUNCH_STREAM
+  return launch_status(name);
+}
+
+// The voxel stage's back half with the devox inside the grid stream
+// (vox_stream_kernel<..., DV = true>): the means launch writes only the
+// compact means rows (vox_means_kernel<2, 256, false>), then the grid stream
+// writes grid + cnt and, from the same means in LDS, devox [b,c,n] and the
+// descriptor [b,c].  Same outputs, bits and order of operations as
+// pcr_extractor_voxel_means_devox + pcr_extractor_voxel_stream; clouds of at
+// most 1024 points (pcr_extractor_stream_devox_ok).
+extern "C" int pcr_extractor_stream_devox_ok(int n, int c, int r) {
+  const int r3 = r * r * r;
+  return n >= 1 && n <= kStreamDvMaxN && c >= 1 && r3 <= 32 * kStreamMaxW && r3 % 128 == 0 &&
+         ((r3 + 31) / 32) % 64 == 0;
+}
+
+extern "C" pcr_status pcr_extractor_voxel_means(const float* features, int b, int c, int n, int r,
+                                                void* workspace, size_t workspace_bytes,
+                                                void* stream) {
+  const char* name = "extractor_voxel_means";
+  VoxWs ws;
+  pcr_status rc = extractor_ws(b, c, n, r, workspace, workspace_bytes, &ws, name);
+  if (rc != PCR_OK) return rc;
+  PCR_REQUIRE(features != nullptr && n <= kMeansPB * kMeansNT,
+              "%s: features required, n <= %d", name, kMeansPB * kMeansNT);
+  if (b == 0) return PCR_OK;
+  const int ngrp = ceil_div(c, 2);
+  const size_t smem = ((size_t)2 * n + (size_t)2 * (n + 1) + n + (n + 1)) * 4;
+  allow_big_lds(vox_means_kernel<2, kMeansNT, false>, smem);
+  hipLaunchKernelGGL((vox_means_kernel<2, kMeansNT, false>), dim3(ngrp * b), dim3(kMeansNT), smem,
+                     as_stream(stream), features, c, n, ws, nullptr, nullptr, nullptr, ngrp);
+  return launch_status(name);
+}
+
+extern "C" pcr_status pcr_extractor_voxel_stream_devox(int b, int c, int n, int r, int* cnt,
+                                                       float* grid, float* devox,
+                                                       const float* dwgts, float* desc,
+                                                       void* workspace, size_t workspace_bytes,
+                                                       void* stream) {
+  const char* name = "extractor_voxel_stream_devox";
+  VoxWs ws;
+  pcr_status rc = extractor_ws(b, c, n, r, workspace, workspace_bytes, &ws, name);
+  if (rc != PCR_OK) return rc;
+  PCR_REQUIRE(grid != nullptr && devox != nullptr && dwgts != nullptr,
+              "%s: grid, devox and dwgts required", name);
+  PCR_REQUIRE(pcr_extractor_stream_devox_ok(n, c, r), "%s: n=%d c=%d r=%d unsupported", name, n,
+              c, r);
+  if (b == 0) return PCR_OK;
+  const int r3 = r * r * r;
+  constexpr int G = kStreamG, NG = kStreamNG;
+  PCR_REQUIRE(G * ws.ms * 4 <= NG * 1024, "%s: means rows too long", name);
+  const int ngrp = ceil_div(c, G);
+  int wpc = device_cus() / b;
+  if (wpc < 1) wpc = 1;
+  if (wpc > ngrp) wpc = ngrp;
+  const int per = ceil_div(ngrp, wpc);
+  const size_t smem = (size_t)kStreamNB * NG * 1024 + (size_t)ws.W * 6 +
+                      ((size_t)ws.ms * 2 + 255) / 256 * 256;
+  allow_big_lds(vox_stream_kernel<4, kStreamNB, 2, 16, G, NG, true>, smem);
+  hipLaunchKernelGGL((vox_stream_kernel<4, kStreamNB, 2, 16, G, NG, true>), dim3(b * wpc),
+                     dim3(5 * 64), smem, as_stream(stream), c, n, r3, ws, grid, cnt, ngrp, wpc,
+                     per, dwgts, devox, desc);
   return launch_status(name);
 }
 

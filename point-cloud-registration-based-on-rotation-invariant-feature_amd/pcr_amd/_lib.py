@@ -62,6 +62,9 @@ SIGNATURES = {
     "pcr_extractor_voxel_grid_devox": (ST, [P, I, I, I, I, P, P, P, P, P, P, P, SZ, P]),
     "pcr_extractor_voxel_means_devox": (ST, [P, I, I, I, I, P, P, P, P, P, SZ, P]),
     "pcr_extractor_voxel_stream": (ST, [I, I, I, I, P, P, P, SZ, P]),
+    "pcr_extractor_stream_devox_ok": (I, [I, I, I]),
+    "pcr_extractor_voxel_means": (ST, [P, I, I, I, I, P, SZ, P]),
+    "pcr_extractor_voxel_stream_devox": (ST, [I, I, I, I, P, P, P, P, P, P, SZ, P]),
     "pcr_runner_create": (ST, [I, ctypes.POINTER(P)]),
     "pcr_runner_destroy": (None, [P]),
     "pcr_runner_grid_times": (ST, [P, P, I, ctypes.POINTER(I)]),
