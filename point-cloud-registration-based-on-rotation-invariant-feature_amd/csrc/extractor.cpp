@@ -341,9 +341,13 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
       PCR_TRY(pcr_extractor_voxel_prep(io.xyz, a->b, a->n, a->r, io.norm_coords, io.ind,
                                        io.dinds, io.dwgts, vw6, a->vox_ws_bytes, vq));
       // c2-sized clouds: the devox + descriptor ride in the grid stream (its
-      // means are in LDS there), so the means launch reads no corner data;
-      // the matching reads devox, so it follows the stream then
-      const bool dv = kStreamDevox && pcr_extractor_stream_devox_ok(a->n, a->c, a->r);
+      // means are in LDS there), so the means launch reads no corner data
+      // (c2 390k -> 405-408k clouds/s).  With pair matching, which reads the
+      // devox, the means launch keeps it and the matching runs before the
+      // stream (pairs: 274k against 266k with the matching behind the
+      // stream, profiles/r05_ab_stream_devox.log)
+      const bool dv = kStreamDevox && a->match_pairs <= 0 &&
+                      pcr_extractor_stream_devox_ok(a->n, a->c, a->r);
       if (dv)
         PCR_TRY(pcr_extractor_voxel_means(io.features, a->b, a->c, a->n, a->r, vw6,
                                           a->vox_ws_bytes, vq));
