@@ -898,8 +898,13 @@ typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 // streamer thread's points (n <= 1024: 1024 / NTS points) are loaded once per
 // workgroup into registers.  Measured: the means launch without its devox ran
 // the c2 step 382k -> 418k clouds/s (the same as with no means launch at all).
+// clouds of <= 1024 points (c2): at 2048 points (c3) the role's 16 corner
+// registers per point made the kernel 171 VGPRs and the c3 step 1.89 ->
+// 1.95 ms (profiles/r05_ab_stream_devox.log), so c3 keeps the devox in the
+// means launch
 constexpr int kStreamDvMaxN = 1024;
-template <int NS, int NB, int U, int AUX, int G = kStreamG, int NG = kStreamNG, bool DV = false>
+// DVN: 0 = no devox role; else the most points per cloud
+template <int NS, int NB, int U, int AUX, int G = kStreamG, int NG = kStreamNG, int DVN = 0>
 __global__ __launch_bounds__((NS + 1) * 64) void vox_stream_kernel(int c, int n, int r3, VoxWs ws,
                                                                   float* __restrict__ out,
                                                                   int* __restrict__ cnt_out,
@@ -1049,9 +1054,11 @@ __global__ __launch_bounds__((NS + 1) * 64) void vox_stream_kernel(int c, int n,
     }
   };
   // DV: this thread's points i = tid + e NTS, their 8 corners' segments
-  // (empty corner -> slot n, whose mean is 0) and weights, for every item
-  constexpr int PBS = DV ? kStreamDvMaxN / NTS : 1;
-  int dsg[PBS][8];
+  // (empty corner -> slot n, whose mean is 0; two u16 per register) and
+  // weights, for every item
+  constexpr bool DV = DVN > 0;
+  constexpr int PBS = DV ? DVN / NTS : 1;
+  unsigned dsg[PBS][4];
   float dwt[PBS][8];
   __shared__ float dred_s[2][DV ? NS : 1][G];  // per-wave descriptor partials, by item parity
   if (DV) {
@@ -1061,10 +1068,12 @@ __global__ __launch_bounds__((NS + 1) * 64) void vox_stream_kernel(int c, int n,
     for (int e = 0; e < PBS; e++) {
       const int i = e * NTS + tid;
 #pragma unroll
+      for (int q = 0; q < 4; q++) dsg[e][q] = 0u;
+#pragma unroll
       for (int q = 0; q < 8; q++) {
         dwt[e][q] = i < n ? Wt[i + (size_t)q * n] : 0.0f;
         const int sg = i < n ? Dg[i + (size_t)q * n] : -1;
-        dsg[e][q] = sg >= 0 ? sg : n;
+        dsg[e][q >> 1] |= (unsigned)(sg >= 0 ? sg : n) << (16 * (q & 1));
       }
     }
   }
@@ -1100,7 +1109,8 @@ __global__ __launch_bounds__((NS + 1) * 64) void vox_stream_kernel(int c, int n,
             if (g < gcount) {
               float fq[8];
 #pragma unroll
-              for (int q = 0; q < 8; q++) fq[q] = ms0[(size_t)g * ms + dsg[e][q]];
+              for (int q = 0; q < 8; q++)
+                fq[q] = ms0[(size_t)g * ms + ((dsg[e][q >> 1] >> (16 * (q & 1))) & 0xFFFFu)];
               const float v = pcr_wsum8(dwt[e], fq);
               ov[(size_t)g * n + i] = v;
               vmax[g] = fmaxf(vmax[g], v);
@@ -2184,8 +2194,7 @@ extern "C" pcr_status pcr_extractor_voxel_stream(int b, int c, int n, int r, int
 // most 1024 points (pcr_extractor_stream_devox_ok).
 extern "C" int pcr_extractor_stream_devox_ok(int n, int c, int r) {
   const int r3 = r * r * r;
-  return n >= 1 && n <= kStreamDvMaxN && c >= 1 && r3 <= 32 * kStreamMaxW && r3 % 128 == 0 &&
-         ((r3 + 31) / 32) % 64 == 0;
+  return n >= 1 && n <= kStreamDvMaxN && c >= 1 && r3 <= 32 * kStreamMaxW && r3 % 2048 == 0;
 }
 
 extern "C" pcr_status pcr_extractor_voxel_means(const float* features, int b, int c, int n, int r,
@@ -2195,14 +2204,23 @@ extern "C" pcr_status pcr_extractor_voxel_means(const float* features, int b, in
   VoxWs ws;
   pcr_status rc = extractor_ws(b, c, n, r, workspace, workspace_bytes, &ws, name);
   if (rc != PCR_OK) return rc;
-  PCR_REQUIRE(features != nullptr && n <= kMeansPB * kMeansNT,
-              "%s: features required, n <= %d", name, kMeansPB * kMeansNT);
+  PCR_REQUIRE(features != nullptr && n <= kMeansMaxN, "%s: features required, n <= %d", name,
+              kMeansMaxN);
   if (b == 0) return PCR_OK;
   const int ngrp = ceil_div(c, 2);
   const size_t smem = ((size_t)2 * n + (size_t)2 * (n + 1) + n + (n + 1)) * 4;
-  allow_big_lds(vox_means_kernel<2, kMeansNT, false>, smem);
-  hipLaunchKernelGGL((vox_means_kernel<2, kMeansNT, false>), dim3(ngrp * b), dim3(kMeansNT), smem,
-                     as_stream(stream), features, c, n, ws, nullptr, nullptr, nullptr, ngrp);
+  // clouds of more than 1024 points: 512 threads, the same four points per thread
+  if (n > kMeansPB * kMeansNT) {
+    allow_big_lds(vox_means_kernel<2, 2 * kMeansNT, false>, smem);
+    hipLaunchKernelGGL((vox_means_kernel<2, 2 * kMeansNT, false>), dim3(ngrp * b),
+                       dim3(2 * kMeansNT), smem, as_stream(stream), features, c, n, ws, nullptr,
+                       nullptr, nullptr, ngrp);
+  } else {
+    allow_big_lds(vox_means_kernel<2, kMeansNT, false>, smem);
+    hipLaunchKernelGGL((vox_means_kernel<2, kMeansNT, false>), dim3(ngrp * b), dim3(kMeansNT),
+                       smem, as_stream(stream), features, c, n, ws, nullptr, nullptr, nullptr,
+                       ngrp);
+  }
   return launch_status(name);
 }
 
@@ -2221,19 +2239,20 @@ extern "C" pcr_status pcr_extractor_voxel_stream_devox(int b, int c, int n, int 
               c, r);
   if (b == 0) return PCR_OK;
   const int r3 = r * r * r;
-  constexpr int G = kStreamG, NG = kStreamNG;
-  PCR_REQUIRE(G * ws.ms * 4 <= NG * 1024, "%s: means rows too long", name);
+  constexpr int G = kStreamG;
+  const int NGP = kStreamNG;
+  PCR_REQUIRE(G * ws.ms * 4 <= NGP * 1024, "%s: means rows too long", name);
   const int ngrp = ceil_div(c, G);
   int wpc = device_cus() / b;
   if (wpc < 1) wpc = 1;
   if (wpc > ngrp) wpc = ngrp;
   const int per = ceil_div(ngrp, wpc);
-  const size_t smem = (size_t)kStreamNB * NG * 1024 + (size_t)ws.W * 6 +
+  const size_t smem = (size_t)kStreamNB * NGP * 1024 + (size_t)ws.W * 6 +
                       ((size_t)ws.ms * 2 + 255) / 256 * 256;
-  allow_big_lds(vox_stream_kernel<4, kStreamNB, 2, 16, G, NG, true>, smem);
-  hipLaunchKernelGGL((vox_stream_kernel<4, kStreamNB, 2, 16, G, NG, true>), dim3(b * wpc),
-                     dim3(5 * 64), smem, as_stream(stream), c, n, r3, ws, grid, cnt, ngrp, wpc,
-                     per, dwgts, devox, desc);
+  allow_big_lds(vox_stream_kernel<4, kStreamNB, 2, 16, G, kStreamNG, kStreamDvMaxN>, smem);
+  hipLaunchKernelGGL((vox_stream_kernel<4, kStreamNB, 2, 16, G, kStreamNG, kStreamDvMaxN>),
+                     dim3(b * wpc), dim3(5 * 64), smem, as_stream(stream), c, n, r3, ws, grid, cnt,
+                     ngrp, wpc, per, dwgts, devox, desc);
   return launch_status(name);
 }
 

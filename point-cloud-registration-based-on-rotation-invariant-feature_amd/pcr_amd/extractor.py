@@ -32,7 +32,10 @@ from .ops import _ptr
 
 class SphExtractor:
     def __init__(self, batch, npoints, channels, k, resolution, device="cuda", relative=True,
-                 with_dist=False, split_ppf=True):
+                 with_dist=False, split_ppf=True, stream_devox=True):
+        # stream_devox: the split voxel stage evaluates the devox inside the
+        # grid stream (False: in the means launch; an A/B switch)
+        self.stream_devox = stream_devox
         self.b, self.n, self.c, self.k, self.r = batch, npoints, channels, k, resolution
         self.relative = relative
         self.split_ppf = split_ppf
@@ -219,6 +222,24 @@ class SphExtractor:
             _ptr(features), self.b, self.c, self.n, self.r, _ptr(self.devox), _ptr(dinds),
             _ptr(dwgts), _ptr(d), _ptr(ws), ws.numel(), stream), "extractor_voxel_means_devox")
 
+    def voxel_means(self, features, stream, slot=0):
+        """Voxel means of the occupied segments into the workspace only (the
+        devox + descriptor then ride in voxel_stream_devox)."""
+        ws = self._set(slot)[1]
+        _lib.check(_lib.load().pcr_extractor_voxel_means(
+            _ptr(features), self.b, self.c, self.n, self.r, _ptr(ws), ws.numel(), stream),
+            "extractor_voxel_means")
+
+    def voxel_stream_devox(self, stream, desc=None, slot=0):
+        """The dense grid + cnt, devox and descriptor from the workspace means
+        (pcr_extractor_voxel_stream_devox: each grid workgroup reads the
+        cloud's corner data once)."""
+        _, ws, _, dwgts, _ = self._set(slot)
+        d = self.desc if desc is None else desc
+        _lib.check(_lib.load().pcr_extractor_voxel_stream_devox(
+            self.b, self.c, self.n, self.r, _ptr(self.cnt), _ptr(self.grid), _ptr(self.devox),
+            _ptr(dwgts), _ptr(d), _ptr(ws), ws.numel(), stream), "extractor_voxel_stream_devox")
+
     def voxel_stream(self, stream, slot=0):
         """The dense grid + cnt from the workspace means (the dominant,
         HBM-bound kernel of the split voxel stage)."""
@@ -337,8 +358,14 @@ class SphExtractor:
         self.voxel_prep(xyz, stream, slot)
         r3 = self.r ** 3
         if self.n <= 2048 and r3 % 2048 == 0 and r3 <= 32768:
-            self.voxel_means_devox(features, stream, desc, slot)
-            self.voxel_stream(stream, slot)
+            if self.stream_devox and _lib.load().pcr_extractor_stream_devox_ok(self.n, self.c,
+                                                                               self.r):
+                # the devox + descriptor inside the grid stream
+                self.voxel_means(features, stream, slot)
+                self.voxel_stream_devox(stream, desc, slot)
+            else:
+                self.voxel_means_devox(features, stream, desc, slot)
+                self.voxel_stream(stream, slot)
             return
         self.voxel_grid(features, stream, slot)
         if self.n <= 4096:
