@@ -111,6 +111,91 @@ __device__ inline void match_load_stage_cm(const float* __restrict__ A,
   }
 }
 
+// pcr_match_key's high word without branches: the float bits of d + 0 (-0 ->
+// +0) mapped to an ascending unsigned order, NaN -> 0 (first)
+__device__ inline unsigned match_key_hi(float d) {
+  const unsigned u = __float_as_uint(d + 0.0f);
+  const unsigned k = u ^ ((unsigned)((int)u >> 31) | 0x80000000u);
+  return d != d ? 0u : k;
+}
+
+// The tile epilogue: per element the diff (pcr_match_diff) and its key's
+// high word (elements outside the matrices: ~0), then
+//  - the row minimum over this lane's two columns by one 32-bit compare (the
+//    columns are ascending, so a tie keeps the first), as a 64-bit key, then
+//    the transpose-reduction over the 32 lanes of a half (as below);
+//  - the column minimum over this lane's 32 rows, visited in ascending row
+//    order, by a strict 32-bit compare (the first row wins a tie);
+// the same (diff, index) minima as pcr_match_key's 64-bit ordering, with no
+// branches and no global loads (the norms are in LDS).  It replaced a
+// per-element 64-bit key loop with bounds branches and the norms loaded from
+// global memory inside it (c4 match call 0.346 -> see DESIGN.md 4.8).
+__device__ inline void match_epilogue(const f32x16 (&acc)[2][2], const float (&sq_s)[2][kMT],
+                                      int i0, int j0, int wi, int wj, int lane, int n1, int n2,
+                                      unsigned long long* __restrict__ rb,
+                                      unsigned long long* __restrict__ cb) {
+  float sc[2];
+#pragma unroll
+  for (int tj = 0; tj < 2; tj++) sc[tj] = sq_s[1][wj * 64 + tj * 32 + (lane & 31)];
+  unsigned cu[2] = {~0u, ~0u};
+  int crow[2] = {0, 0};
+  // one 32-row half (ti) at a time: 16 keys per lane, a transpose-reduction
+  // over lane bits 0-3 (15 shuffles: each step swaps half of the remaining
+  // rows with the partner), then lanes l and l ^ 16 (the other 16 columns)
+  // combine; 32 registers of keys instead of 64
+#pragma unroll
+  for (int ti = 0; ti < 2; ti++) {
+    unsigned long long R[16];
+#pragma unroll
+    for (int v = 0; v < 16; v++) {
+      const int rl = wi * 64 + ti * 32 + (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5);
+      const float sr = sq_s[0][rl];
+      const int c0 = j0 + wj * 64 + (lane & 31);
+      const bool rok = i0 + rl < n1;
+      unsigned u[2];
+#pragma unroll
+      for (int tj = 0; tj < 2; tj++) {
+        // an element outside the matrices keys as ~0: above every real key
+        // (+inf maps to 0xFF800000), so it never wins
+        const bool ok = rok && c0 + 32 * tj < n2;
+        u[tj] = ok ? match_key_hi(pcr_match_diff(sr, sc[tj], acc[ti][tj][v])) : ~0u;
+        const bool lt = u[tj] < cu[tj];
+        cu[tj] = lt ? u[tj] : cu[tj];
+        crow[tj] = lt ? i0 + rl : crow[tj];
+      }
+      const bool second = u[1] < u[0];
+      const unsigned um = second ? u[1] : u[0];
+      R[v] = um == ~0u ? ~0ull
+                       : ((unsigned long long)um << 32) | (unsigned)(second ? c0 + 32 : c0);
+    }
+#pragma unroll
+    for (int h = 8; h >= 1; h >>= 1) {
+      const bool up = (lane & h) != 0;
+#pragma unroll
+      for (int i = 0; i < h; i++) {
+        const unsigned long long send = up ? R[i] : R[i + h];
+        const unsigned long long keep = up ? R[i + h] : R[i];
+        const unsigned long long recv = shfl_xor_u64(send, h);
+        R[i] = recv < keep ? recv : keep;
+      }
+    }
+    const unsigned long long o = shfl_xor_u64(R[0], 16);
+    const unsigned long long rmin = o < R[0] ? o : R[0];
+    const int v = lane & 15;
+    const int row = i0 + wi * 64 + ti * 32 + (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5);
+    if ((lane & 16) == 0 && row < n1) atomicMin(rb + row, rmin);
+  }
+#pragma unroll
+  for (int tj = 0; tj < 2; tj++) {
+    const unsigned long long m0 =
+        cu[tj] == ~0u ? ~0ull : ((unsigned long long)cu[tj] << 32) | (unsigned)crow[tj];
+    const unsigned long long o = shfl_xor_u64(m0, 32);
+    const unsigned long long m = o < m0 ? o : m0;
+    const int col = j0 + wj * 64 + tj * 32 + lane;
+    if (lane < 32 && col < n2) atomicMin(cb + col, m);
+  }
+}
+
 // Channels run through LDS in stages of 32, double-buffered: the next
 // stage's global loads are in flight while the MFMAs consume this one, and
 // one barrier per stage suffices (a buffer is rewritten two stages later,
@@ -122,10 +207,20 @@ __global__ __launch_bounds__(256) void match_tile_kernel(
     unsigned long long* __restrict__ rowbest, unsigned long long* __restrict__ colbest) {
   __shared__ float a_s[2][kKC][kMPad];  // [buf][k][i]
   __shared__ float b_s[2][kKC][kMPad];  // [buf][k][j]
+  __shared__ float sq_s[2][kMT];        // the tile's row / column norms
   const int p = blockIdx.z;
   const int i0 = blockIdx.y * kMT, j0 = blockIdx.x * kMT;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wi = wv >> 1, wj = wv & 1;  // 2 x 2 waves, 64 x 64 each
+  // the norms the epilogue reads, staged with the first stage (they used to
+  // be 34 dependent global loads per lane inside the epilogue)
+  if (tid < kMT) {
+    const int row = i0 + tid;
+    sq_s[0][tid] = row < n1 ? sq1[(size_t)p * n1 + row] : 0.0f;
+  } else {
+    const int col = j0 + tid - kMT;
+    sq_s[1][tid - kMT] = col < n2 ? sq2[(size_t)p * n2 + col] : 0.0f;
+  }
   const float* A = f1 + (size_t)p * n1 * c;
   const float* B = f2 + (size_t)p * n2 * c;
   f32x16 acc[2][2];
@@ -172,60 +267,8 @@ __global__ __launch_bounds__(256) void match_tile_kernel(
     }
   }
   // epilogue: C/D layout col = lane & 31, row = (v & 3) + 8 (v >> 2) + 4 (lane >> 5)
-  unsigned long long* rb = rowbest + (size_t)p * n1;
-  unsigned long long* cb = colbest + (size_t)p * n2;
-  const float* s1 = sq1 + (size_t)p * n1;
-  const float* s2 = sq2 + (size_t)p * n2;
-  unsigned long long cmin[2] = {~0ull, ~0ull};
-  // row minima: R[16 ti + v] = min over this lane's two columns, then a
-  // transpose-reduction over the 32 lanes of each half (xor 16, 8, 4, 2, 1:
-  // each step swaps half of the remaining rows with the partner), 31 64-bit
-  // shuffles instead of 5 per row; lane l ends with row s = l & 31
-  unsigned long long R[32];
-#pragma unroll
-  for (int ti = 0; ti < 2; ti++) {
-#pragma unroll
-    for (int v = 0; v < 16; v++) {
-      const int row = i0 + wi * 64 + ti * 32 + (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5);
-      const float sr = row < n1 ? s1[row] : 0.0f;
-      unsigned long long rmin = ~0ull;
-#pragma unroll
-      for (int tj = 0; tj < 2; tj++) {
-        const int col = j0 + wj * 64 + tj * 32 + (lane & 31);
-        if (row < n1 && col < n2) {
-          const float d = pcr_match_diff(sr, s2[col], acc[ti][tj][v]);
-          const unsigned long long kr = pcr_match_key(d, col);
-          const unsigned long long kc = pcr_match_key(d, row);
-          rmin = kr < rmin ? kr : rmin;
-          cmin[tj] = kc < cmin[tj] ? kc : cmin[tj];
-        }
-      }
-      R[ti * 16 + v] = rmin;
-    }
-  }
-#pragma unroll
-  for (int h = 16; h >= 1; h >>= 1) {
-    const bool up = (lane & h) != 0;
-#pragma unroll
-    for (int i = 0; i < h; i++) {
-      const unsigned long long send = up ? R[i] : R[i + h];
-      const unsigned long long keep = up ? R[i + h] : R[i];
-      const unsigned long long recv = shfl_xor_u64(send, h);
-      R[i] = recv < keep ? recv : keep;
-    }
-  }
-  {
-    const int sidx = lane & 31, ti = sidx >> 4, v = sidx & 15;
-    const int row = i0 + wi * 64 + ti * 32 + (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5);
-    if (row < n1) atomicMin(rb + row, R[0]);
-  }
-#pragma unroll
-  for (int tj = 0; tj < 2; tj++) {
-    const unsigned long long o = shfl_xor_u64(cmin[tj], 32);
-    const unsigned long long m = o < cmin[tj] ? o : cmin[tj];
-    const int col = j0 + wj * 64 + tj * 32 + lane;
-    if (lane < 32 && col < n2) atomicMin(cb + col, m);
-  }
+  match_epilogue(acc, sq_s, i0, j0, wi, wj, lane, n1, n2, rowbest + (size_t)p * n1,
+                 colbest + (size_t)p * n2);
 }
 
 // corr12 / corr21 from the minima; mutual pairs compacted in ascending i
