@@ -2064,9 +2064,11 @@ __global__ __launch_bounds__(kWselWaves * 64) void knn_wsel_kernel(KnnSet s, int
       int nb;
       if (pass < 3) {
         // count ~ t^1.5 near the k-th distance (smooth clouds: ~1.6 passes)
+        // (raw v_log / v_exp: any estimate is correct here, the bracket
+        // below keeps it inside (lo, hi); the library forms add range fixups)
         const float f = __uint_as_float((unsigned)tb) *
-                        __builtin_exp2f(0.6666667f * __builtin_log2f(
-                                                         tgt * __builtin_amdgcn_rcpf((float)max(cnt, 1))));
+                        __builtin_amdgcn_exp2f(0.6666667f * __builtin_amdgcn_logf(
+                                                                tgt * __builtin_amdgcn_rcpf((float)max(cnt, 1))));
         nb = f < 1e30f ? (int)__float_as_uint(f) : kWselTmax;
       } else {
         // steep counts (an outlier facing the bulk): bisect the bracket's bits
