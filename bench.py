@@ -330,7 +330,13 @@ class ExtractWorkload:
             # matching: both clouds' [C, N] features read, corr12 / corr21 /
             # idx1 / idx2 written (4 x 4N), per pair
             self.step_bytes += (2 * 4 * c * n + 16 * n) * (b // 2)
-        self.kernel_bytes = stream_kernel_bytes_per_cloud(r, c) * b
+        # the c2 extractor's grid stream also writes devox + descriptor
+        # (pcr_extractor_voxel_stream_devox; pairs keep them in the means)
+        from pcr_amd import _lib
+        self.stream_devox = args.workload == "extract" and bool(
+            _lib.load().pcr_extractor_stream_devox_ok(n, c, r))
+        self.kernel_bytes = stream_kernel_bytes_per_cloud(
+            r, c, n if self.stream_devox else None) * b
         # grid launches bracketed with timing events in the timed call (each
         # event record on the grid queue costs ~3.5 us: 10 of 20 steps timed
         # made the driver's 20-step line 3.5% slower than untimed)
@@ -431,7 +437,9 @@ class ExtractWorkload:
             except (OSError, ValueError):
                 pass
         return step_traffic, {
-            "name": "vox_stream_kernel (sph-vox dense grid + cnt from the voxel means)",
+            "name": ("vox_stream_kernel (sph-vox dense grid + cnt from the voxel means, and "
+                     "the sph devox + descriptor of the same means)" if self.stream_devox else
+                     "vox_stream_kernel (sph-vox dense grid + cnt from the voxel means)"),
             "bound": "hbm", "avg_ms_in_step": round(avg, 5), "launches_timed": len(ms),
             "bytes_per_launch": self.kernel_bytes, "achieved": round(gbs, 1),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),

@@ -687,14 +687,19 @@ def grid_kernel_bytes_per_cloud(n, r, c):
     return 4 * c * n + 4 * c * r3 + 4 * r3
 
 
-def stream_kernel_bytes_per_cloud(r, c):
+def stream_kernel_bytes_per_cloud(r, c, n=None):
     """Algorithmic HBM bytes of the split voxel stage's dominant kernel
     (vox_stream_kernel: the spherical_avg_voxelize outputs)
-    per cloud: grid written 4C r^3, cnt written 4 r^3.  Its reads of the
-    compact voxel means (4C per occupied voxel) and of the occupancy bitmap
-    are artefacts of this design and not counted."""
+    per cloud: grid written 4C r^3, cnt written 4 r^3; with n (the kernel's
+    devox role, clouds of <= 1024 points) also the spherical devox of 8d:
+    devox written 4CN, the corner data read 64N, the descriptor written 4C.
+    Its reads of the compact voxel means (4C per occupied voxel) and of the
+    occupancy bitmap are artefacts of this design and not counted."""
     r3 = r ** 3
-    return 4 * c * r3 + 4 * r3
+    b = 4 * c * r3 + 4 * r3
+    if n is not None:
+        b += 4 * c * n + 64 * n + 4 * c
+    return b
 
 
 def fused_grid_kernel_bytes_per_cloud(n, r, c):
