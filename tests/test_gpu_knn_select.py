@@ -133,6 +133,26 @@ def test_select_nan_points(dev):
     check_self(dev, xyz, 32)
 
 
+@pytest.mark.parametrize("n", [1536, 2048])
+def test_select_sorted_2k_edge_cases(dev, n):
+    """The extractor's selection at c3 sizes (1024 < n <= 2048) on the inputs
+    that exercise its bound growth, tie and fallback paths: a lattice (equal
+    distances), 300 copies of one point, far points past 10000, NaN points,
+    an outlier facing the cloud; k = 32, 16, 1."""
+    xyz = np.concatenate([edge_clouds_for_knn(1, n, seed=11),
+                          gaussian_clouds(3, n, seed=n + 3)[0]]).astype(np.float32)
+    xyz[1, :, 100:400] = xyz[1, :, 100:101]
+    xyz[2, :, n - 40:] += np.float32(500.0)
+    xyz[2, :, 3] = np.nan
+    xyz[3, 1, 900] = np.nan
+    xyz[3, :, 5] = (30.0, 0.0, 0.0)
+    xyz = np.ascontiguousarray(xyz)
+    nrm = np.ascontiguousarray(np.roll(xyz, 1, axis=1))
+    for k in (32, 16, 1):
+        _, ei = oracle.knn_dir(xyz, xyz, k)
+        check_sorted(dev, xyz, nrm, k, ei)
+
+
 def test_select_two_sets(dev):
     """Non-self query/candidate sets of different sizes, both directions."""
     from pcr_amd import ops
