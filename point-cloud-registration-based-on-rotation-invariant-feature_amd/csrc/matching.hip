@@ -200,8 +200,11 @@ __device__ inline void match_epilogue(const f32x16 (&acc)[2][2], const float (&s
 // stage's global loads are in flight while the MFMAs consume this one, and
 // one barrier per stage suffices (a buffer is rewritten two stages later,
 // after every wave passed the barrier in between).
+#ifndef PCR_MATCH_WPE
+#define PCR_MATCH_WPE 3
+#endif
 template <bool CM>
-__global__ __launch_bounds__(256) void match_tile_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PCR_MATCH_WPE))) void match_tile_kernel(
     const float* __restrict__ f1, const float* __restrict__ f2, int n1, int n2, int c,
     const float* __restrict__ sq1, const float* __restrict__ sq2,
     unsigned long long* __restrict__ rowbest, unsigned long long* __restrict__ colbest) {
