@@ -15,11 +15,6 @@
 #endif
 constexpr bool kStreamDevox = PCR_STREAM_DEVOX != 0;
 
-#ifndef PCR_S6_PACE
-// schedules 6 / 7: the KNN chain of step s >= PCR_S6_HEAD waits for the
-// voxel means of step s - PCR_S6_PACE (0: no pacing)
-#define PCR_S6_PACE 0
-#endif
 #ifndef PCR_S6_HEAD
 // the KNN chains of a call's first PCR_S6_HEAD steps wait for step 0's voxel
 // means: 20-step calls 366k -> 375k clouds/s (3 interleaved rounds,
@@ -34,7 +29,7 @@ namespace {
 // every pcr_extractor_run call.  A wait captures the event's most recent
 // record at the time it is enqueued, so re-recording across steps and calls
 // keeps the same ordering as fresh events.
-constexpr int kSyncEvents = 12;  // fork, means_done[2], -, -, join[3], pace[4]
+constexpr int kSyncEvents = 8;
 }  // namespace
 }  // namespace pcr
 
@@ -288,7 +283,6 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
   const int t_first = (steps - rn->timed_last) / 2;
   hipEvent_t* e = rn->sync;
   hipEvent_t fork = e[0], means_done[2] = {e[1], e[2]}, join[3] = {e[5], e[6], e[7]};
-  hipEvent_t* const pace = e + 8;  // [4], ring of the voxel means of the last steps
   // schedules 6 / 7 over a ring that one call wraps onto other queues
   // (nsets not a multiple of the queue count): per-set events, made once
   // per ring size (the first call, outside any timed region)
@@ -362,8 +356,6 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
                                                 io.dinds, io.dwgts, desc, vw6, a->vox_ws_bytes,
                                                 vq));
       if (s < nvq - 1) PCR_HIP(hipEventRecord(means_done[s], vq), "offset record");
-      if (PCR_S6_PACE > 0 && s + PCR_S6_PACE < steps)
-        PCR_HIP(hipEventRecord(pace[s & 3], vq), "pace record");
       if (!dv) PCR_TRY(match_pairs(a, io, vq, iv, nvq));
       const bool timed = s >= t_first && s < t_first + rn->timed_last;
       if (timed) PCR_HIP(hipEventRecord(rn->t0[s - t_first], vq), "timing record");
@@ -388,10 +380,6 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
       PCR_TRY(knn_part());
       if (s != 0) PCR_TRY(vox_part());
     } else {
-      // pacing: the KNN chains run at most PCR_S6_PACE steps ahead of the
-      // voxel chains, so the call does not end on voxel work alone
-      if (PCR_S6_PACE > 0 && s >= PCR_S6_PACE)
-        PCR_HIP(hipStreamWaitEvent(kq, pace[(s - PCR_S6_PACE) & 3], 0), "pace wait");
       PCR_TRY(knn_part());
       PCR_TRY(vox_part());
     }
