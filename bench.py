@@ -88,11 +88,14 @@ def parse(argv=None):
                     help="diagnostic: no timing events around the dominant kernel")
     ap.add_argument("--no-verify", action="store_true",
                     help="diagnostic: skip the output check before the warm-up")
-    ap.add_argument("--c3-schedule", choices=("pipelined", "serial"), default="pipelined",
-                    help="c3: pipelined = each batch's KNN + local PPF on a side stream one "
-                         "batch ahead, overlapping the previous step's backwards "
-                         "(SphExtractor.pipelined_steps); serial = forward (joined), then "
-                         "the backwards")
+    ap.add_argument("--c3-schedule", choices=("pipelined", "pipelined-nbr", "serial"),
+                    default="pipelined",
+                    help="c3: pipelined = each batch's KNN + local PPF and its voxel head "
+                         "(prep + means + devox) on side streams one batch ahead, overlapping "
+                         "the previous step's grid stream and backwards "
+                         "(SphExtractor.pipelined_steps(voxel_ahead=True)); pipelined-nbr = "
+                         "only the KNN + PPF ahead (round 5's schedule); serial = forward "
+                         "(joined), then the backwards")
     ap.add_argument("--cu-split", type=float, default=0.0,
                     help="extract diagnostic: the KNN queues on this fraction of the CUs, the "
                          "voxel queues (s_vox and the caller's stream) on the rest (CU-masked "
@@ -526,9 +529,12 @@ class C3Workload:
             if keep is not None:
                 keep.append(({kk: v.clone() for kk, v in out.items()}, res))
         # prefetch: batch(s + 1) before step s's voxel side and consume; the
-        # bench's batch tensors are read-only, so that is allowed
+        # bench's batch tensors are read-only, so that is allowed.  The voxel
+        # head (prep + means + devox) of batch s + 1 runs ahead on a side
+        # stream too, unless --c3-schedule pipelined-nbr
         self.ex.pipelined_steps(steps, lambda s: self.inputs, consume,
-                                select_events=self.sev if timed else None, prefetch=True)
+                                select_events=self.sev if timed else None, prefetch=True,
+                                voxel_ahead=self.args.c3_schedule == "pipelined")
 
     def verify(self):
         """Three pipelined steps vs the serial forward + backwards: every

@@ -68,6 +68,7 @@ class SphExtractor:
         self._runner, self._runner_cap = None, 0
         self._static_in = None
         self._set1 = None
+        self._vsep, self._vset1 = False, None
         self._ppf1 = None
         self._args, self._args_key = None, None
 
@@ -103,6 +104,18 @@ class SphExtractor:
             self._ppf1 = torch.empty_like(self.local_ppf)
             self._order_new_buffers()
         return self._ppf1
+
+    def _vset(self, slot):
+        """The voxel outputs of slot `slot`: (norm_coords, ind, devox, desc).
+        One set unless a pipeline runs the next batch's voxel head ahead
+        (pipelined_steps(voxel_ahead=True)): then slot 1 has its own."""
+        if slot == 0 or not self._vsep:
+            return self.norm_coords, self.ind, self.devox, self.desc
+        if self._vset1 is None:
+            e = torch.empty_like
+            self._vset1 = (e(self.norm_coords), e(self.ind), e(self.devox), e(self.desc))
+            self._order_new_buffers()
+        return self._vset1
 
     def neighbor_stage(self, xyz, normals, stream):
         """Sort + select + PPF in one call (the eager, unsplit path)."""
@@ -192,8 +205,9 @@ class SphExtractor:
 
     def voxel_prep(self, xyz, stream, slot=0):
         _, ws, dinds, dwgts, _ = self._set(slot)
+        nc, ind, _, _ = self._vset(slot)
         _lib.check(_lib.load().pcr_extractor_voxel_prep(
-            _ptr(xyz), self.b, self.n, self.r, _ptr(self.norm_coords), _ptr(self.ind),
+            _ptr(xyz), self.b, self.n, self.r, _ptr(nc), _ptr(ind),
             _ptr(dinds), _ptr(dwgts), _ptr(ws), ws.numel(), stream), "extractor_voxel_prep")
 
     def voxel_grid(self, features, stream, slot=0):
@@ -217,9 +231,10 @@ class SphExtractor:
         """Voxel means of the occupied segments into the workspace + devox +
         descriptor (the first half of the split voxel stage)."""
         _, ws, dinds, dwgts, _ = self._set(slot)
-        d = self.desc if desc is None else desc
+        _, _, devox, vdesc = self._vset(slot)
+        d = vdesc if desc is None else desc
         _lib.check(_lib.load().pcr_extractor_voxel_means_devox(
-            _ptr(features), self.b, self.c, self.n, self.r, _ptr(self.devox), _ptr(dinds),
+            _ptr(features), self.b, self.c, self.n, self.r, _ptr(devox), _ptr(dinds),
             _ptr(dwgts), _ptr(d), _ptr(ws), ws.numel(), stream), "extractor_voxel_means_devox")
 
     def voxel_means(self, features, stream, slot=0):
@@ -235,9 +250,10 @@ class SphExtractor:
         (pcr_extractor_voxel_stream_devox: each grid workgroup reads the
         cloud's corner data once)."""
         _, ws, _, dwgts, _ = self._set(slot)
-        d = self.desc if desc is None else desc
+        _, _, devox, vdesc = self._vset(slot)
+        d = vdesc if desc is None else desc
         _lib.check(_lib.load().pcr_extractor_voxel_stream_devox(
-            self.b, self.c, self.n, self.r, _ptr(self.cnt), _ptr(self.grid), _ptr(self.devox),
+            self.b, self.c, self.n, self.r, _ptr(self.cnt), _ptr(self.grid), _ptr(devox),
             _ptr(dwgts), _ptr(d), _ptr(ws), ws.numel(), stream), "extractor_voxel_stream_devox")
 
     def voxel_stream(self, stream, slot=0):
@@ -252,16 +268,18 @@ class SphExtractor:
         """Devox + descriptor from the dense grid (after voxel_grid on the
         same stream): the 80 corner voxels per channel staged in LDS."""
         _, _, dinds, dwgts, _ = self._set(slot)
-        d = self.desc if desc is None else desc
+        _, _, devox, vdesc = self._vset(slot)
+        d = vdesc if desc is None else desc
         _lib.check(_lib.load().pcr_extractor_grid_devox(
             _ptr(self.grid), _ptr(dinds), _ptr(dwgts), self.b, self.c, self.n, self.r,
-            _ptr(self.devox), _ptr(d), stream), "extractor_grid_devox")
+            _ptr(devox), _ptr(d), stream), "extractor_grid_devox")
 
     def voxel_devox(self, features, stream, desc=None, slot=0):
         _, ws, dinds, dwgts, _ = self._set(slot)
-        d = self.desc if desc is None else desc
+        _, _, devox, vdesc = self._vset(slot)
+        d = vdesc if desc is None else desc
         _lib.check(_lib.load().pcr_extractor_voxel_devox(
-            _ptr(features), self.b, self.c, self.n, self.r, _ptr(self.devox), _ptr(dinds),
+            _ptr(features), self.b, self.c, self.n, self.r, _ptr(devox), _ptr(dinds),
             _ptr(dwgts), _ptr(d), _ptr(ws), ws.numel(), stream), "extractor_voxel_devox")
 
     def _check_inputs(self, xyz, normals, features):
@@ -355,25 +373,48 @@ class SphExtractor:
         use the split stage: voxel means + devox + descriptor in one launch,
         then the dense grid streamed from the compact means (c3: 0.60 +
         0.16 ms -> see DESIGN.md 4)."""
-        self.voxel_prep(xyz, stream, slot)
-        r3 = self.r ** 3
-        if self.n <= 2048 and r3 % 2048 == 0 and r3 <= 32768:
-            if self.stream_devox and _lib.load().pcr_extractor_stream_devox_ok(self.n, self.c,
-                                                                               self.r):
-                # the devox + descriptor inside the grid stream (DESIGN.md 4.5)
-                self.voxel_means(features, stream, slot)
-                self.voxel_stream_devox(stream, desc, slot)
-            else:
-                self.voxel_means_devox(features, stream, desc, slot)
-                self.voxel_stream(stream, slot)
+        if self._split_voxels():
+            self.voxel_head(xyz, features, stream, slot, desc)
+            self.voxel_tail(stream, slot, desc)
             return
+        self.voxel_prep(xyz, stream, slot)
         self.voxel_grid(features, stream, slot)
         if self.n <= 4096:
             self.grid_devox(stream, desc, slot)
         else:
             self.voxel_devox(features, stream, desc, slot)
 
-    def pipelined_steps(self, steps, batch, consume, select_events=None, prefetch=False):
+    def _split_voxels(self):
+        """Clouds of <= 2048 points on grids the streaming kernel takes (r^3 a
+        multiple of 2048, <= 32^3): the split voxel stage (head: prep +
+        means; tail: the dense-grid stream)."""
+        r3 = self.r ** 3
+        return self.n <= 2048 and r3 % 2048 == 0 and r3 <= 32768
+
+    def _stream_devox(self):
+        return self.stream_devox and bool(
+            _lib.load().pcr_extractor_stream_devox_ok(self.n, self.c, self.r))
+
+    def voxel_head(self, xyz, features, stream, slot=0, desc=None):
+        """The split voxel stage's head: prep, then the voxel means (with the
+        devox + descriptor unless they ride in the grid stream)."""
+        self.voxel_prep(xyz, stream, slot)
+        if self._stream_devox():
+            self.voxel_means(features, stream, slot)
+        else:
+            self.voxel_means_devox(features, stream, desc, slot)
+
+    def voxel_tail(self, stream, slot=0, desc=None):
+        """The split voxel stage's tail: the dense grid + cnt streamed from the
+        head's means (with the devox + descriptor for <= 1024-point clouds,
+        DESIGN.md 4.5)."""
+        if self._stream_devox():
+            self.voxel_stream_devox(stream, desc, slot)
+        else:
+            self.voxel_stream(stream, slot)
+
+    def pipelined_steps(self, steps, batch, consume, select_events=None, prefetch=False,
+                        voxel_ahead=False):
         """`steps` train steps whose neighbour side runs one batch ahead.
 
         A batch's self-KNN + local PPF depend on its coordinates and normals
@@ -406,7 +447,13 @@ class SphExtractor:
         return NEW storage (never a tensor step s still reads) and not to
         depend on consume(s).
         select_events: optional list of (ev0, ev1) per step, recorded on s_nbr
-        around that step's selection launch (its in-step duration)."""
+        around that step's selection launch (its in-step duration).
+        voxel_ahead=True (needs prefetch=True and the split voxel stage):
+        the voxel head of batch s+1 (prep + means, devox) also runs one batch
+        ahead, on s_vox, beside step s's grid stream and consume; only the
+        grid stream stays on the caller's stream.  The voxel outputs then
+        alternate between two sets like the index sets (outputs(slot)); batch
+        s+1's head waits until step s-1's consume is done with its set."""
         cur = torch.cuda.current_stream(self.device)
         # set 1's buffers are made here, before s_nbr forks from the caller's
         # stream.  Made lazily inside the loop they could reuse a block the
@@ -414,8 +461,13 @@ class SphExtractor:
         # pending on the caller's stream, and s_nbr wrote them with no order
         # against those kernels (an illegal-address fault on the GPU when the
         # KNN workspace landed there).
+        ahead = bool(voxel_ahead) and bool(prefetch) and self._split_voxels()
+        self._vsep = ahead
         self._set(1)
         self._ppf(1)
+        if ahead:
+            self._vset(1)
+            self.s_vox.wait_stream(cur)
         self.s_nbr.wait_stream(cur)
 
         def fetch(s):
@@ -426,7 +478,24 @@ class SphExtractor:
             return t, ev
 
         done = [None, None]
+
+        def head(s, item):
+            # batch s's voxel head on s_vox, after its producers and after
+            # step s-2's consume (the last reader of set s % 2)
+            (hx, _, hf), e_h = item
+            q = s & 1
+            self.s_vox.wait_event(e_h)
+            if done[q] is not None:
+                self.s_vox.wait_event(done[q])
+            hx.record_stream(self.s_vox)
+            hf.record_stream(self.s_vox)
+            self.voxel_head(hx, hf, self.s_vox.cuda_stream, q)
+            ev = torch.cuda.Event()
+            ev.record(self.s_vox)
+            return ev
+
         nxt = fetch(0) if steps > 0 else None
+        e_vh = head(0, nxt) if ahead and steps > 0 else None
         for s in range(steps):
             (xyz, normals, features), e_in = nxt
             q = s & 1
@@ -440,7 +509,12 @@ class SphExtractor:
                 # the next batch is produced ahead of this step's voxel side
                 # and consume (its neighbours wait for its producers only)
                 nxt = fetch(s + 1) if s + 1 < steps else None
-            self.enqueue_voxels(xyz, features, cur.cuda_stream, q)
+            if ahead:
+                cur.wait_event(e_vh)
+                self.voxel_tail(cur.cuda_stream, q)
+                e_vh = head(s + 1, nxt) if s + 1 < steps else None
+            else:
+                self.enqueue_voxels(xyz, features, cur.cuda_stream, q)
             cur.wait_event(e_nbr)
             consume(s, self.outputs(slot=q, idx_slot=q))
             ev = torch.cuda.Event()
@@ -449,14 +523,17 @@ class SphExtractor:
             if not prefetch:
                 nxt = fetch(s + 1) if s + 1 < steps else None
         cur.wait_stream(self.s_nbr)
+        if ahead:
+            cur.wait_stream(self.s_vox)
 
     def outputs(self, slot=0, idx_slot=0):
         _, _, dinds, dwgts, _ = self._set(slot)
+        nc, ind, devox, desc = self._vset(slot)
         return {
             "knn_idx": self._set(idx_slot)[4], "local_ppf": self._ppf(idx_slot),
-            "norm_coords": self.norm_coords,
-            "ind": self.ind, "cnt": self.cnt, "grid": self.grid, "devox": self.devox,
-            "dinds": dinds, "dwgts": dwgts, "desc": self.desc,
+            "norm_coords": nc,
+            "ind": ind, "cnt": self.cnt, "grid": self.grid, "devox": devox,
+            "dinds": dinds, "dwgts": dwgts, "desc": desc,
         }
 
     def _get_runner(self, timed_steps):

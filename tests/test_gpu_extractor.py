@@ -298,14 +298,16 @@ def test_extractor_ind_vs_reference_fp32_normalisation(dev, seed):
     assert total <= b * n // 1000
 
 
-@pytest.mark.parametrize("prefetch", [False, True])
+@pytest.mark.parametrize("prefetch", [False, True, "voxel_ahead"])
 @pytest.mark.parametrize("b,n,c,k,r", [(4, 1024, 16, 32, 16), (2, 2048, 32, 32, 32),
                                        (3, 1500, 7, 16, 16)])
 def test_extractor_pipelined_steps(dev, b, n, c, k, r, prefetch):
     """SphExtractor.pipelined_steps (bench.py c3: each batch's KNN + local
-    PPF on s_nbr one batch ahead of the caller's voxel side and backwards):
-    every step sees exactly its own batch's outputs, equal to the oracle,
-    and the consume callback's devox backward equals the serial one."""
+    PPF on s_nbr one batch ahead of the caller's voxel side and backwards;
+    voxel_ahead: each batch's voxel head too, on s_vox, with alternating
+    voxel output sets): every step sees exactly its own batch's outputs,
+    equal to the oracle, and the consume callback's devox backward equals
+    the serial one."""
     from pcr_amd import ops
     from pcr_amd.extractor import SphExtractor
     batches = [gaussian_clouds(b, n, seed=40 + s, c=c) for s in range(4)]
@@ -319,7 +321,8 @@ def test_extractor_pipelined_steps(dev, b, n, c, k, r, prefetch):
         gg = ops.spherical_trilinear_devoxelize_backward(gy, out["dinds"], out["dwgts"], r)
         got.append(({kk: v.clone() for kk, v in out.items()}, gg))
 
-    ex.pipelined_steps(4, lambda s: tb[s], consume, prefetch=prefetch)
+    ex.pipelined_steps(4, lambda s: tb[s], consume, prefetch=bool(prefetch),
+                       voxel_ahead=prefetch == "voxel_ahead")
     torch.cuda.synchronize()
     assert len(got) == 4
     for s, (out, gg) in enumerate(got):
