@@ -903,6 +903,68 @@ typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 // 1.95 ms (profiles/r05_ab_stream_devox.log), so c3 keeps the devox in the
 // means launch
 constexpr int kStreamDvMaxN = 1024;
+// One streaming iteration of the grid-stream kernels: U groups of 4
+// consecutive cells per thread, branch-free -- every LDS read of the U groups
+// (occupancy word + prefix, then the means / counts, slot n = 0 for empty
+// cells) is issued before any is waited on; one 16-byte store per channel
+// (+ cnt) and group.  Stores with cache policy AUX (16 = sc1: write-through,
+// the line is not kept in the XCD's L2, so the grid stream does not evict the
+// other kernels' working sets).
+template <int NTS, int U, int AUX, int G>
+__device__ inline void stream_cells(int base0, float* ob, int gcount, const float* ms0, int* cb,
+                                    int r3, int n, int ms, const unsigned* bm_s,
+                                    const unsigned short* pre_s, const unsigned short* scnt_s) {
+  unsigned word[U];
+  int pw[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const int base = min(base0 + u * NTS * 4, r3 - 4);
+    word[u] = bm_s[base >> 5];
+    pw[u] = pre_s[base >> 5];
+  }
+  int ix[U][4];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const int sh = (base0 + u * NTS * 4) & 31;
+    const unsigned nib = (word[u] >> sh) & 15u;
+    const int pre = pw[u] + __popc(word[u] & ((1u << sh) - 1u));
+    ix[u][0] = (nib & 1u) ? pre : n;
+    ix[u][1] = (nib & 2u) ? pre + (int)(nib & 1u) : n;
+    ix[u][2] = (nib & 4u) ? pre + __popc(nib & 3u) : n;
+    ix[u][3] = (nib & 8u) ? pre + __popc(nib & 7u) : n;
+  }
+  float4 v[U][G];
+#pragma unroll
+  for (int u = 0; u < U; u++)
+#pragma unroll
+    for (int g = 0; g < G; g++) {
+      if (g < gcount) {
+        const float* ms_g = ms0 + (size_t)g * ms;
+        v[u][g] = float4{ms_g[ix[u][0]], ms_g[ix[u][1]], ms_g[ix[u][2]], ms_g[ix[u][3]]};
+      }
+    }
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(ob, (short)0, G * r3 * 4, 0x00020000);
+#pragma unroll
+  for (int g = 0; g < G; g++) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int base = base0 + u * NTS * 4;
+      if (base < r3 && g < gcount)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v[u][g]), rs,
+                                               (g * r3 + base) * 4, 0, AUX);
+    }
+  }
+  if (cb) {
+    const auto rc = __builtin_amdgcn_make_buffer_rsrc(cb, (short)0, r3 * 4, 0x00020000);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int base = base0 + u * NTS * 4;
+      const u32x4_t cv = {scnt_s[ix[u][0]], scnt_s[ix[u][1]], scnt_s[ix[u][2]], scnt_s[ix[u][3]]};
+      if (base < r3) __builtin_amdgcn_raw_buffer_store_b128(cv, rc, base * 4, 0, AUX);
+    }
+  }
+}
+
 // DVN: 0 = no devox role; else the most points per cloud
 template <int NS, int NB, int U, int AUX, int G = kStreamG, int NG = kStreamNG, int DVN = 0>
 __global__ __launch_bounds__((NS + 1) * 64) void vox_stream_kernel(int c, int n, int r3, VoxWs ws,
@@ -995,64 +1057,6 @@ __global__ __launch_bounds__((NS + 1) * 64) void vox_stream_kernel(int c, int n,
   }
 
   // ---- streamer waves
-  // U streaming iterations at once, branch-free: every LDS read of the U
-  // groups of 4 consecutive cells (occupancy word + prefix, then the means /
-  // counts, slot n = 0 for empty cells) is issued before any is waited on;
-  // one 16-byte store per channel (+ cnt) and group
-  auto stream_u = [&](int base0, float* ob, int g_lo, int gcount, const float* ms0, int* cb) {
-    unsigned word[U];
-    int pw[U];
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      const int base = min(base0 + u * NTS * 4, r3 - 4);
-      word[u] = bm_s[base >> 5];
-      pw[u] = pre_s[base >> 5];
-    }
-    int ix[U][4];
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      const int sh = (base0 + u * NTS * 4) & 31;
-      const unsigned nib = (word[u] >> sh) & 15u;
-      const int pre = pw[u] + __popc(word[u] & ((1u << sh) - 1u));
-      ix[u][0] = (nib & 1u) ? pre : n;
-      ix[u][1] = (nib & 2u) ? pre + (int)(nib & 1u) : n;
-      ix[u][2] = (nib & 4u) ? pre + __popc(nib & 3u) : n;
-      ix[u][3] = (nib & 8u) ? pre + __popc(nib & 7u) : n;
-    }
-    float4 v[U][G];
-#pragma unroll
-    for (int u = 0; u < U; u++)
-#pragma unroll
-      for (int g = 0; g < G; g++) {
-        if (g >= g_lo && g < gcount) {
-          const float* ms_g = ms0 + (size_t)g * ms;
-          v[u][g] = float4{ms_g[ix[u][0]], ms_g[ix[u][1]], ms_g[ix[u][2]], ms_g[ix[u][3]]};
-        }
-      }
-    // buffer stores with cache policy AUX (16 = sc1: write-through, the
-    // line is not kept in the XCD's L2, so the grid stream does not evict
-    // the other kernels' working sets)
-    const auto rs = __builtin_amdgcn_make_buffer_rsrc(ob, (short)0, G * r3 * 4, 0x00020000);
-#pragma unroll
-    for (int g = 0; g < G; g++) {
-#pragma unroll
-      for (int u = 0; u < U; u++) {
-        const int base = base0 + u * NTS * 4;
-        if (base < r3 && g >= g_lo && g < gcount)
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v[u][g]), rs,
-                                                 (g * r3 + base) * 4, 0, AUX);
-      }
-    }
-    if (cb) {
-      const auto rc = __builtin_amdgcn_make_buffer_rsrc(cb, (short)0, r3 * 4, 0x00020000);
-#pragma unroll
-      for (int u = 0; u < U; u++) {
-        const int base = base0 + u * NTS * 4;
-        const u32x4_t cv = {scnt_s[ix[u][0]], scnt_s[ix[u][1]], scnt_s[ix[u][2]], scnt_s[ix[u][3]]};
-        if (base < r3) __builtin_amdgcn_raw_buffer_store_b128(cv, rc, base * 4, 0, AUX);
-      }
-    }
-  };
   // DV: this thread's points i = tid + e NTS, their 8 corners' segments
   // (empty corner -> slot n, whose mean is 0; two u16 per register) and
   // weights, for every item
@@ -1092,7 +1096,8 @@ __global__ __launch_bounds__((NS + 1) * 64) void vox_stream_kernel(int c, int n,
     const float* ms0 = mean_s + (size_t)(it % NB) * (BUFB / 4);
     for (int st = 0; st < nstep; st++) {
       const int sp = st + rot < nstep ? st + rot : st + rot - nstep;
-      stream_u(sp * NTS * 4 * U + tid * 4, ob, 0, gcount, ms0, cb);
+      stream_cells<NTS, U, AUX, G>(sp * NTS * 4 * U + tid * 4, ob, gcount, ms0, cb, r3, n, ms,
+                                   bm_s, pre_s, scnt_s);
     }
     if (DV) {
       // devox of the item's channels (vox_means_kernel's loop) + descriptor partials

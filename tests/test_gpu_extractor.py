@@ -177,6 +177,67 @@ def test_extractor_runner_multi_queue_rings(dev, schedule, rings):
         ex.run_ring(tb[:schedule - 5], 2, schedule=schedule)
 
 
+@pytest.mark.parametrize("b,n,c,r", [(3, 1000, 7, 16), (2, 300, 5, 32), (4, 1024, 64, 32),
+                                     (2, 1, 3, 16), (5, 64, 1, 16)])
+@pytest.mark.parametrize("with_desc", [True, False])
+def test_voxel_back_half_variants_identical(dev, b, n, c, r, with_desc):
+    """The two back halves of the split voxel stage after one prep give the
+    same bits: means_devox + stream (the reference composition) and means +
+    stream_devox (devox + descriptor inside the grid stream, the c2 product
+    path) -- grid, cnt, devox and desc (NULL desc included), at clouds below
+    1024 points, odd channel counts (a last item with one channel) and a
+    one-point cloud; one size also against the oracle."""
+    from pcr_amd import _lib
+    from pcr_amd.ops import _ptr
+    lib = _lib.load()
+    assert lib.pcr_extractor_stream_devox_ok(n, c, r)
+    xyz, _, feat = gaussian_clouds(b, n, seed=7 * n + c, c=c)
+    tx, tf = T(xyz, dev), T(feat, dev)
+    r3 = r ** 3
+    ws = torch.empty(lib.pcr_extractor_workspace_size(b, n, c, r), dtype=torch.uint8, device=dev)
+    e = torch.empty
+    nc, ind = e((b, 3, n), device=dev), e((b, n), dtype=torch.int32, device=dev)
+    dinds, dwgts = e((b, 8, n), dtype=torch.int32, device=dev), e((b, 8, n), device=dev)
+    st = torch.cuda.current_stream().cuda_stream
+    _lib.check(lib.pcr_extractor_voxel_prep(_ptr(tx), b, n, r, _ptr(nc), _ptr(ind), _ptr(dinds),
+                                            _ptr(dwgts), _ptr(ws), ws.numel(), st), "prep")
+    outs = []
+    for variant in range(2):
+        cnt = torch.full((b, r3), -7, dtype=torch.int32, device=dev)
+        grid = torch.full((b, c, r3), float("nan"), device=dev)
+        devox = torch.full((b, c, n), float("nan"), device=dev)
+        desc = torch.full((b, c), float("nan"), device=dev) if with_desc else None
+        if variant == 0:
+            # means_devox needs a descriptor buffer: a scratch one when desc is NULL
+            d0 = desc if with_desc else e((b, c), device=dev)
+            _lib.check(lib.pcr_extractor_voxel_means_devox(
+                _ptr(tf), b, c, n, r, _ptr(devox), _ptr(dinds), _ptr(dwgts), _ptr(d0),
+                _ptr(ws), ws.numel(), st), "means_devox")
+            _lib.check(lib.pcr_extractor_voxel_stream(b, c, n, r, _ptr(cnt), _ptr(grid), _ptr(ws),
+                                                      ws.numel(), st), "stream")
+        elif variant == 1:
+            _lib.check(lib.pcr_extractor_voxel_means(_ptr(tf), b, c, n, r, _ptr(ws), ws.numel(),
+                                                     st), "means")
+            _lib.check(lib.pcr_extractor_voxel_stream_devox(
+                b, c, n, r, _ptr(cnt), _ptr(grid), _ptr(devox), _ptr(dwgts), _ptr(desc),
+                _ptr(ws), ws.numel(), st), "stream_devox")
+        outs.append((cnt, grid, devox, desc))
+    torch.cuda.synchronize()
+    for v in (1,):
+        for name, a, o in zip(("cnt", "grid", "devox", "desc"), outs[0], outs[v]):
+            if a is None:
+                assert o is None
+                continue
+            assert torch.equal(a, o), (v, name)
+    if b == 3:
+        ref = expected_step(xyz, gaussian_clouds(b, n, seed=7 * n + c, c=c)[1], feat, 1, r)
+        cnt, grid, devox, desc = outs[1]
+        assert np.array_equal(N(cnt), ref["cnt"]) and np.array_equal(N(grid), ref["grid"])
+        assert np.array_equal(N(devox), ref["devox"])
+        if with_desc:
+            assert np.array_equal(N(desc), ref["desc"])
+
+
 def test_extractor_full_size_properties(dev):
     """BASELINE c2 shape: 32 x 1024, k=32, r=32, C=64 -- size-independent
     properties: ind consistent with cnt, grid empty where cnt == 0, the grid
