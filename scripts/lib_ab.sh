@@ -1,7 +1,9 @@
 #!/bin/bash
-# A/B of library builds (lib/libpcr_amd_exp_<name>.so, made by hand with
-# -D knobs): interleaved bench.py runs of each workload per build, each under
-# its own time limit; stops at the first crash / timeout.
+# A/B of library builds (lib/libpcr_<name>.so: "amd" is the product, other
+# builds are copied in by hand, e.g. lib/libpcr_ab_base.so from a worktree of
+# the previous commit, and deleted after the A/B): interleaved bench.py runs
+# of each workload per build, each under its own time limit; stops at the
+# first crash / timeout.  BENCH_ARGS: extra bench.py flags; TAG: log prefix.
 #   usage: scripts/lib_ab.sh "<workload> ..." <rounds> <name> [<name> ...]
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out
@@ -11,8 +13,8 @@ wls=$1; rounds=$2; shift 2
 for r in $(seq 1 "$rounds"); do
   for wl in $wls; do
     for name in "$@"; do
-      out=gpurun_out/ab_${wl}_${name}_$r.log
-      PCR_AMD_LIB=$LIBDIR/libpcr_amd_exp_$name.so timeout -k 10 300 \
+      out=gpurun_out/${TAG:-ab}_${wl}_${name}_$r.log
+      PCR_AMD_LIB=$LIBDIR/libpcr_$name.so timeout -k 10 300 \
         python bench.py --workload "$wl" --no-cpu-baseline $BENCH_ARGS > "$out" 2>&1
       rc=$?
       if [ $rc -ne 0 ]; then echo "$wl $name rc=$rc"; tail -5 "$out"; exit $rc; fi
