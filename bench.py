@@ -107,9 +107,9 @@ def parse(argv=None):
                     help="most pipelined steps per native runner call (extract / pairs); "
                          "--steps and --warmup are split into calls of at most this many")
     ap.add_argument("--batches", type=int, default=None,
-                    help="extract / pairs: distinct input batches cycled through the timed "
-                         "steps (the runner's batch ring; each batch has its own output set; "
-                         "default 20 extract, 8 pairs)")
+                    help="distinct input batches cycled through the timed steps (extract / "
+                         "pairs: the runner's batch ring, each batch with its own output set; "
+                         "default 20 extract, 8 pairs, 4 c3)")
     args = ap.parse_args(argv)
     b, n, k, r, c = DEFAULTS[args.workload]
     args.batch = b if args.batch is None else args.batch
@@ -123,7 +123,7 @@ def parse(argv=None):
     if args.warmup is None:
         args.warmup = 3 if heavy else 40
     if args.batches is None:
-        args.batches = 8 if args.workload == "pairs" else 20
+        args.batches = {"pairs": 8, "c3": 4}.get(args.workload, 20)
     if args.schedule is None:
         # pairs: 250.5k vs 234.3k clouds/s with schedule 7 (the matching
         # lengthens the voxel chain); extract: 381-395k with 6 against
@@ -483,9 +483,14 @@ class C3Workload:
         self.ops = ops
         self.args, self.dev, self.world = args, dev, world
         b, n, c, k, r = args.batch, args.points, args.channels, args.k, args.res
-        self.inputs = synthetic_inputs(b, n, c, dev, seed=1234 + rank)
+        # a ring of R distinct batches (and upstream gradients): step s
+        # trains on batch s % R, as the reference's loader hands every step a
+        # new batch (train.py:138-153)
+        self.R = args.batches
+        self.batches = [synthetic_inputs(b, n, c, dev, seed=1234 + 7919 * rank + i)
+                        for i in range(self.R)]
         g = torch.Generator(device=dev).manual_seed(99 + rank)
-        self.gy = torch.randn((b, c, n), generator=g, device=dev)
+        self.gys = [torch.randn((b, c, n), generator=g, device=dev) for _ in range(self.R)]
         self.ex = SphExtractor(b, n, c, k, r, device=dev)
         self.main_stream = None
         if args.c3_cu_split > 0:
@@ -502,48 +507,48 @@ class C3Workload:
         self.step_bytes = fwd * b + self.devox_bwd_bytes + vox_bwd * b
         self.t = []
 
-    def _backward(self, out, ev=None):
-        """The step's backward share: devox backward of the synthetic
-        upstream gradient, then voxelize backward of the gradient grid."""
+    def _backward(self, s, out, ev=None):
+        """Step s's backward share: devox backward of its synthetic upstream
+        gradient, then voxelize backward of the gradient grid."""
         ops = self.ops
         if ev is not None:
             ev[0].record()
-        gg = ops.spherical_trilinear_devoxelize_backward(self.gy, out["dinds"], out["dwgts"],
-                                                         self.args.res)
+        gg = ops.spherical_trilinear_devoxelize_backward(self.gys[s % self.R], out["dinds"],
+                                                         out["dwgts"], self.args.res)
         if ev is not None:
             ev[1].record()
         gx = ops.spherical_avg_voxelize_backward(gg, out["ind"], out["cnt"])
         return gg, gx
 
-    def _serial(self, steps, timed, keep=None):
-        xyz, nrm, feat = self.inputs
-        for s in range(steps):
-            out = self.ex.forward(xyz, nrm, feat)
-            res = self._backward(out, self.ev[s] if timed else None)
+    def _serial(self, steps, timed, keep=None, first=0):
+        for s in range(first, first + steps):
+            out = self.ex.forward(*self.batches[s % self.R])
+            res = self._backward(s, out, self.ev[s - first] if timed else None)
             if keep is not None:
                 keep.append((out, res))
 
     def _pipelined(self, steps, timed, keep=None):
         def consume(s, out):
-            res = self._backward(out, self.ev[s] if timed else None)
+            res = self._backward(s, out, self.ev[s] if timed else None)
             if keep is not None:
                 keep.append(({kk: v.clone() for kk, v in out.items()}, res))
         # prefetch: batch(s + 1) before step s's voxel side and consume; the
         # bench's batch tensors are read-only, so that is allowed.  The voxel
         # head (prep + means + devox) of batch s + 1 runs ahead on a side
         # stream too (DESIGN.md 4.6), unless --c3-schedule pipelined-nbr
-        self.ex.pipelined_steps(steps, lambda s: self.inputs, consume,
+        self.ex.pipelined_steps(steps, lambda s: self.batches[s % self.R], consume,
                                 select_events=self.sev if timed else None, prefetch=True,
                                 voxel_ahead=self.args.c3_schedule == "pipelined")
 
     def verify(self):
-        """Three pipelined steps vs the serial forward + backwards: every
-        forward output of the last step and both backward results must be
-        identical (outputs poisoned first)."""
+        """Three pipelined steps (batches 0, 1, 2 of the ring) vs the serial
+        forward + backwards of the third: every forward output of the last
+        step and both backward results must be identical (outputs poisoned
+        first)."""
         if self.args.c3_schedule == "serial":
             return None
         ref = []
-        self._serial(1, False, ref)
+        self._serial(1, False, ref, first=2)
         ref = ({kk: v.clone() for kk, v in ref[0][0].items()}, [t.clone() for t in ref[0][1]])
         for t in [self.ex.local_ppf, self.ex.knn_idx, self.ex.grid, self.ex.devox, self.ex.ind,
                   self.ex.cnt] + [self.ex._ppf(1), self.ex._set(1)[4]]:
@@ -637,7 +642,7 @@ class C3Workload:
                 "resolution": a.res, "channels": a.channels,
                 "global_batch": a.batch * self.world,
                 "parallelism": "dp%d (clouds sharded, no collective)" % self.world,
-                "schedule": a.c3_schedule,
+                "schedule": a.c3_schedule, "distinct_batches": self.R,
                 "cu_split": a.c3_cu_split or None}
 
 
@@ -872,16 +877,16 @@ def main(argv=None):
     value = args.batch * world * args.steps / elapsed
     # per rank: every rank moves its own HBM
     step_gbs = wl.step_bytes * args.steps / elapsed / 1e9
-    if isinstance(kernel, dict) and kernel.get("bytes_per_launch"):
-        # one launch of the dominant kernel per step: its bytes over the step
-        # time is the rate the step sustains for it.  avg_ms_in_step above is
-        # the latency of one launch, which overlapping launches (two in
-        # flight under schedule 6) stretch, so its frac is not comparable
-        # across schedules; this one is.
+    if isinstance(kernel, dict) and kernel.get("bytes_per_launch") and \
+            args.workload in ("extract", "pairs"):
+        # one launch of the dominant kernel per step, two in flight under
+        # the runner's schedules: its bytes over the step time is the rate
+        # the step sustains for it (achieved / frac).  avg_ms_in_step is the
+        # latency of one launch, which the overlap stretches: not a rate.
         agg = kernel["bytes_per_launch"] / (elapsed / args.steps) / 1e9
-        kernel["aggregate"] = {"achieved": round(agg, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                               "frac": round(agg / HBM_PEAK_GBS, 4),
-                               "level": "bytes_per_launch / ms_per_step (one launch per step)"}
+        kernel["achieved"] = round(agg, 1)
+        kernel["frac"] = round(agg / HBM_PEAK_GBS, 4)
+        kernel["level"] = "bytes_per_launch / ms_per_step (one launch per step)"
     result = {
         "metric": METRIC if args.workload in ("extract", "pairs") else
         "point-clouds/sec (%d pts, k=%d) %s" % (args.points, args.k,
@@ -908,7 +913,9 @@ def main(argv=None):
                               % (wl.step_bytes // args.batch, args.batch),
                      "kernel": kernel},
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:
+        # after the timed region, on rank 0's host cores, at every N (the
+        # other ranks wait at the barrier below)
         result["cpu_baseline"] = cpu_baseline(args)
     elif rank == 0:
         result["cpu_baseline"] = None

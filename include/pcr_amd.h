@@ -510,6 +510,11 @@ typedef struct pcr_extractor_args {
   const pcr_extractor_set *sets;
   /* schedule 7: the third voxel workspace (vox_ws_bytes) */
   void *vox_ws3;
+  /* nonzero: the spherical devox + descriptor stay in the means launch
+   * (pcr_extractor_voxel_means_devox + pcr_extractor_voxel_stream) even where
+   * the grid stream could evaluate them (pcr_extractor_stream_devox_ok); 0
+   * (the default): they ride in the grid stream there */
+  int devox_in_means;
 } pcr_extractor_args;
 pcr_status pcr_extractor_run(pcr_runner *runner, const pcr_extractor_args *args, int steps,
                              int schedule, float *desc_steps, void *origin, void *s_nbr,

@@ -10,17 +10,10 @@
 
 #include "common.hpp"
 
-#ifndef PCR_STREAM_DEVOX
-#define PCR_STREAM_DEVOX 1  // A/B builds: 0 = the means launch keeps the devox
-#endif
-constexpr bool kStreamDevox = PCR_STREAM_DEVOX != 0;
-
-#ifndef PCR_S6_HEAD
-// the KNN chains of a call's first PCR_S6_HEAD steps wait for step 0's voxel
+// the KNN chains of a call's first kS6Head steps wait for step 0's voxel
 // means: 20-step calls 366k -> 375k clouds/s (3 interleaved rounds,
-// profiles/r05_ab_head_wait.log), 200 steps unchanged; A/B builds: 0 = none
-#define PCR_S6_HEAD 2
-#endif
+// profiles/r05_ab_head_wait.log), 200 steps unchanged
+constexpr int kS6Head = 2;
 
 namespace pcr {
 namespace {
@@ -346,7 +339,7 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
       // devox, the means launch keeps it and the matching runs before the
       // stream (pairs: 274k against 266k with the matching behind the
       // stream, profiles/r05_ab_stream_devox.log)
-      const bool dv = kStreamDevox && a->match_pairs <= 0 &&
+      const bool dv = !a->devox_in_means && a->match_pairs <= 0 &&
                       pcr_extractor_stream_devox_ok(a->n, a->c, a->r);
       if (dv)
         PCR_TRY(pcr_extractor_voxel_means(io.features, a->b, a->c, a->n, a->r, vw6,
@@ -370,11 +363,10 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
       if (dv) PCR_TRY(match_pairs(a, io, vq, iv, nvq));
       return PCR_OK;
     };
-#if PCR_S6_HEAD
-    // the head of a call: the KNN chains of the first PCR_S6_HEAD steps wait
-    // for step 0's voxel means, so prep + means of step 0 get the chip first
-    // and its grid stream starts sooner (the call's fill)
-    if (s < PCR_S6_HEAD) {
+    // the head of a call: the KNN chains of the first kS6Head steps wait for
+    // step 0's voxel means, so prep + means of step 0 get the chip first and
+    // its grid stream starts sooner (the call's fill)
+    if (s < kS6Head) {
       if (s == 0) PCR_TRY(vox_part());
       PCR_HIP(hipStreamWaitEvent(kq, means_done[0], 0), "head wait");
       PCR_TRY(knn_part());
@@ -383,10 +375,6 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
       PCR_TRY(knn_part());
       PCR_TRY(vox_part());
     }
-#else
-    PCR_TRY(knn_part());
-    PCR_TRY(vox_part());
-#endif
     if (rv && s + a->nsets < steps) {
       PCR_HIP(hipEventRecord(rv[2 * t], vq), "ring record");
       PCR_HIP(hipEventRecord(rv[2 * t + 1], kq), "ring record");

@@ -29,11 +29,6 @@ constexpr int kBigCellBits = 15;          // top Morton bits of the global sort 
 constexpr int kBigCells = 1 << kBigCellBits;
 constexpr int kBlk = 64;
 
-#ifdef PCR_DIAG
-// per wave of the first 1024 workgroups: count end, count visits, collect
-// end, collect visits, collect start (s_memtime)
-static __device__ unsigned long long pcr_diag_wave[1024][8][8];
-#endif
 
 struct KnnSet {
   float* x;   // [b][npad] sorted coordinates (NaN padding)
@@ -651,12 +646,6 @@ __global__ __launch_bounds__(KnnNW<KMAX>::wg * 64) void knn_block_kernel(
   PCR_STAMP(1);
   (void)nflush;
   (void)nproc;
-#ifdef PCR_DIAG
-  if (threadIdx.x == 0 && PCR_WG_LINEAR < 1024) {
-    pcr_diag_stamps[PCR_WG_LINEAR][8] = nflush;
-    pcr_diag_stamps[PCR_WG_LINEAR][9] = nproc;
-  }
-#endif
   // merge the NW lists of a query block: tree of bitonic merges through LDS.
   // The partner's k-k front sentinels (key 0) must not enter the result:
   // they read as +inf.
@@ -770,10 +759,7 @@ __global__ __launch_bounds__(KnnNW<KMAX>::wg * 64) void knn_block_kernel(
 // reference's result: the k lexicographically smallest (d, index) with
 // d < 10000, unfilled slots (10000, 0).
 constexpr int kNB = 24;
-#ifndef PCR_KNN_CAP
-#define PCR_KNN_CAP 88
-#endif
-constexpr int kCap = PCR_KNN_CAP;
+constexpr int kCap = 88;
 constexpr int kSelCache = 1024;  // candidates staged in LDS per workgroup
 constexpr int kSelMaxK = 32;
 constexpr int kCap64 = 112;  // the same selection for 32 < k <= 64 (large clouds): two workgroups per CU
@@ -833,16 +819,6 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     const float* __restrict__ qxyz, const float* __restrict__ qnrm,
     const float* __restrict__ cxyz, const float* __restrict__ cnrm, int relative,
     float* __restrict__ ppf, int sorted_emit) {
-#ifdef PCR_DIAG
-  // experiment bits (diagnostic build only): 1 count without LDS atomics,
-  // 2 candidates from registers instead of LDS, 4 stop after the count,
-  // 8 stop after the collect, 16 collect without stores
-  const int dbg = sorted_emit >> 8;
-  sorted_emit &= 0xFF;
-  int dbg_sink = 0;
-#else
-  constexpr int dbg = 0;
-#endif
   constexpr int FPD = 32 / CB;              // wave fields per counter dword
   constexpr int NG = (NW + FPD - 1) / FPD;  // counter dwords per (bin, lane)
   // the histogram is dead once the cut is chosen: the collected keys reuse it
@@ -950,17 +926,6 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
       // the ids of the wave's 8 candidates (u16) are read with them only
       // when the callback uses them (the collect pass)
       auto rd = [&](int o, float4 (&X)[2], float4 (&Y)[2], float4 (&Z)[2], uint4& J) {
-        if (dbg & 2) {
-          const float f = (float)o * 1e-3f;
-#pragma unroll
-          for (int h = 0; h < 2; h++) {
-            X[h] = float4{f, f + 1.0f, f + 2.0f, f + 3.0f};
-            Y[h] = float4{f - 1.0f, f, f + 0.5f, f - 0.5f};
-            Z[h] = float4{f * 0.5f, f * 0.25f, f, f + 0.25f};
-          }
-          if (WANT_J) J = uint4{(unsigned)o, (unsigned)o + 1u, (unsigned)o + 2u, (unsigned)o + 3u};
-          return;
-        }
 #pragma unroll
         for (int h = 0; h < 2; h++) {
           X[h] = *(const float4*)(cand_s + o + 4 * h);
@@ -1146,10 +1111,6 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
   };
   __syncthreads();
   PCR_STAMP(0);
-#ifdef PCR_DIAG
-  if (threadIdx.x == 0 && PCR_WG_LINEAR < 1024)
-    pcr_diag_stamps[PCR_WG_LINEAR][14] = __builtin_amdgcn_s_memrealtime();
-#endif
 
   // 1. bound
   {
@@ -1217,9 +1178,6 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
   int total = 0, slot = 0, bstar = -1, lo_total = 0, slot_lo = 0;
   int shift = 21, base = ebase;
   unsigned ucut = 0u, ulo = 0u;
-#ifdef PCR_DIAG
-  int diag_reason = fallback ? 1 : 0;
-#endif
   auto count_visit = [&](float lim) {
     unsigned* hw = hist_s + (size_t)(wv / FPD) * (kNB + 1) * kBlk + lane;
     const unsigned inc = 1u << ((wv % FPD) * CB);
@@ -1232,12 +1190,6 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
 #pragma unroll
       for (int h = 0; h < 4; h++) {
         const int e = med3_i32((int)(__float_as_uint(d[h]) >> sh), base, top);
-#ifdef PCR_DIAG
-        if (dbg & 1) {
-          dbg_sink += e;
-          continue;
-        }
-#endif
         __hip_atomic_fetch_add(hwb + e * kBlk, inc, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_WORKGROUP);
       }
@@ -1280,12 +1232,6 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     } else {
       count_visit(lim);
     }
-#ifdef PCR_DIAG
-    if (lane == 0 && PCR_WG_LINEAR < 1024) {
-      pcr_diag_wave[PCR_WG_LINEAR][wv][0] = __builtin_amdgcn_s_memtime();
-      pcr_diag_wave[PCR_WG_LINEAR][wv][1] = (unsigned long long)nvisit;
-    }
-#endif
     __syncthreads();
     PCR_STAMP(2);
     // wave 0 finds the cut of the 64 queries (the other waves would repeat
@@ -1357,9 +1303,6 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
   if (!fallback) {
     count_cut(ftop);
     const bool no_cut = __any(qlive && bstar < 0);
-#ifdef PCR_DIAG
-    diag_reason |= (no_cut ? 2 : 0) | (__any(overflow()) ? 4 : 0);
-#endif
     if (!no_cut && __any(overflow())) {
       // refine: bin 0 = below the cut bin, bins 1..16 = its 16 sub-bins
       const float lim = qlive ? __uint_as_float((unsigned)(base + bstar + 1) << 21) : 0.0f;
@@ -1369,16 +1312,7 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
       for (int i = threadIdx.x; i < NG * (kNB + 1) * kBlk; i += NW * kBlk) hist_s[i] = 0u;
       __syncthreads();
       count_cut(lim);
-#ifdef PCR_DIAG
-      diag_reason |= 8;
-#endif
     }
-#ifdef PCR_DIAG
-    if (dbg & 4) {
-      if (dbg_sink == 0x7fffffff) hist_s[lane] = (unsigned)dbg_sink;
-      return;
-    }
-#endif
     fallback = __any(qlive && bstar < 0) || __any(overflow());
     if (qlive && !fallback) {
       ucut = (unsigned)(base + bstar + 1) << shift;
@@ -1386,23 +1320,12 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     }
   }
   __syncthreads();  // histogram reads done: buf_s overwrites it
-#ifdef PCR_DIAG
-  if (threadIdx.x == 0 && PCR_WG_LINEAR < 1024) {
-    pcr_diag_stamps[PCR_WG_LINEAR][8] = diag_reason;
-    pcr_diag_stamps[PCR_WG_LINEAR][9] = (unsigned long long)total;
-    pcr_diag_stamps[PCR_WG_LINEAR][10] = (unsigned long long)nvisit;
-  }
-#endif
   (void)nvisit;
 
   if (!fallback) {
     // 4. collect
     const float fcut = __uint_as_float(ucut);
     int slot_cut = cut0 + (slot - slot_lo);
-#ifdef PCR_DIAG
-    const int nv0 = nvisit;
-    if (lane == 0 && PCR_WG_LINEAR < 1024) pcr_diag_wave[PCR_WG_LINEAR][wv][4] = __builtin_amdgcn_s_memtime();
-#endif
     visit(fcut, std::true_type(), [&](int pos, const float (&d)[4], uint2 jp) {
       bool take[4];
 #pragma unroll
@@ -1416,7 +1339,7 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
 #pragma unroll
         for (int h = 0; h < 4; h++) {
           // exec-masked: only the taking lanes store (few lanes of a wave)
-          if (take[h] && !(dbg & 16)) {
+          if (take[h]) {
             const bool lo = __float_as_uint(d[h]) < ulo;
             buf_s[(lo ? slot_lo : slot_cut) * kBlk + lane] = make_key_finite(d[h], j4[h]);
             slot_lo += lo ? 1 : 0;
@@ -1429,21 +1352,12 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
     // rows past a lane's own count, up to the wave-wide maximum rounded to
     // four (the sweep reads four rows per wait: eight made this phase the
     // kernel's VGPR peak, 94 instead of 72), read as padding
-#ifdef PCR_DIAG
-    if (dbg & 8) return;
-#endif
     const int cnt_c = total - lo_total;
     auto wave_max_i = [&](int v) {
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off, kWave));
       return __builtin_amdgcn_readfirstlane(v);
     };
-#ifdef PCR_DIAG
-    if (lane == 0 && PCR_WG_LINEAR < 1024) {
-      pcr_diag_wave[PCR_WG_LINEAR][wv][2] = __builtin_amdgcn_s_memtime();
-      pcr_diag_wave[PCR_WG_LINEAR][wv][3] = (unsigned long long)(nvisit - nv0);
-    }
-#endif
     const int smax = wave_max_i(lo_total), cmax = wave_max_i(cnt_c);
     const int spad = (smax + 3) & ~3, cpad = (cmax + 3) & ~3;
     for (int i = lo_total + wv; i < spad; i += NW) buf_s[i * kBlk + lane] = PCR_KEY_PAD;
@@ -1539,10 +1453,6 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
         // (c5 KNN + PPF 2.12 -> 2.09 ms)
         __builtin_nontemporal_store(buf_s[sl * kBlk + q], &rows[(size_t)q * kSkeyK + sl]);
       }
-#ifdef PCR_DIAG
-      if (threadIdx.x == 0 && PCR_WG_LINEAR < 1024)
-        pcr_diag_stamps[PCR_WG_LINEAR][15] = __builtin_amdgcn_s_memrealtime();
-#endif
       return;
     }
     if (!qlive) return;
@@ -1597,10 +1507,6 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
       }
     }
     PCR_STAMP(6);
-#ifdef PCR_DIAG
-    if (threadIdx.x == 0 && PCR_WG_LINEAR < 1024)
-      pcr_diag_stamps[PCR_WG_LINEAR][15] = __builtin_amdgcn_s_memrealtime();
-#endif
     return;
   }
 
@@ -1695,76 +1601,11 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
 // (knn.cu:24-46).  Written as neighbour ids in sorted query order (KnnSet::
 // sidx rows, like knn_select_kernel's sorted_emit 1) through an LDS tile, so
 // every store is a whole 256-byte row.
-#ifndef PCR_WSEL_DEFAULT
-#define PCR_WSEL_DEFAULT 1  // A/B builds: 0 = the per-lane knn_select_kernel
-#endif
 constexpr int kWselChunk = 2;  // consecutive queries a wave takes at a time
 constexpr int kWselWaves = 8;  // waves per workgroup: one 64-query block
 constexpr int kWselCap = 64;   // keys collected per query (one per lane)
 constexpr int kWselTmax = 0x461C3FFF;  // bits of the largest float below 10000
 
-#ifdef PCR_WSEL_CSORT
-// One compare-exchange stage of the sort below on 31-bit keys (so partner -
-// x never overflows): t = partner - x, and the lower lane of the pair takes
-// the partner when t < 0, the upper lane when t > 0, i.e. when
-// (t ^ dir) < 0 with dir = 0 / -1 on lower / upper lanes: x += t & ((t ^
-// dir) >> 31).  Five plain VALU (the partner's DPP folds into the subtract),
-// no VCC / SGPR chain, so the compiler can interleave stages of two queries.
-__device__ inline unsigned wsel_ce(unsigned x, unsigned p, int dir) {
-  const int t = (int)(p - x);
-  return x + (unsigned)(t & ((t ^ dir) >> 31));
-}
-template <int CTRL>
-__device__ inline unsigned wsel_dpp(unsigned v) {
-  return (unsigned)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
-}
-// lane ^ 4 / lane ^ 8 inside a 16-lane row: two bank-masked row shifts
-template <int SH>
-__device__ inline unsigned wsel_xrow(unsigned v) {
-  constexpr int lo_banks = SH == 4 ? 0x5 : 0x3;  // lanes that read lane + SH
-  const int a = __builtin_amdgcn_update_dpp(0, (int)v, 0x100 + SH, 0xF, lo_banks, false);
-  return (unsigned)__builtin_amdgcn_update_dpp(a, (int)v, 0x110 + SH, 0xF, 0xF ^ lo_banks, false);
-}
-// lane ^ 16 / lane ^ 32: gfx950's permlane swaps of a register with itself
-__device__ inline unsigned wsel_x16p(unsigned v) {
-  return __builtin_amdgcn_permlane16_swap(v, v, false, false)[0] |
-         0u;  // element 0: the first operand after the swap (rows swapped pairwise)
-}
-__device__ inline unsigned wsel_x32p(unsigned v) {
-  return __builtin_amdgcn_permlane32_swap(v, v, false, false)[0] | 0u;
-}
-
-// ascending 64-lane bitonic sort of unique 31-bit keys ("mirror" form: the
-// first stage of each merge compares i with its mirror i ^ (kk - 1), so every
-// block sorts ascending and the lower lane of a pair always keeps the min).
-// d[m] = 0 on the lanes with (lane & 2^m) == 0, else -1.
-__device__ inline unsigned wsel_sort64(unsigned x, const int (&d)[6]) {
-  constexpr int X1 = 0xB1, X2 = 0x4E, M4 = 0x1B, M8 = 0x141, M16 = 0x140;
-  x = wsel_ce(x, wsel_dpp<X1>(x), d[0]);
-  x = wsel_ce(x, wsel_dpp<M4>(x), d[1]);
-  x = wsel_ce(x, wsel_dpp<X1>(x), d[0]);
-  x = wsel_ce(x, wsel_dpp<M8>(x), d[2]);
-  x = wsel_ce(x, wsel_dpp<X2>(x), d[1]);
-  x = wsel_ce(x, wsel_dpp<X1>(x), d[0]);
-  x = wsel_ce(x, wsel_dpp<M16>(x), d[3]);
-  x = wsel_ce(x, wsel_xrow<4>(x), d[2]);
-  x = wsel_ce(x, wsel_dpp<X2>(x), d[1]);
-  x = wsel_ce(x, wsel_dpp<X1>(x), d[0]);
-  x = wsel_ce(x, wsel_x16p(wsel_dpp<M16>(x)), d[4]);  // mirror 32
-  x = wsel_ce(x, wsel_xrow<8>(x), d[3]);
-  x = wsel_ce(x, wsel_xrow<4>(x), d[2]);
-  x = wsel_ce(x, wsel_dpp<X2>(x), d[1]);
-  x = wsel_ce(x, wsel_dpp<X1>(x), d[0]);
-  x = wsel_ce(x, wsel_x32p(wsel_x16p(wsel_dpp<M16>(x))), d[5]);  // mirror 64
-  x = wsel_ce(x, wsel_x16p(x), d[4]);
-  x = wsel_ce(x, wsel_xrow<8>(x), d[3]);
-  x = wsel_ce(x, wsel_xrow<4>(x), d[2]);
-  x = wsel_ce(x, wsel_dpp<X2>(x), d[1]);
-  x = wsel_ce(x, wsel_dpp<X1>(x), d[0]);
-  return x;
-}
-
-#else
 // One compare-exchange stage of the sort below where the lower lanes of the
 // pairs are the even lanes (m = 1) or lanes 0-1 of each quad (m = 2): the
 // partner by DPP, folded into the compare and the select (2 VALU + 2 SALU):
@@ -1850,7 +1691,7 @@ PCR_WSEL_ROW_STAGE(wsel_m64,
 // ascending 64-lane bitonic sort ("mirror" form: the first stage of each
 // merge compares i with its mirror i ^ (kk - 1), so every block sorts
 // ascending and the lower lane of a pair always keeps the minimum)
-__device__ inline unsigned wsel_sort64(unsigned x, const int (&)[6]) {
+__device__ inline unsigned wsel_sort64(unsigned x) {
   x = wsel_x1(x);
   x = wsel_m4(x);
   x = wsel_x1(x);
@@ -1877,7 +1718,6 @@ __device__ inline unsigned wsel_sort64(unsigned x, const int (&)[6]) {
   asm volatile("s_nop 1");
   return x;
 }
-#endif
 
 // the same on 64-bit keys (d bits << 32 | original index): exact, rare
 __device__ inline unsigned long long wsel_sort64_exact(unsigned long long x, int lane) {
@@ -1927,12 +1767,6 @@ __global__ __launch_bounds__(kWselWaves * 64) void knn_wsel_kernel(KnnSet s, int
   const int lane = threadIdx.x & 63;
   const size_t cb = (size_t)b * s.npad;
   const int nr = s.npad / kBlk;  // candidate registers in use (<= R)
-#ifdef PCR_DIAG
-  if (threadIdx.x == 0 && PCR_WG_LINEAR < 1023) {
-    pcr_diag_stamps[PCR_WG_LINEAR][12] = __builtin_amdgcn_s_memrealtime();
-    pcr_diag_stamps[PCR_WG_LINEAR][0] = __builtin_amdgcn_s_memtime();
-  }
-#endif
   typedef float pf2v __attribute__((ext_vector_type(2)));
   // the whole cloud, one candidate per lane and register (NaN padding); the
   // candidates' original indices in LDS (cj_s[p], p = 64 r + lane: the
@@ -1986,34 +1820,13 @@ __global__ __launch_bounds__(kWselWaves * 64) void knn_wsel_kernel(KnnSet s, int
       if (u < PCR_KNN_UNDEF) tb = (int)__float_as_uint(u);
     }
   }
-#ifdef PCR_DIAG
-  if (threadIdx.x == 0 && PCR_WG_LINEAR < 1023) pcr_diag_stamps[PCR_WG_LINEAR][1] = __builtin_amdgcn_s_memtime();
-  int dg_exact = 0, dg_slow = 0, dg_keys = 0, dg_pass = 0;
-#endif
   unsigned* kd = kbuf_s[0][wv];
   int* kj = (int*)kbuf_s[1][wv];
   const unsigned kd_addr =  // LDS byte address of the wave's rows
       (unsigned)(uintptr_t)((__attribute__((address_space(3))) unsigned*)kd);
   const float tgt = 0.5f * (float)(k + kWselCap);
-  int sdir[6];  // the sort's lane directions: 0 where lane & 2^m is clear, else -1
-#pragma unroll
-  for (int m = 0; m < 6; m++) sdir[m] = (lane >> m) & 1 ? -1 : 0;
-#ifdef PCR_DIAG
-  unsigned long long ph[6] = {0, 0, 0, 0, 0, 0}, pt = 0;
-#define WSEL_PHASE(i)                                                    \
-  do {                                                                   \
-    const unsigned long long now_ = __builtin_amdgcn_s_memtime();        \
-    if ((i) > 0) ph[(i) - 1] += now_ - pt;                               \
-    pt = now_;                                                           \
-  } while (0)
-#else
-#define WSEL_PHASE(i) \
-  do {                \
-  } while (0)
-#endif
 #pragma unroll 1
   for (int qi = q0; qi < kBlk;) {
-    WSEL_PHASE(0);
     const int qj = __builtin_amdgcn_readlane(qjl, qi);
     if (qj < 0) {
       if (lane < kSortedK) tile_s[qi][lane] = 0;
@@ -2033,7 +1846,6 @@ __global__ __launch_bounds__(kWselWaves * 64) void knn_wsel_kernel(KnnSet s, int
       db[2 * h] = __float_as_uint(d[0]);
       db[2 * h + 1] = __float_as_uint(d[1]);
     }
-    WSEL_PHASE(1);
     // 2. threshold: count(d <= t) by ballots (NaN bits compare above every t)
     // the last pass's ballots are kept for the compaction when they fit in
     // SGPRs (R = 16: 32 of them); R = 32 ballots again there
@@ -2056,9 +1868,6 @@ __global__ __launch_bounds__(kWselWaves * 64) void knn_wsel_kernel(KnnSet s, int
     for (int pass = 0;; pass++) {
       cnt = count_le(tb);
       if (cnt >= k && cnt <= kWselCap) break;
-#ifdef PCR_DIAG
-      dg_pass++;
-#endif
       if (cnt < k) {
         lo = tb;
         cnt_lo = cnt;
@@ -2087,7 +1896,6 @@ __global__ __launch_bounds__(kWselWaves * 64) void knn_wsel_kernel(KnnSet s, int
       if (nb <= lo || nb >= hi) nb = lo + ((hi - lo) >> 1);
       tb = __builtin_amdgcn_readfirstlane(nb);
     }
-    WSEL_PHASE(2);
     int ntake;
     if (!exact) {
       // 3. compact the cnt <= 64 keys with d <= t (the last pass's ballots)
@@ -2129,22 +1937,15 @@ __global__ __launch_bounds__(kWselWaves * 64) void knn_wsel_kernel(KnnSet s, int
       }
       ntake = k;
     }
-    WSEL_PHASE(3);
     // 4. sort 31-bit keys: d bits >> 6 (25 bits: d < 10000) and the slot as payload
     const unsigned dl = lane < ntake ? kd[lane] : 0xFFFFFFFFu;
     unsigned key = lane < ntake ? ((dl >> 6) << 6) | (unsigned)lane : 0x7FFFFFFFu;
-    key = wsel_sort64(key, sdir);
-    WSEL_PHASE(4);
+    key = wsel_sort64(key);
     // a truncated-distance tie among the first k (or at the k-th) needs the
     // exact order (lane i sees lane i + 1: DPP wave_shl:1)
     const unsigned nxt = (unsigned)__builtin_amdgcn_mov_dpp((int)key, 0x130, 0xF, 0xF, false);
     const bool tie = lane < k && lane + 1 < ntake && (key >> 6) == (nxt >> 6);
     const bool slow = __any(tie);
-#ifdef PCR_DIAG
-    dg_exact += exact ? 1 : 0;
-    dg_slow += slow ? 1 : 0;
-    dg_keys += ntake;
-#endif
     if (!slow) {
       const int jo = lane < ntake ? cj_s[kj[key & 63u]] : 0;
       if (lane < k) tile_s[qi][lane] = jo;
@@ -2157,26 +1958,9 @@ __global__ __launch_bounds__(kWselWaves * 64) void knn_wsel_kernel(KnnSet s, int
     // the rows are read before the next query's appends rewrite them (LDS
     // operations of a wave complete in order; this keeps the compiler's order)
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    WSEL_PHASE(5);
     if (++qi % kWselChunk == 0) qi = __builtin_amdgcn_readfirstlane(grab());
   }
-#undef WSEL_PHASE
-#ifdef PCR_DIAG
-  if (lane == 0 && PCR_WG_LINEAR < 1023) pcr_diag_stamps[PCR_WG_LINEAR][4 + wv] = __builtin_amdgcn_s_memtime();
-  // per-wave path counts: (exact << 48 | slow << 32 | passes << 16 | keys / 8), read back by
-  // scripts/wsel_diag.py (no atomics: a shared counter would queue every wave's exit)
-  if (lane == 0 && PCR_WG_LINEAR < 1023)
-    pcr_diag_wave[PCR_WG_LINEAR][wv][0] = ((unsigned long long)dg_exact << 48) |
-                                          ((unsigned long long)dg_slow << 32) |
-                                          ((unsigned long long)dg_pass << 16) | (unsigned)(dg_keys / 8);
-  if (lane == 0 && PCR_WG_LINEAR < 1023)
-    for (int i = 0; i < 5; i++) pcr_diag_wave[PCR_WG_LINEAR][wv][1 + i] = ph[i];
-#endif
   __syncthreads();
-#ifdef PCR_DIAG
-  if (threadIdx.x == 0 && PCR_WG_LINEAR < 1023)
-    pcr_diag_stamps[PCR_WG_LINEAR][13] = __builtin_amdgcn_s_memrealtime();
-#endif
   for (int sl = wv; sl < k; sl += kWselWaves)
     s.sidx[((size_t)b * kSortedK + sl) * s.npad + (size_t)qblk * kBlk + lane] = tile_s[lane][sl];
 }
@@ -2312,7 +2096,7 @@ static void launch_select(const KnnSet& qs, const KnnSet& cs, int b, int k, floa
 #define PCR_SEL(CBV, CLV, CACHEV)                                                             \
   hipLaunchKernelGGL((knn_select_kernel<NW, CBV, CLV, PPF, CAP, KSEL, CACHEV>), grid, blk, 0, st, \
                      qs, cs, k, dist, idx, qxyz, qnrm, cxyz, cnrm, relative, ppf,              \
-                     sorted_emit | (PCR_KNOB("PCR_KNN_DBG", 0) << 8))
+                     sorted_emit)
   if constexpr (CAP == kCap) {
     // c3 clouds (2048 points): 32 KB of candidates in LDS, two workgroups per CU
     if (cs.npad > kSelCache && cs.npad <= 2 * kSelCache) {
@@ -2383,12 +2167,7 @@ static pcr_status launch_block(const KnnSet& qs, const KnnSet& cs, int b, int k,
                                int* idx, const float* qxyz, const float* qnrm, const float* cxyz,
                                const float* cnrm, int relative, float* ppf, hipStream_t st,
                                int sorted_emit = 0) {
-#ifdef PCR_DIAG
-  static const int impl = getenv("PCR_KNN_IMPL") ? atoi(getenv("PCR_KNN_IMPL")) : 0;
-#else
-  constexpr int impl = 0;
-#endif
-  const bool sel = impl == 0 && (k <= kSelMaxK || (k <= kSelMaxK64 && cs.npad > kSelCache));
+  const bool sel = k <= kSelMaxK || (k <= kSelMaxK64 && cs.npad > kSelCache);
   if (sel && sorted_emit == 0 && qs.skey != nullptr) {
     // queries past kSortedMaxN: keys in sorted query order, then un-permuted
     if (k <= kSelMaxK)
@@ -2400,10 +2179,10 @@ static pcr_status launch_block(const KnnSet& qs, const KnnSet& cs, int b, int k,
     launch_emit<PPF>(qs, cs, b, k, dist, idx, qxyz, qnrm, cxyz, cnrm, relative, ppf, st);
     return PCR_OK;
   }
-  if (k <= kSelMaxK && impl == 0) {
+  if (k <= kSelMaxK) {
     launch_select<8, PPF>(qs, cs, b, k, dist, idx, qxyz, qnrm, cxyz, cnrm, relative, ppf, st,
                           sorted_emit);
-  } else if (k <= kSelMaxK64 && cs.npad > kSelCache && impl == 0) {
+  } else if (k <= kSelMaxK64 && cs.npad > kSelCache) {
     // large clouds (BASELINE c5, k = 64): the pruned threshold selection with
     // room for 2.75 k collected keys per query
     launch_select<8, PPF, kCap64, kSelMaxK64>(qs, cs, b, k, dist, idx, qxyz, qnrm, cxyz, cnrm,
@@ -2450,7 +2229,7 @@ pcr_status knn_spatial(const float* xyz1, const float* xyz2, int b, int n, int m
     // against 32.8 for knn_select_kernel).  At 2048 points its R = 32
     // registers per coordinate leave 2 waves per SIMD and it lost (928 us
     // against 600 at c3), so those keep the per-lane kernel.
-    if (s1.npad <= 16 * kBlk && PCR_KNOB("PCR_KNN_WSEL", PCR_WSEL_DEFAULT)) {
+    if (s1.npad <= 16 * kBlk) {
       hipLaunchKernelGGL((knn_wsel_kernel<16>), dim3(s1.nblk, b), dim3(kWselWaves * 64), 0, st,
                          s1, k);
       return PCR_OK;
@@ -2486,9 +2265,3 @@ extern "C" size_t pcr_knn_workspace_size(int b, int n, int m) {
   return pcr::knn_ws_size(b, n, m);
 }
 
-#ifdef PCR_DIAG
-PCR_DIAG_READER(pcr_diag_read_knn)
-extern "C" int pcr_diag_read_knn_wave(unsigned long long* host) {
-  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(pcr::pcr_diag_wave), sizeof(pcr::pcr_diag_wave));
-}
-#endif

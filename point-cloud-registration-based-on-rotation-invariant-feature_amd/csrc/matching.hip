@@ -54,10 +54,7 @@ constexpr int kMT = 128;  // tile rows (f1) and columns (f2)
 // 34 KB, four workgroups per CU) measured 0.417 -> 0.350 ms at c4 (128 pairs
 // x 1024 points, C = 64) and 1.59 -> 1.47 ms at C = 512 against 32 (68 KB,
 // two per CU: the epilogue of one workgroup had too few MFMAs beside it)
-#ifndef PCR_MATCH_KC
-#define PCR_MATCH_KC 16
-#endif
-constexpr int kKC = PCR_MATCH_KC;
+constexpr int kKC = 16;
 constexpr int kMPad = kMT + 4;
 constexpr int kE = kKC * kMT / 256;  // channels of one row each thread stages per stage
 
@@ -196,15 +193,14 @@ __device__ inline void match_epilogue(const f32x16 (&acc)[2][2], const float (&s
   }
 }
 
-// Channels run through LDS in stages of 32, double-buffered: the next
+// Channels run through LDS in stages of kKC, double-buffered: the next
 // stage's global loads are in flight while the MFMAs consume this one, and
 // one barrier per stage suffices (a buffer is rewritten two stages later,
-// after every wave passed the barrier in between).
-#ifndef PCR_MATCH_WPE
-#define PCR_MATCH_WPE 3
-#endif
+// after every wave passed the barrier in between).  Three waves per SIMD:
+// the accumulators stay in the unified VGPR file (143 VGPRs, no AGPRs)
+// (DESIGN.md 4.8).
 template <bool CM>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PCR_MATCH_WPE))) void match_tile_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void match_tile_kernel(
     const float* __restrict__ f1, const float* __restrict__ f2, int n1, int n2, int c,
     const float* __restrict__ sq1, const float* __restrict__ sq2,
     unsigned long long* __restrict__ rowbest, unsigned long long* __restrict__ colbest) {

@@ -1240,7 +1240,7 @@ extern "C" pcr_status pcr_knn_ppf_sorted(const float* xyz, const float* normals,
   // thread, and splitting it re-stages the 48 KB cloud per range (c3: 100 ->
   // 160 us), so those keep one workgroup per (cloud, 4 slots).
   constexpr int SL = 4;
-  const int pr = PCR_KNOB("PCR_PPF_RANGES", n <= 1024 ? ceil_div(n, 512) : 1);
+  const int pr = n <= 1024 ? ceil_div(n, 512) : 1;
   // 16-byte LDS-DMA pieces and output vectors when every row is 16-byte
   // aligned: four points per thread (local_ppf_quad_kernel)
   const bool v16 = n % 4 == 0 && npad % 4 == 0 &&
@@ -1304,25 +1304,15 @@ extern "C" pcr_status pcr_local_ppf_forward(const float* points, const float* no
   PCR_REQUIRE(b >= 0 && n >= 1 && m >= 0 && u >= 0, "local_ppf_forward: invalid sizes");
   PCR_REQUIRE(u <= 65535, "local_ppf_forward: u too large");
   if (b == 0 || m == 0 || u == 0) return PCR_OK;
-  // diagnostic builds: PCR_PPF_SL = slots per thread of the LDS-staged kernel
-  // (0: the unstaged kernel)
-  static const int sl = PCR_KNOB("PCR_PPF_SL", 8);
   PCR_PRIO_INIT();
   if (points == centers && normals == center_normals && n == m && idx_kmajor &&
-      n <= kPpfSelfMaxN && sl != 0) {
+      n <= kPpfSelfMaxN) {
 #define PCR_PPF_SELF(SLV)                                                                     \
   hipLaunchKernelGGL((local_ppf_self_kernel<SLV>), dim3(ceil_div(n, 256), ceil_div(u, SLV), b), \
                      dim3(256), (size_t)6 * n * 4, as_stream(stream), points, normals, idx, n,  \
                      u, relative, out, nullptr, nullptr, 0, nullptr)
-#ifdef PCR_DIAG
-    if (sl == 16) PCR_PPF_SELF(16);
-    else if (sl == 32) PCR_PPF_SELF(32);
-    else if (sl == 4) PCR_PPF_SELF(4);
-    else
-#endif
-      PCR_PPF_SELF(8);
+    PCR_PPF_SELF(8);
 #undef PCR_PPF_SELF
-#undef PCR_PPF_SELF_NT
     return launch_status("local_ppf_forward");
   }
   hipLaunchKernelGGL(local_ppf_kernel, dim3(ceil_div(m, 256), u, b), dim3(256), 0,

@@ -1144,13 +1144,6 @@ __global__ __launch_bounds__((NS + 1) * 64) void vox_stream_kernel(int c, int n,
   }
 }
 
-// workgroups of a grid launch: every item its own workgroup unless
-// PCR_GRID_WGS caps the count (then each loops over several items)
-static int grid_wgs(int nitems) {
-  static const int cap = PCR_KNOB("PCR_GRID_WGS", 0);
-  return cap > 0 && cap < nitems ? cap : nitems;
-}
-
 // ------------------------------------------------------ backward gather
 // grad_x[b,j,i] = grad_y[b,j,ind[i]] * (1/cnt)  (spherical_vox.cu:151-162)
 // One thread per point and kGradCG channels: the point's voxel and count are
@@ -1857,12 +1850,6 @@ static size_t grid_smem_bytes(int G, int n, int nw) {
   return ((size_t)G * n + (size_t)G * (n + 1) + (n + 1) + 2 * (size_t)nw) * 4;
 }
 
-// issue priority of the prep kernel (PCR_PREP_PRIO=0 turns the boost off)
-static int prep_prio() {
-  static const int p = PCR_KNOB("PCR_PREP_PRIO", 1);
-  return p;
-}
-
 // Launch helpers.  `what`: 1 = prep only, 2 = grid only, 3 = both.
 template <int MODE>
 static pcr_status run_voxelize(const float* features, const float* coords_f, const int* coords_i,
@@ -1886,40 +1873,36 @@ static pcr_status run_voxelize(const float* features, const float* coords_f, con
               name, ws_bytes, need);
   PCR_PRIO_INIT();
   if (what & 1) {
-    // clouds of <= 1024 points: a 256- or 512-thread workgroup (PCR_PREP_NT_DEF
-    // below) rather than 1024, so a prep workgroup fits on a CU beside the
-    // other queues' kernels instead of waiting for whole CUs to drain
+    // clouds of <= 1024 points: a 256- or 512-thread workgroup rather than
+    // 1024, so a prep workgroup fits on a CU beside the other queues'
+    // kernels instead of waiting for whole CUs to drain.  257..1024 points:
+    // 512 threads (two points each): under the runner's schedule 6 the prep
+    // kernel heads the critical voxel chain, c2 379-385k -> 385-394k
+    // clouds/s against 256 threads (3 interleaved rounds,
+    // profiles/r04_ab_prep.log); 1024 threads measured between the two
     const bool small = n <= kSmallPrepN;
     const int nt = small ? kSmallPrepThreads : kPrepThreads;
     const int npad = next_pow2(n < nt ? nt : n);
     size_t prep_smem = (size_t)npad * 8 + (size_t)ws.W * 8 + (size_t)n * 8;
     PCR_REQUIRE(prep_smem <= 150 * 1024, "%s: prep LDS %zu too large", name, prep_smem);
-// clouds of 257..1024 points: 512 threads (two points each).  Under the
-// runner's schedule 6 the prep kernel heads the critical voxel chain: c2
-// 379-385k -> 385-394k clouds/s against 256 threads (3 interleaved rounds,
-// profiles/r04_ab_prep.log); 1024 threads measured between the two
-#ifndef PCR_PREP_NT_DEF
-#define PCR_PREP_NT_DEF 512
-#endif
-    static const int exp_nt = PCR_KNOB("PCR_PREP_NT", PCR_PREP_NT_DEF);
-    if (small && exp_nt == 512 && n > 256) {
+    if (small && n > 256) {
       const int npad5 = next_pow2(n < 512 ? 512 : n);
       const size_t sm5 = (size_t)npad5 * 8 + (size_t)ws.W * 8 + (size_t)n * 8;
       allow_big_lds(vox_prep_kernel<MODE, 512>, sm5);
       hipLaunchKernelGGL((vox_prep_kernel<MODE, 512>), dim3(b), dim3(512), sm5, stream, coords_f,
-                         coords_i, n, r, npad5, norm_out, ind, ws, dinds, dwgts, prep_prio());
-    } else if (small && exp_nt != 1024) {
+                         coords_i, n, r, npad5, norm_out, ind, ws, dinds, dwgts, 1);
+    } else if (small) {
       allow_big_lds(vox_prep_kernel<MODE, kSmallPrepThreads>, prep_smem);
       hipLaunchKernelGGL((vox_prep_kernel<MODE, kSmallPrepThreads>), dim3(b),
                          dim3(kSmallPrepThreads), prep_smem, stream, coords_f, coords_i, n, r,
-                         npad, norm_out, ind, ws, dinds, dwgts, prep_prio());
+                         npad, norm_out, ind, ws, dinds, dwgts, 1);
     } else {
       const int npad1 = next_pow2(n < kPrepThreads ? kPrepThreads : n);
       const size_t sm1 = (size_t)npad1 * 8 + (size_t)ws.W * 8 + (size_t)n * 8;
       allow_big_lds(vox_prep_kernel<MODE, kPrepThreads>, sm1);
       hipLaunchKernelGGL((vox_prep_kernel<MODE, kPrepThreads>), dim3(b), dim3(kPrepThreads),
                          sm1, stream, coords_f, coords_i, n, r, npad1, norm_out, ind, ws,
-                         dinds, dwgts, prep_prio());
+                         dinds, dwgts, 1);
     }
   }
   const bool do_grid = (what & 2) != 0;
@@ -1941,7 +1924,7 @@ static pcr_status run_voxelize(const float* features, const float* coords_f, con
     const size_t smem = grid_smem_bytes(G, n, nw);
     PCR_REQUIRE(smem <= 150 * 1024, "%s: grid LDS %zu too large", name, smem);
     allow_big_lds(vox_grid_kernel<3, kGridThreads, 2>, smem);
-    hipLaunchKernelGGL((vox_grid_kernel<3, kGridThreads, 2>), dim3(grid_wgs(ngrp * b)),
+    hipLaunchKernelGGL((vox_grid_kernel<3, kGridThreads, 2>), dim3(ngrp * b),
                        dim3(kGridThreads), smem, stream, features, c, n, r3, G, tile, ws, out, cnt,
                        dinds, dwgts, devox, desc, 1, ngrp, ngrp * b);
   } else if (do_dev) {
@@ -1962,7 +1945,7 @@ static pcr_status run_voxelize(const float* features, const float* coords_f, con
     PCR_REQUIRE(smem <= 150 * 1024, "%s: grid LDS %zu too large", name, smem);
     allow_big_lds(vox_grid_kernel<1, kGridThreads, 2>, smem);
     hipLaunchKernelGGL((vox_grid_kernel<1, kGridThreads, 2>),
-                       dim3(grid_wgs(ntiles * ngrp * b)), dim3(kGridThreads), smem, stream,
+                       dim3(ntiles * ngrp * b), dim3(kGridThreads), smem, stream,
                        features, c, n, r3, G, tile, ws, out, cnt, nullptr, nullptr, nullptr,
                        nullptr, ntiles, ngrp, ntiles * ngrp * b);
   }
@@ -2070,44 +2053,34 @@ extern "C" pcr_status pcr_extractor_voxel_means_devox(const float* features, int
   const int r3 = r * r * r;
   const int tile = ((r3 + 31) / 32) * 32;
   const int nw = tile / 32 + 1;
-  static const int mv = PCR_KNOB("PCR_MEANS_V", 3);
-  static const int mg = PCR_KNOB("PCR_MEANS_G", 2);
-  if (mv == 3 && n <= kMeansMaxN) {
-    // G channels per workgroup (G = 2: ~24 KB of LDS, so it fits beside the
-    // KNN selection's workgroups); every workgroup of a cloud reads the
-    // cloud's corner data, so a larger G reads less of it in all
-#define PCR_LAUNCH_MEANS(GV, NTV)                                                             \
-  do {                                                                                       \
-    const int ngrp = ceil_div(c, GV);                                                        \
-    const size_t smem = ((size_t)GV * n + (size_t)GV * (n + 1) + n + (n + 1)) * 4;           \
-    allow_big_lds(vox_means_kernel<GV, NTV>, smem);                                          \
-    hipLaunchKernelGGL((vox_means_kernel<GV, NTV>), dim3(ngrp * b), dim3(NTV), smem,         \
-                       as_stream(stream), features, c, n, ws, dwgts, devox, desc, ngrp);     \
-  } while (0)
-    // clouds of more than 1024 points (c3: 2048): 512 threads, the same four
-    // points per thread
-    if (n > kMeansPB * kMeansNT) PCR_LAUNCH_MEANS(2, 2 * kMeansNT);
-    else if (mg == 4) PCR_LAUNCH_MEANS(4, kMeansNT);
-    else if (mg == 8) PCR_LAUNCH_MEANS(8, kMeansNT);
-    else PCR_LAUNCH_MEANS(2, kMeansNT);
-#undef PCR_LAUNCH_MEANS
+  if (n <= kMeansMaxN) {
+    // 2 channels per workgroup (~24 KB of LDS, so it fits beside the KNN
+    // selection's workgroups); clouds of more than 1024 points (c3: 2048):
+    // 512 threads, the same four points per thread (4 or 8 channels per
+    // workgroup measured +1% / -2% in the c2 step)
+    const int nt = n > kMeansPB * kMeansNT ? 2 * kMeansNT : kMeansNT;
+    const int ngrp = ceil_div(c, 2);
+    const size_t smem = ((size_t)2 * n + (size_t)2 * (n + 1) + n + (n + 1)) * 4;
+    if (nt == kMeansNT) {
+      allow_big_lds(vox_means_kernel<2, kMeansNT>, smem);
+      hipLaunchKernelGGL((vox_means_kernel<2, kMeansNT>), dim3(ngrp * b), dim3(kMeansNT), smem,
+                         as_stream(stream), features, c, n, ws, dwgts, devox, desc, ngrp);
+    } else {
+      allow_big_lds(vox_means_kernel<2, 2 * kMeansNT>, smem);
+      hipLaunchKernelGGL((vox_means_kernel<2, 2 * kMeansNT>), dim3(ngrp * b), dim3(2 * kMeansNT),
+                         smem, as_stream(stream), features, c, n, ws, dwgts, devox, desc, ngrp);
+    }
     return launch_status(name);
   }
+  // larger clouds: the grid kernel's devox part (means formed per workgroup)
   int G = 1;
-  const int ngrp = pick_groups(c, n, mv == 0 ? 4 : 2, &G);
+  const int ngrp = pick_groups(c, n, 2, &G);
   const size_t smem = grid_smem_bytes(G, n, nw);
   PCR_REQUIRE(smem <= 150 * 1024, "%s: LDS %zu too large", name, smem);
-  if (mv == 0) {
-    allow_big_lds(vox_grid_kernel<2, kDevoxThreads, 4>, smem);
-    hipLaunchKernelGGL((vox_grid_kernel<2, kDevoxThreads, 4>), dim3(ngrp * b), dim3(kDevoxThreads),
-                       smem, as_stream(stream), features, c, n, r3, G, tile, ws, nullptr, nullptr,
-                       dinds, dwgts, devox, desc, 1, ngrp, ngrp * b);
-  } else {
-    allow_big_lds(vox_grid_kernel<2, 256, 2>, smem);
-    hipLaunchKernelGGL((vox_grid_kernel<2, 256, 2>), dim3(ngrp * b), dim3(256), smem,
-                       as_stream(stream), features, c, n, r3, G, tile, ws, nullptr, nullptr, dinds,
-                       dwgts, devox, desc, 1, ngrp, ngrp * b);
-  }
+  allow_big_lds(vox_grid_kernel<2, 256, 2>, smem);
+  hipLaunchKernelGGL((vox_grid_kernel<2, 256, 2>), dim3(ngrp * b), dim3(256), smem,
+                     as_stream(stream), features, c, n, r3, G, tile, ws, nullptr, nullptr, dinds,
+                     dwgts, devox, desc, 1, ngrp, ngrp * b);
   return launch_status(name);
 }
 
@@ -2137,55 +2110,33 @@ extern "C" pcr_status pcr_extractor_voxel_stream(int b, int c, int n, int r, int
   PCR_REQUIRE(n <= kStreamMaxN && r3 <= 32 * kStreamMaxW && r3 % 128 == 0,
               "%s: n=%d r=%d unsupported (n <= %d, r^3 <= %d, r^3 %% 128 == 0)", name, n, r,
               kStreamMaxN, 32 * kStreamMaxW);
-  // channels per item G (one occupancy / segment-index computation per G
-  // stores) and means buffers NB; diagnostic builds can pick other shapes
-  // (two channels and three buffers: 36 KB, so the grid kernel fits on a CU
-  // beside two selection workgroups; four channels per item measured ~3%
-  // slower in the step despite half the index work per store)
-  static const int gk = PCR_KNOB("PCR_STREAM_G", kStreamG);
-  static const int nbk = PCR_KNOB("PCR_STREAM_NB", 0);
-  // clouds of more than 1024 points (c3): two channels, 17 pieces per item
+  // two channels per item and three means buffers: 36 KB, so the grid
+  // kernel fits on a CU beside two selection workgroups (four channels per
+  // item measured ~3% slower in the step despite half the index work per
+  // store); clouds of more than 1024 points (c3): 17 pieces per item
   const bool wide = n > 1024;
-  const int G = wide ? 2 : gk == 8 ? 8 : gk == 4 ? 4 : 2;
-  const int NGP = G == 8 ? 33 : (G == 4 || wide) ? 17 : 9;  // 1 KB pieces holding G rows of ms floats
-  const int NB = (G == 2 || wide) ? kStreamNB : (G == 4 && nbk == 3) ? 3 : 2;
+  constexpr int G = kStreamG;
+  const int NGP = wide ? 17 : kStreamNG;  // 1 KB pieces holding G rows of ms floats
   PCR_REQUIRE(G * ws.ms * 4 <= NGP * 1024, "%s: means rows too long", name);
   const int ngrp = ceil_div(c, G);
   // a few workgroups per cloud (about one per CU in all), each a contiguous
   // range of channel-group items of that cloud
-  static const int cap = PCR_KNOB("PCR_STREAM_WGS", 0);
-  const int total = cap > 0 ? cap : device_cus();
-  int wpc = total / (b > 0 ? b : 1);
+  int wpc = device_cus() / (b > 0 ? b : 1);
   if (wpc < 1) wpc = 1;
   if (wpc > ngrp) wpc = ngrp;
   const int per = ceil_div(ngrp, wpc);
   PCR_REQUIRE(ws.W % 64 == 0, "%s: r^3 %% 2048 != 0 unsupported", name);
-  const size_t smem = (size_t)NB * NGP * 1024 + (size_t)ws.W * 6 +
+  const size_t smem = (size_t)kStreamNB * NGP * 1024 + (size_t)ws.W * 6 +
                       ((size_t)ws.ms * 2 + 255) / 256 * 256;
-#ifdef PCR_DIAG
-  static const int aux = PCR_KNOB("PCR_STREAM_AUX", 16);  // store cache policy experiments
-  static const int nsk = PCR_KNOB("PCR_STREAM_NS", 4);    // streamer waves per workgroup
-#endif
-#define PCR_LAUNCH_STREAM(NSV, NBV, UV, AV, GV, NGV)                                           \
+#define PCR_LAUNCH_STREAM(NGV)                                                                 \
   do {                                                                                        \
-    allow_big_lds(vox_stream_kernel<NSV, NBV, UV, AV, GV, NGV>, smem);                        \
-    hipLaunchKernelGGL((vox_stream_kernel<NSV, NBV, UV, AV, GV, NGV>), dim3(b * wpc),         \
-                       dim3((NSV + 1) * 64), smem, as_stream(stream), c, n, r3, ws, grid, cnt, \
-                       ngrp, wpc, per, nullptr, nullptr, nullptr);                            \
+    allow_big_lds(vox_stream_kernel<4, kStreamNB, 2, 16, G, NGV>, smem);                      \
+    hipLaunchKernelGGL((vox_stream_kernel<4, kStreamNB, 2, 16, G, NGV>), dim3(b * wpc),       \
+                       dim3(5 * 64), smem, as_stream(stream), c, n, r3, ws, grid, cnt, ngrp,   \
+                       wpc, per, nullptr, nullptr, nullptr);                                  \
   } while (0)
-  if (wide) PCR_LAUNCH_STREAM(4, kStreamNB, 2, 16, kStreamG, 17);
-  else
-#ifdef PCR_DIAG
-  if (G == 4 && NB == 3) PCR_LAUNCH_STREAM(4, 3, 2, 16, 4, 17);
-  else if (G == 4) PCR_LAUNCH_STREAM(4, 2, 2, 16, 4, 17);
-  else if (G == 8) PCR_LAUNCH_STREAM(4, 2, 2, 16, 8, 33);
-  else if (aux == 0) PCR_LAUNCH_STREAM(4, 3, 2, 0, 2, 9);
-  else if (aux == 2) PCR_LAUNCH_STREAM(4, 3, 2, 2, 2, 9);
-  else if (nsk == 2) PCR_LAUNCH_STREAM(2, 3, 2, 16, 2, 9);
-  else if (nsk == 8) PCR_LAUNCH_STREAM(8, 3, 2, 16, 2, 9);
-  else
-#endif
-    PCR_LAUNCH_STREAM(4, kStreamNB, 2, 16, kStreamG, kStreamNG);
+  if (wide) PCR_LAUNCH_STREAM(17);
+  else PCR_LAUNCH_STREAM(kStreamNG);
 #undef PCR_LAUNCH_STREAM
   return launch_status(name);
 }

@@ -108,7 +108,7 @@ class ExtractorArgs(ctypes.Structure):
                 ("match_pairs", I), ("corr12", P), ("corr21", P), ("idx1", P), ("idx2", P),
                 ("match_count", P), ("match_ws", P), ("match_ws_bytes", SZ),
                 ("nsets", I), ("set0", I), ("sets", ctypes.POINTER(ExtractorSet)),
-                ("vox_ws3", P)]
+                ("vox_ws3", P), ("devox_in_means", I)]
 
 
 _lib = None

@@ -34,7 +34,9 @@ class SphExtractor:
     def __init__(self, batch, npoints, channels, k, resolution, device="cuda", relative=True,
                  with_dist=False, split_ppf=True, stream_devox=True):
         # stream_devox: the split voxel stage evaluates the devox inside the
-        # grid stream (False: in the means launch; an A/B switch)
+        # grid stream where it applies (<= 1024 points); False keeps it in the
+        # means launch, in the eager / pipelined paths and in the native
+        # runner (pcr_extractor_args.devox_in_means)
         self.stream_devox = stream_devox
         self.b, self.n, self.c, self.k, self.r = batch, npoints, channels, k, resolution
         self.relative = relative
@@ -453,7 +455,12 @@ class SphExtractor:
         ahead, on s_vox, beside step s's grid stream and consume; only the
         grid stream stays on the caller's stream.  The voxel outputs then
         alternate between two sets like the index sets (outputs(slot)); batch
-        s+1's head waits until step s-1's consume is done with its set."""
+        s+1's head waits until step s-1's consume is done with its set.  The
+        second set is this call's only: consume(s, outputs) receives it, and
+        after the call outputs(slot) is back to one voxel set.
+
+        (Round 5 changed the default to prefetch=False: callers that relied
+        on the overlap pass prefetch=True, as the bench does.)"""
         cur = torch.cuda.current_stream(self.device)
         # set 1's buffers are made here, before s_nbr forks from the caller's
         # stream.  Made lazily inside the loop they could reuse a block the
@@ -494,37 +501,42 @@ class SphExtractor:
             ev.record(self.s_vox)
             return ev
 
-        nxt = fetch(0) if steps > 0 else None
-        e_vh = head(0, nxt) if ahead and steps > 0 else None
-        for s in range(steps):
-            (xyz, normals, features), e_in = nxt
-            q = s & 1
-            self.s_nbr.wait_event(e_in)
-            xyz.record_stream(self.s_nbr)
-            normals.record_stream(self.s_nbr)
-            e_nbr = self.enqueue_neighbors(
-                xyz, normals, q, after=done[q],
-                events=select_events[s] if select_events is not None else None)
-            if prefetch:
-                # the next batch is produced ahead of this step's voxel side
-                # and consume (its neighbours wait for its producers only)
-                nxt = fetch(s + 1) if s + 1 < steps else None
+        try:
+            nxt = fetch(0) if steps > 0 else None
+            e_vh = head(0, nxt) if ahead and steps > 0 else None
+            for s in range(steps):
+                (xyz, normals, features), e_in = nxt
+                q = s & 1
+                self.s_nbr.wait_event(e_in)
+                xyz.record_stream(self.s_nbr)
+                normals.record_stream(self.s_nbr)
+                e_nbr = self.enqueue_neighbors(
+                    xyz, normals, q, after=done[q],
+                    events=select_events[s] if select_events is not None else None)
+                if prefetch:
+                    # the next batch is produced ahead of this step's voxel side
+                    # and consume (its neighbours wait for its producers only)
+                    nxt = fetch(s + 1) if s + 1 < steps else None
+                if ahead:
+                    cur.wait_event(e_vh)
+                    self.voxel_tail(cur.cuda_stream, q)
+                    e_vh = head(s + 1, nxt) if s + 1 < steps else None
+                else:
+                    self.enqueue_voxels(xyz, features, cur.cuda_stream, q)
+                cur.wait_event(e_nbr)
+                consume(s, self.outputs(slot=q, idx_slot=q))
+                ev = torch.cuda.Event()
+                ev.record(cur)
+                done[q] = ev
+                if not prefetch:
+                    nxt = fetch(s + 1) if s + 1 < steps else None
+            cur.wait_stream(self.s_nbr)
             if ahead:
-                cur.wait_event(e_vh)
-                self.voxel_tail(cur.cuda_stream, q)
-                e_vh = head(s + 1, nxt) if s + 1 < steps else None
-            else:
-                self.enqueue_voxels(xyz, features, cur.cuda_stream, q)
-            cur.wait_event(e_nbr)
-            consume(s, self.outputs(slot=q, idx_slot=q))
-            ev = torch.cuda.Event()
-            ev.record(cur)
-            done[q] = ev
-            if not prefetch:
-                nxt = fetch(s + 1) if s + 1 < steps else None
-        cur.wait_stream(self.s_nbr)
-        if ahead:
-            cur.wait_stream(self.s_vox)
+                cur.wait_stream(self.s_vox)
+        finally:
+            # the second voxel output set serves this call's consume() only:
+            # later eager calls (voxel_prep / outputs(slot=1) ...) use set 0
+            self._vsep = False
 
     def outputs(self, slot=0, idx_slot=0):
         _, _, dinds, dwgts, _ = self._set(slot)
@@ -603,6 +615,7 @@ class SphExtractor:
             self._ws3 = torch.empty_like(self.ws)
             self._order_new_buffers()
         a.vox_ws3 = _ptr(self._ws3)
+        a.devox_in_means = 0 if self.stream_devox else 1
         if match is not None:
             if 2 * match.pairs != self.b or match.n != self.n:
                 raise RuntimeError("match buffers are for %d pairs of %d points"
