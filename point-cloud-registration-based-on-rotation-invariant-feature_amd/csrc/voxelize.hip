@@ -46,7 +46,11 @@ struct VoxWs {
   int* nseg;         // [b]
   unsigned* bitmap;  // [b][W] occupancy bits
   int* wprefix;      // [b][W] occupied voxels before word w
+  unsigned short* wpre16;  // [b][W] the same as u16 (clouds of < 65536 points): the grid
+                           // stream loads it instead of scanning the bitmap again
   int* dseg;         // [b][8][n] segment of each devox corner (-1: empty / none)
+  unsigned* dseg16;  // [b][n][4]: the same as u16 pairs, empty -> n (n <= 65535): one
+                     // 16-byte load per point for the grid stream's devox role
   float* means;      // [b][c][ms] voxel means per occupied segment (extractor only)
   unsigned short* segcnt;  // [b][ms] points per occupied segment (extractor only)
   int ms;            // row stride of means / segcnt: n + 1 rounded up to 4
@@ -71,23 +75,28 @@ static size_t vox_ws_layout(int b, int n, int r, VoxWs* ws, void* base, int cm =
   int* nseg = (int*)take((size_t)b * 4);
   unsigned* bitmap = (unsigned*)take((size_t)b * W * 4);
   int* wprefix = (int*)take((size_t)b * W * 4);
+  unsigned short* wpre16 = (unsigned short*)take((size_t)b * W * 2);
   int* dseg = (int*)take((size_t)b * 8 * n * 4);
+  unsigned* dseg16 = (unsigned*)take((size_t)b * n * 16);
   const int ms = (n + 1 + 3) / 4 * 4;
   // + 16 KB: vox_stream_kernel's LDS-DMA reads a whole item's pieces, past
   // the last row when c is odd
   float* means = cm > 0 ? (float*)take((size_t)b * cm * ms * 4 + 16384) : nullptr;
-  unsigned short* segcnt = cm > 0 ? (unsigned short*)take((size_t)b * ms * 2 + 16) : nullptr;
+  // (+ 256 B: the grid stream's LDS-DMA reads whole 256-byte pieces)
+  unsigned short* segcnt = cm > 0 ? (unsigned short*)take((size_t)b * ms * 2 + 256) : nullptr;
   if (ws) {
     ws->means = means;
     ws->segcnt = segcnt;
     ws->ms = ms;
     ws->dseg = dseg;
+    ws->dseg16 = dseg16;
     ws->perm = perm;
     ws->seg_off = seg_off;
     ws->seg_vox = seg_vox;
     ws->nseg = nseg;
     ws->bitmap = bitmap;
     ws->wprefix = wprefix;
+    ws->wpre16 = wpre16;
     ws->W = W;
   }
   return off;
@@ -328,6 +337,7 @@ __global__ __launch_bounds__(NT) void vox_prep_kernel(
       const unsigned word = bm[w];
       gbm[w] = word;
       gpre[w] = run;
+      ws.wpre16[(size_t)b * W + w] = (unsigned short)run;
       pre_l[w] = run;
       run += __popc(word);
     }
@@ -347,6 +357,7 @@ __global__ __launch_bounds__(NT) void vox_prep_kernel(
         // dropped or not interpolated (spherical_trilinear_devox.cu:41-65
         // `continue`): every corner -1, so the output is +0 as untouched
         const bool skip = !corner_ok[e];
+        unsigned pk[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
         for (int q = 0; q < 8; q++) {
           const int cell = corner_cell[MODE == kSphNormalize ? e : 0][q];
@@ -356,7 +367,10 @@ __global__ __launch_bounds__(NT) void vox_prep_kernel(
             if (word & bit) sg = pre_l[cell >> 5] + __popc(word & (bit - 1u));
           }
           D[i + (size_t)q * n] = sg;
+          pk[q >> 1] |= (unsigned)(sg >= 0 ? sg : n) << (16 * (q & 1));
         }
+        if (n <= 65535)
+          *(uint4*)(ws.dseg16 + ((size_t)b * n + i) * 4) = uint4{pk[0], pk[1], pk[2], pk[3]};
       }
     }
   }
@@ -824,6 +838,10 @@ __global__ __launch_bounds__(NT) void vox_means_kernel(
     }
     if (grp == 0) ws.segcnt[(size_t)b * ws.ms + si] = (unsigned short)(end - off);
   }
+  // the unused counts (slot n included) are 0, so the grid stream loads the
+  // row as it stands
+  if (grp == 0)
+    for (int si = nseg + tid; si < ws.ms; si += NT) ws.segcnt[(size_t)b * ws.ms + si] = 0;
   if (tid < gcount) mo[(size_t)tid * ws.ms + n] = 0.0f;  // the empty-cell slot
   lds_barrier();
 
@@ -982,8 +1000,8 @@ __global__ __launch_bounds__((NS + 1) * 64) void vox_stream_kernel(int c, int n,
   const int ms = ws.ms;
   float* mean_s = (float*)smem_raw;                                // [NB][BUFB / 4]
   unsigned* bm_s = (unsigned*)(smem_raw + NB * BUFB);              // [W]
-  unsigned short* pre_s = (unsigned short*)(bm_s + W);             // [W]
-  unsigned short* scnt_s = pre_s + W;                              // [ms -> 256 B], slot n = 0
+  unsigned short* pre_s = (unsigned short*)(bm_s + W);             // [W -> 256 B]
+  unsigned short* scnt_s = pre_s + (W + 127) / 128 * 128;          // [ms -> 256 B], slot n = 0
   (void)PCR_PRIO(5);
   const int b = blockIdx.x / wpc;
   const int j0 = (blockIdx.x % wpc) * per;
@@ -1007,40 +1025,31 @@ __global__ __launch_bounds__((NS + 1) * 64) void vox_stream_kernel(int c, int n,
     };
     // every load of the prologue in flight at once: the first two items'
     // means, the bitmap, the segment counts and nseg
+#ifdef PCR_DIAG
+    if (tid == NTS && PCR_WG_LINEAR < 1024) pcr_diag_stamps[PCR_WG_LINEAR][6] = __builtin_amdgcn_s_memtime();
+#endif
 #pragma unroll
     for (int q = 0; q < D; q++)
       if (q < nit) issue(j0 + q, q);
     {
-      // bitmap and segment counts by LDS-DMA too (4-byte pieces: 256 B per
-      // wave instruction), so the loader holds no staging registers
-      const char* gbm = (const char*)(ws.bitmap + (size_t)b * W);
-      for (int p = 0; p < W / 64; p++)
-        __builtin_amdgcn_global_load_lds((gbl_void_p)(gbm + p * 256 + lt * 4),
-                                         (lds_void_p)((char*)bm_s + p * 256), 4, 0, 0);
-      const char* gsc = (const char*)(ws.segcnt + (size_t)b * ms);
-      for (int p = 0; p < (ms * 2 + 255) / 256; p++)
-        __builtin_amdgcn_global_load_lds((gbl_void_p)(gsc + p * 256 + lt * 4),
-                                         (lds_void_p)((char*)scnt_s + p * 256), 4, 0, 0);
-      const int nseg = ws.nseg[b];
-      wait_vmcnt<0>();
-      // word prefix (u16) from the landed bitmap; unused counts -> 0 (slot n)
-      int carry = 0;
-      for (int q = 0; q < W / 64; q++) {
-        const int w = q * 64 + lt;
-        const unsigned v = bm_s[w];
-        const int pc = __popc(v);
-        int incl = pc;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-          const int o = __shfl_up(incl, off, kWave);
-          if (lt >= off) incl += o;
-        }
-        pre_s[w] = (unsigned short)(carry + incl - pc);
-        carry += __shfl(incl, 63, kWave);
-      }
-      for (int s2 = nseg + lt; s2 < ms; s2 += 64) scnt_s[s2] = 0;
+      // bitmap, its word prefix (prep's) and the segment counts (the means
+      // launch's, unused slots 0) by LDS-DMA too (4-byte pieces: 256 B per
+      // wave instruction), so the loader holds no staging registers and
+      // computes nothing before the first barrier (round 6: the word prefix
+      // was scanned here, 4 us of the launch's 8 us prologue)
+      auto dma4 = [&](void* dst, const void* src, int nbytes) {
+        for (int p = 0; p * 256 < nbytes; p++)
+          __builtin_amdgcn_global_load_lds((gbl_void_p)((const char*)src + p * 256 + lt * 4),
+                                           (lds_void_p)((char*)dst + p * 256), 4, 0, 0);
+      };
+      dma4(bm_s, ws.bitmap + (size_t)b * W, W * 4);
+      dma4(pre_s, ws.wpre16 + (size_t)b * W, W * 2);
+      dma4(scnt_s, ws.segcnt + (size_t)b * ms, ms * 2);
     }
-    wait_vmcnt<0>();  // the plain loads above already waited; keeps it simple
+    wait_vmcnt<0>();
+#ifdef PCR_DIAG
+    if (tid == NTS && PCR_WG_LINEAR < 1024) pcr_diag_stamps[PCR_WG_LINEAR][7] = __builtin_amdgcn_s_memtime();
+#endif
     lds_only_barrier();
     for (int it = 0; it < nit; it++) {
       // buffer (it + D) % NB held item it - 1, released by the last barrier;
@@ -1058,30 +1067,33 @@ __global__ __launch_bounds__((NS + 1) * 64) void vox_stream_kernel(int c, int n,
 
   // ---- streamer waves
   // DV: this thread's points i = tid + e NTS, their 8 corners' segments
-  // (empty corner -> slot n, whose mean is 0; two u16 per register) and
-  // weights, for every item
+  // (empty corner -> slot n, whose mean is 0; two u16 per register, prep's
+  // packed map: one 16-byte load per point) and weights, for every item.
+  // Issued after the first barrier (the loader's prologue loads go first)
+  // and waited for only at the first item's devox (round 6: the packing used
+  // to wait for them before the first barrier, so the launch's first grid
+  // stores waited behind 16 MB of corner loads)
   constexpr bool DV = DVN > 0;
   constexpr int PBS = DV ? DVN / NTS : 1;
+  lds_only_barrier();
   unsigned dsg[PBS][4];
   float dwt[PBS][8];
   __shared__ float dred_s[2][DV ? NS : 1][G];  // per-wave descriptor partials, by item parity
   if (DV) {
     const float* Wt = dwgts + (size_t)b * 8 * n;
-    const int* Dg = ws.dseg + (size_t)b * 8 * n;
+    const uint4* Dg = (const uint4*)(ws.dseg16 + (size_t)b * n * 4);
 #pragma unroll
     for (int e = 0; e < PBS; e++) {
       const int i = e * NTS + tid;
+      const uint4 v = i < n ? Dg[i] : uint4{0u, 0u, 0u, 0u};
+      dsg[e][0] = v.x;
+      dsg[e][1] = v.y;
+      dsg[e][2] = v.z;
+      dsg[e][3] = v.w;
 #pragma unroll
-      for (int q = 0; q < 4; q++) dsg[e][q] = 0u;
-#pragma unroll
-      for (int q = 0; q < 8; q++) {
-        dwt[e][q] = i < n ? Wt[i + (size_t)q * n] : 0.0f;
-        const int sg = i < n ? Dg[i + (size_t)q * n] : -1;
-        dsg[e][q >> 1] |= (unsigned)(sg >= 0 ? sg : n) << (16 * (q & 1));
-      }
+      for (int q = 0; q < 8; q++) dwt[e][q] = i < n ? Wt[i + (size_t)q * n] : 0.0f;
     }
   }
-  lds_only_barrier();
   PCR_STAMP(1);
   // the sweep starts at a workgroup-dependent step of the item and wraps, so
   // the workgroups do not all hit the same HBM channels at once
@@ -1099,6 +1111,7 @@ __global__ __launch_bounds__((NS + 1) * 64) void vox_stream_kernel(int c, int n,
       stream_cells<NTS, U, AUX, G>(sp * NTS * 4 * U + tid * 4, ob, gcount, ms0, cb, r3, n, ms,
                                    bm_s, pre_s, scnt_s);
     }
+    if (it < 4) PCR_STAMP(12 + it);
     if (DV) {
       // devox of the item's channels (vox_means_kernel's loop) + descriptor partials
       float vmax[G];
@@ -1142,6 +1155,14 @@ __global__ __launch_bounds__((NS + 1) * 64) void vox_stream_kernel(int c, int n,
       desc[(size_t)b * c + c0 + tid] = m;
     }
   }
+}
+
+// LDS of vox_stream_kernel: kStreamNB means buffers of NGP KB, the bitmap,
+// its u16 word prefix and the u16 segment counts (each in whole 256-byte
+// LDS-DMA pieces)
+static size_t stream_smem_bytes(int NGP, int W, int ms) {
+  return (size_t)kStreamNB * NGP * 1024 + (size_t)W * 4 + ((size_t)W * 2 + 255) / 256 * 256 +
+         ((size_t)ms * 2 + 255) / 256 * 256;
 }
 
 // ------------------------------------------------------ backward gather
@@ -2126,8 +2147,7 @@ extern "C" pcr_status pcr_extractor_voxel_stream(int b, int c, int n, int r, int
   if (wpc > ngrp) wpc = ngrp;
   const int per = ceil_div(ngrp, wpc);
   PCR_REQUIRE(ws.W % 64 == 0, "%s: r^3 %% 2048 != 0 unsupported", name);
-  const size_t smem = (size_t)kStreamNB * NGP * 1024 + (size_t)ws.W * 6 +
-                      ((size_t)ws.ms * 2 + 255) / 256 * 256;
+  const size_t smem = stream_smem_bytes(NGP, ws.W, ws.ms);
 #define PCR_LAUNCH_STREAM(NGV)                                                                 \
   do {                                                                                        \
     allow_big_lds(vox_stream_kernel<4, kStreamNB, 2, 16, G, NGV>, smem);                      \
@@ -2203,8 +2223,7 @@ extern "C" pcr_status pcr_extractor_voxel_stream_devox(int b, int c, int n, int 
   if (wpc < 1) wpc = 1;
   if (wpc > ngrp) wpc = ngrp;
   const int per = ceil_div(ngrp, wpc);
-  const size_t smem = (size_t)kStreamNB * NGP * 1024 + (size_t)ws.W * 6 +
-                      ((size_t)ws.ms * 2 + 255) / 256 * 256;
+  const size_t smem = stream_smem_bytes(NGP, ws.W, ws.ms);
   allow_big_lds(vox_stream_kernel<4, kStreamNB, 2, 16, G, kStreamNG, kStreamDvMaxN>, smem);
   hipLaunchKernelGGL((vox_stream_kernel<4, kStreamNB, 2, 16, G, kStreamNG, kStreamDvMaxN>),
                      dim3(b * wpc), dim3(5 * 64), smem, as_stream(stream), c, n, r3, ws, grid, cnt,

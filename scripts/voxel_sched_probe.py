@@ -1,7 +1,11 @@
 """Probe of the c2 voxel chain alone (no KNN chain): how fast can the voxel
 side go, and how do two grid streams share HBM?  At BASELINE c2 (32 x 1024,
 C = 64, r = 32), HIP events on the caller's stream around S steps:
-  one     one grid stream launch (pcr_extractor_voxel_stream_devox) at a time
+  one     one grid stream launch (pcr_extractor_voxel_stream_devox) at a time,
+          NB output sets in turn (no Infinity-Cache reuse of the grid lines)
+  onenodv the same without the devox role (pcr_extractor_voxel_stream; the
+          devox then comes from the means launch, not timed here)
+  same    one grid stream launch at a time into the SAME output set
   two     two grid stream launches at once, on two streams
   sched6  the runner's voxel chains only: prep -> means -> stream of step s on
           queue s % 2 with workspace s % 2 (schedule 6 without the KNN chain)
@@ -89,7 +93,20 @@ torch.cuda.synchronize()
 
 def one():
     for s in range(S):
-        stream(s % 2, s % 2, q[0].cuda_stream)
+        stream(s % NB, s % 2, q[0].cuda_stream)
+
+
+def onenodv():
+    for s in range(S):
+        i = s % NB
+        _lib.check(lib.pcr_extractor_voxel_stream(b, c, n, r, _ptr(cnt[i]), _ptr(grid[i]),
+                                                  _ptr(ws[s % 2]), wsb, q[0].cuda_stream),
+                   "stream")
+
+
+def same():
+    for s in range(S):
+        stream(0, 0, q[0].cuda_stream)
 
 
 def two():
@@ -128,7 +145,8 @@ def split():
             done[t % 2] = ev
 
 
-for name, fn in (("one", one), ("two", two), ("sched6", sched6), ("split", split)):
+for name, fn in (("one", one), ("onenodv", onenodv), ("same", same), ("two", two),
+                 ("sched6", sched6)):
     fn()  # warm-up
     t = timed(fn)
     print("%-7s %7.1f us per step  (%.2f TB/s of grid + cnt + devox stream bytes)" % (
