@@ -73,6 +73,7 @@ class SphExtractor:
         self._vsep, self._vset1 = False, None
         self._ppf1 = None
         self._args, self._args_key = None, None
+        self._ring_seen = None  # (batch tuples, match, args key) of the last run_ring
 
     # ---------------------------------------------------------------- stages
     # Buffers a later stage of the same step reads (the two workspaces and the
@@ -711,15 +712,25 @@ class SphExtractor:
         R = len(batches)
         if R < 1:
             raise RuntimeError("run_ring needs at least one batch")
-        for t in batches:
-            self._check_inputs(*t)
         mp = match.pairs if match is not None else 0
         ring = self.ring_outputs(R, mp)
         ntimed = min(steps, (steps if timed is True else int(timed)) if timed else 0)
         runner = self._get_runner(ntimed)
         if self._runner_cap:
             _lib.check(_lib.load().pcr_runner_set_timed(runner, ntimed), "runner_set_timed")
-        key = ("ring", tuple(tuple(x.data_ptr() for x in t) for t in batches), match)
+        # the same batch tuples as the last call (tuples are immutable, so
+        # the same tensors): checked and keyed then.  Checking 20 batches
+        # and keying their pointers cost ~23 us of host time in front of
+        # the first launch (scripts/host_enqueue_probe.py)
+        prev = self._ring_seen
+        if prev is not None and len(prev[0]) == R and prev[1] is match and \
+                all(t is u for t, u in zip(batches, prev[0])):
+            key = prev[2]
+        else:
+            for t in batches:
+                self._check_inputs(*t)
+            key = ("ring", tuple(tuple(x.data_ptr() for x in t) for t in batches), match)
+            self._ring_seen = (tuple(batches), match, key)
         if self._args_key != key:
             a = self._make_args(*batches[0], match)
             sets = (_lib.ExtractorSet * R)()

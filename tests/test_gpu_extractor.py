@@ -141,6 +141,30 @@ def test_extractor_runner_batch_ring(dev, schedule):
         set0 = (set0 + steps) % 3
 
 
+def test_extractor_runner_ring_list_mutated(dev):
+    """run_ring skips re-checking a call's batch tuples when they are the
+    ones of the previous call; a tuple replaced in the SAME list object is
+    checked and keyed again: its set then holds the new batch's outputs, and
+    a replacement of the wrong shape is refused."""
+    from pcr_amd.extractor import SphExtractor
+    b, n, c, k, r = 4, 1024, 16, 32, 32
+    batches = [gaussian_clouds(b, n, seed=140 + i, c=c) for i in range(4)]
+    tb = [tuple(T(a, dev) for a in bt) for bt in batches[:3]]
+    ex = SphExtractor(b, n, c, k, r, device=dev)
+    ring = ex.ring_outputs(3)
+    ex.run_ring(tb, 3, 0, schedule=6)
+    ex.run_ring(tb, 3, 0, schedule=6)  # the cached path
+    tb[1] = tuple(T(a, dev) for a in batches[3])
+    ex.run_ring(tb, 3, 0, schedule=6)
+    torch.cuda.synchronize()
+    exp = expected_step(*batches[3], k, r)
+    for key in ("knn_idx", "ind", "cnt", "grid", "devox"):
+        assert np.array_equal(N(ring[1][key]), exp[key]), key
+    tb[2] = (tb[2][0][:, :, :512].contiguous(), tb[2][1], tb[2][2])
+    with pytest.raises(RuntimeError):
+        ex.run_ring(tb, 3, 0, schedule=6)
+
+
 @pytest.mark.parametrize("schedule,rings", [(6, ((2, 5), (5, 7))), (7, ((3, 7), (4, 9)))])
 def test_extractor_runner_multi_queue_rings(dev, schedule, rings):
     """Schedules 6 (two voxel + two KNN queues) and 7 (three voxel + one
