@@ -35,6 +35,7 @@ bounded sample of the same workload on this box's host cores.
 """
 import argparse
 import json
+import math
 import os
 import socket
 import subprocess
@@ -86,6 +87,12 @@ def parse(argv=None):
                          "6 (extract), 7 (pairs: the matching lengthens the voxel chain)")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="diagnostic: no timing events around the dominant kernel")
+    ap.add_argument("--settle-ms", type=float, default=50.0,
+                    help="untimed calls of the timed call's shape (min(steps, "
+                         "steps-per-launch) steps each, synchronized) for at least this long "
+                         "after the output check and before the warm-up: a short timed region "
+                         "right after the GPU idled measures its ramp, not the steady state "
+                         "(DESIGN.md 4.9, scripts/first_call_probe.py); 0 = off")
     ap.add_argument("--no-verify", action="store_true",
                     help="diagnostic: skip the output check before the warm-up")
     ap.add_argument("--c3-schedule", choices=("pipelined", "pipelined-nbr", "serial"),
@@ -829,6 +836,35 @@ WORKLOADS = {"extract": ExtractWorkload, "pairs": ExtractWorkload, "c3": C3Workl
              "c5": C5Workload}
 
 
+def settle_runs(wl, args, dev):
+    """Untimed runner calls of the timed call's shape, each synchronized as
+    the timed one is, for at least --settle-ms: after the output check the
+    GPU has idled, and the first short calls after an idle run 3-5% slower
+    than the same call repeated (20-step c2 calls: 1.55-1.64 ms for the
+    first, 1.48-1.51 ms from the fourth on; an idle of 0.5 s brings the slow
+    calls back; scripts/first_call_probe.py).  The W warm-up steps and the
+    K timed steps are unchanged."""
+    if args.settle_ms <= 0:
+        return None
+    m = min(args.steps, args.steps_per_launch) if args.workload in ("extract", "pairs") \
+        else args.steps
+    m = max(1, m)
+    t0 = time.perf_counter()
+    wl.run(m, timed=False)
+    torch.cuda.synchronize(dev)
+    # the same number of calls on every rank (the calls all-gather)
+    calls = max(1, math.ceil(args.settle_ms / ((time.perf_counter() - t0) * 1e3)))
+    if dist.is_available() and dist.is_initialized():
+        t = torch.tensor([calls], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        calls = int(t.item())
+    for _ in range(calls - 1):
+        wl.run(m, timed=False)
+        torch.cuda.synchronize(dev)
+    return {"ms": round((time.perf_counter() - t0) * 1e3, 1), "calls": calls,
+            "steps_per_call": m}
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse(argv)
@@ -856,6 +892,7 @@ def main(argv=None):
     # (extract / pairs: runner vs single-step path, every output poisoned
     # first), which also brings the GPU up to clock
     verified = False if args.no_verify else wl.verify()
+    settle = settle_runs(wl, args, dev)
     wl.run(args.warmup, timed=False)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -905,6 +942,7 @@ def main(argv=None):
         "dtype": "f32",
         "data": "synthetic (seeded gaussian clouds, unit normals, U(-1,1) features)",
         "outputs_verified": verified,
+        "settle": settle,
         "config": wl.config(),
         "roofline": {"bound": "hbm", "achieved": round(step_gbs, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(step_gbs / HBM_PEAK_GBS, 4),
