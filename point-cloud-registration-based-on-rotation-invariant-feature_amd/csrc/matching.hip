@@ -18,37 +18,6 @@ namespace pcr {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-// |f|^2 per row (pcr_match_sqnorm: the sequential fmaf chain); one thread per row
-__global__ __launch_bounds__(256) void match_sqnorm_kernel(const float* __restrict__ f, int rows,
-                                                           int c, float* __restrict__ sq) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= rows) return;
-  sq[i] = pcr_match_sqnorm(f + i * c, c);
-}
-
-// the same chain over channel-major features [p][c][n] (the extractor's
-// per-point feature layout): consecutive threads read consecutive points
-__global__ __launch_bounds__(256) void match_sqnorm_cm_kernel(const float* __restrict__ f, int n,
-                                                              int c, float* __restrict__ sq) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const int p = blockIdx.y;
-  if (i >= n) return;
-  const float* col = f + (size_t)p * c * n + i;
-  float s = 0.0f;
-  int k = 0;
-  // 16 loads in flight before the (ordered) chain consumes them
-  for (; k + 16 <= c; k += 16) {
-    float v[16];
-#pragma unroll
-    for (int e = 0; e < 16; e++) v[e] = col[(size_t)(k + e) * n];
-#pragma unroll
-    for (int e = 0; e < 16; e++) s = __builtin_fmaf(v[e], v[e], s);
-  }
-  for (; k < c; k++) s = __builtin_fmaf(col[(size_t)k * n], col[(size_t)k * n], s);
-  const float r = __builtin_sqrtf(s);
-  sq[(size_t)p * n + i] = r * r;  // pcr_match_sqnorm
-}
-
 constexpr int kMT = 128;  // tile rows (f1) and columns (f2)
 // channels per LDS stage: 16 (two double-buffered stages of A and B take
 // 34 KB, four workgroups per CU) measured 0.417 -> 0.350 ms at c4 (128 pairs
@@ -202,7 +171,6 @@ __device__ inline void match_epilogue(const f32x16 (&acc)[2][2], const float (&s
 template <bool CM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void match_tile_kernel(
     const float* __restrict__ f1, const float* __restrict__ f2, int n1, int n2, int c,
-    const float* __restrict__ sq1, const float* __restrict__ sq2,
     unsigned long long* __restrict__ rowbest, unsigned long long* __restrict__ colbest) {
   __shared__ float a_s[2][kKC][kMPad];  // [buf][k][i]
   __shared__ float b_s[2][kKC][kMPad];  // [buf][k][j]
@@ -211,15 +179,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void m
   const int i0 = blockIdx.y * kMT, j0 = blockIdx.x * kMT;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wi = wv >> 1, wj = wv & 1;  // 2 x 2 waves, 64 x 64 each
-  // the norms the epilogue reads, staged with the first stage (they used to
-  // be 34 dependent global loads per lane inside the epilogue)
-  if (tid < kMT) {
-    const int row = i0 + tid;
-    sq_s[0][tid] = row < n1 ? sq1[(size_t)p * n1 + row] : 0.0f;
-  } else {
-    const int col = j0 + tid - kMT;
-    sq_s[1][tid - kMT] = col < n2 ? sq2[(size_t)p * n2 + col] : 0.0f;
-  }
+  // the norms the epilogue reads: thread t runs pcr_match_sqnorm's ordered
+  // fmaf chain for row t of A (t < kMT) or row t - kMT of B over the channels
+  // as each stage lands in LDS (zero padding adds exact zeros), so no norm
+  // launches and no norm loads (pairs step: two launches fewer)
+  float nrm = 0.0f;
+  const float* const nrow = tid < kMT ? &a_s[0][0][tid] : &b_s[0][0][tid - kMT];
   const float* A = f1 + (size_t)p * n1 * c;
   const float* B = f2 + (size_t)p * n2 * c;
   f32x16 acc[2][2];
@@ -264,7 +229,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void m
         for (int tj = 0; tj < 2; tj++)
           acc[ti][tj] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[ti], bq[tj], acc[ti][tj], 0, 0, 0);
     }
+    const float* col = nrow + buf * kKC * kMPad;  // a_s / b_s [buf][0][row]
+#pragma unroll
+    for (int e = 0; e < kKC; e++) {
+      const float v = col[e * kMPad];
+      nrm = __builtin_fmaf(v, v, nrm);
+    }
   }
+  {
+    const float r = __builtin_sqrtf(nrm);  // pcr_match_sqnorm: sqrt of the sum, squared
+    sq_s[tid < kMT ? 0 : 1][tid & (kMT - 1)] = r * r;
+  }
+  lds_barrier();
   // epilogue: C/D layout col = lane & 31, row = (v & 3) + 8 (v >> 2) + 4 (lane >> 5)
   match_epilogue(acc, sq_s, i0, j0, wi, wj, lane, n1, n2, rowbest + (size_t)p * n1,
                  colbest + (size_t)p * n2);
@@ -307,21 +283,17 @@ __global__ __launch_bounds__(1024) void match_finalize_kernel(
   if (tid == 0) count[p] = base;
 }
 
-static size_t match_ws_layout(int p, int n1, int n2, float** sq1, float** sq2,
-                              unsigned long long** rb, unsigned long long** cb, char* base) {
+static size_t match_ws_layout(int p, int n1, int n2, unsigned long long** rb,
+                              unsigned long long** cb, char* base) {
   size_t off = 0;
   auto take = [&](size_t bytes) {
     char* q = base ? base + off : nullptr;
     off = (off + bytes + 255) / 256 * 256;
     return q;
   };
-  float* a = (float*)take((size_t)p * n1 * 4);
-  float* b = (float*)take((size_t)p * n2 * 4);
   unsigned long long* r = (unsigned long long*)take((size_t)p * n1 * 8);
   unsigned long long* c = (unsigned long long*)take((size_t)p * n2 * 8);
-  if (sq1) {
-    *sq1 = a;
-    *sq2 = b;
+  if (rb) {
     *rb = r;
     *cb = c;
   }
@@ -334,7 +306,7 @@ using namespace pcr;
 
 extern "C" size_t pcr_mutual_nn_workspace_size(int p, int n1, int n2) {
   if (p <= 0 || n1 <= 0 || n2 <= 0) return 256;
-  return match_ws_layout(p, n1, n2, nullptr, nullptr, nullptr, nullptr, nullptr);
+  return match_ws_layout(p, n1, n2, nullptr, nullptr, nullptr);
 }
 
 static pcr_status mutual_nn(bool cm, const float* f1, const float* f2, int p, int n1, int n2,
@@ -344,30 +316,20 @@ static pcr_status mutual_nn(bool cm, const float* f1, const float* f2, int p, in
   PCR_REQUIRE(p >= 0 && n1 >= 1 && n2 >= 1 && c >= 1, "%s: invalid sizes", name);
   PCR_REQUIRE(p <= 65535, "%s: too many pairs (%d)", name, p);
   if (p == 0) return PCR_OK;
-  float *sq1, *sq2;
   unsigned long long *rb, *cb;
-  const size_t need = match_ws_layout(p, n1, n2, &sq1, &sq2, &rb, &cb, (char*)workspace);
+  const size_t need = match_ws_layout(p, n1, n2, &rb, &cb, (char*)workspace);
   PCR_REQUIRE(workspace != nullptr && workspace_bytes >= need,
               "%s: workspace too small (%zu < %zu)", name, workspace_bytes, need);
   hipStream_t st = as_stream(stream);
-  if (hipMemsetAsync(rb, 0xFF, (size_t)p * n1 * 8, st) != hipSuccess ||
-      hipMemsetAsync(cb, 0xFF, (size_t)p * n2 * 8, st) != hipSuccess)
+  // the row and column minima are adjacent in the workspace: one fill
+  if (hipMemsetAsync(rb, 0xFF, (size_t)((char*)(cb + (size_t)p * n2) - (char*)rb), st) !=
+      hipSuccess)
     return launch_status(name);
-  if (cm) {
-    hipLaunchKernelGGL(match_sqnorm_cm_kernel, dim3(ceil_div(n1, 256), p), dim3(256), 0, st, f1,
-                       n1, c, sq1);
-    hipLaunchKernelGGL(match_sqnorm_cm_kernel, dim3(ceil_div(n2, 256), p), dim3(256), 0, st, f2,
-                       n2, c, sq2);
-    hipLaunchKernelGGL(match_tile_kernel<true>, dim3(ceil_div(n2, kMT), ceil_div(n1, kMT), p),
-                       dim3(256), 0, st, f1, f2, n1, n2, c, sq1, sq2, rb, cb);
-  } else {
-    hipLaunchKernelGGL(match_sqnorm_kernel, dim3((unsigned)ceil_div64((int64_t)p * n1, 256)),
-                       dim3(256), 0, st, f1, p * n1, c, sq1);
-    hipLaunchKernelGGL(match_sqnorm_kernel, dim3((unsigned)ceil_div64((int64_t)p * n2, 256)),
-                       dim3(256), 0, st, f2, p * n2, c, sq2);
-    hipLaunchKernelGGL(match_tile_kernel<false>, dim3(ceil_div(n2, kMT), ceil_div(n1, kMT), p),
-                       dim3(256), 0, st, f1, f2, n1, n2, c, sq1, sq2, rb, cb);
-  }
+  const dim3 grid(ceil_div(n2, kMT), ceil_div(n1, kMT), p);
+  if (cm)
+    hipLaunchKernelGGL(match_tile_kernel<true>, grid, dim3(256), 0, st, f1, f2, n1, n2, c, rb, cb);
+  else
+    hipLaunchKernelGGL(match_tile_kernel<false>, grid, dim3(256), 0, st, f1, f2, n1, n2, c, rb, cb);
   hipLaunchKernelGGL(match_finalize_kernel, dim3(p), dim3(1024), 0, st, rb, cb, n1, n2, corr12,
                      corr21, idx1, idx2, count);
   return launch_status(name);
