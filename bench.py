@@ -83,8 +83,7 @@ def parse(argv=None):
                     help="pcr_extractor_run schedule (include/pcr_amd.h): 6 = two "
                          "independent pipelines per chain (voxel chain on s_vox / origin, KNN "
                          "chain on s_nbr / s_pre by step parity), no cross-queue events, 7 = as 6 "
-                         "with three voxel queues (s_vox / origin / s_pre) and one KNN queue; default "
-                         "6 (extract), 7 (pairs: the matching lengthens the voxel chain)")
+                         "with three voxel queues (s_vox / origin / s_pre) and one KNN queue; default 6")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="diagnostic: no timing events around the dominant kernel")
     ap.add_argument("--settle-ms", type=float, default=50.0,
@@ -132,10 +131,12 @@ def parse(argv=None):
     if args.batches is None:
         args.batches = {"pairs": 8, "c3": 4}.get(args.workload, 20)
     if args.schedule is None:
-        # pairs: 250.5k vs 234.3k clouds/s with schedule 7 (the matching
-        # lengthens the voxel chain); extract: 381-395k with 6 against
-        # 305-319k with 7 (one KNN queue is then the critical chain)
-        args.schedule = 7 if args.workload == "pairs" else 6
+        # extract: 381-395k with 6 against 305-319k with 7 (one KNN queue
+        # is then the critical chain).  pairs: 7 while the matching was six
+        # launches (250.5k vs 234.3k in round 4); with the norms in the tile
+        # kernel 6 is ahead, 316.7-321.8k vs 313.4-314.9k (three interleaved
+        # rounds, profiles/r06_pairs_schedule.log)
+        args.schedule = 6
     if args.batches < 1:
         ap.error("--batches must be >= 1")
     if args.schedule >= 6 and args.batches < args.schedule - 4 and \

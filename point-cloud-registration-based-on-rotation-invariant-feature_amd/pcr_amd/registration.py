@@ -83,7 +83,7 @@ class PairExtractor:
         out.update(self.match.outputs())
         return out
 
-    def run_ring(self, batches, steps, set0=0, desc_steps=None, schedule=7, timed=False):
+    def run_ring(self, batches, steps, set0=0, desc_steps=None, schedule=6, timed=False):
         """`steps` pipelined steps of extraction + matching over a batch ring
         of packed [2P, ...] batches (SphExtractor.run_ring): step s matches
         the pairs of batches[(set0 + s) % R] into that ring set's corr12 /
