@@ -341,11 +341,10 @@ class ExtractWorkload:
             # matching: both clouds' [C, N] features read, corr12 / corr21 /
             # idx1 / idx2 written (4 x 4N), per pair
             self.step_bytes += (2 * 4 * c * n + 16 * n) * (b // 2)
-        # the c2 extractor's grid stream also writes devox + descriptor
-        # (pcr_extractor_voxel_stream_devox; pairs keep them in the means)
+        # the grid stream also writes devox + descriptor at c2-sized clouds
+        # (pcr_extractor_voxel_stream_devox; pairs too since round 6)
         from pcr_amd import _lib
-        self.stream_devox = args.workload == "extract" and bool(
-            _lib.load().pcr_extractor_stream_devox_ok(n, c, r))
+        self.stream_devox = bool(_lib.load().pcr_extractor_stream_devox_ok(n, c, r))
         self.kernel_bytes = stream_kernel_bytes_per_cloud(
             r, c, n if self.stream_devox else None) * b
         # grid launches bracketed with timing events in the timed call (each

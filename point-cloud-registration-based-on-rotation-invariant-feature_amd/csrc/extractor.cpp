@@ -336,11 +336,11 @@ extern "C" pcr_status pcr_extractor_run(pcr_runner* runner, const pcr_extractor_
       // c2-sized clouds: the devox + descriptor ride in the grid stream (its
       // means are in LDS there), so the means launch reads no corner data
       // (c2 390k -> 405-408k clouds/s).  With pair matching, which reads the
-      // devox, the means launch keeps it and the matching runs before the
-      // stream (pairs: 274k against 266k with the matching behind the
-      // stream, profiles/r05_ab_stream_devox.log)
-      const bool dv = !a->devox_in_means && a->match_pairs <= 0 &&
-                      pcr_extractor_stream_devox_ok(a->n, a->c, a->r);
+      // devox, the matching then runs behind the stream on the same queue:
+      // since round 6 (matching of four launches, schedule 6) 337-343k
+      // against 326-330k clouds/s with the devox in the means launch and the
+      // matching ahead of the stream (profiles/r06_ab_pairs_stream_devox.log)
+      const bool dv = !a->devox_in_means && pcr_extractor_stream_devox_ok(a->n, a->c, a->r);
       if (dv)
         PCR_TRY(pcr_extractor_voxel_means(io.features, a->b, a->c, a->n, a->r, vw6,
                                           a->vox_ws_bytes, vq));

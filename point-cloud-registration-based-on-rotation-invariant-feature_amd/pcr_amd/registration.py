@@ -17,7 +17,8 @@ one step of a rank's shard of P pairs is:
     collective.
 
 The native runner (pcr_extractor_run with match_pairs = P) enqueues the
-matching on the prep stream right after each step's devox, so S steps of
+matching on each step's voxel queue right after its devox (behind the grid
+stream, which evaluates the devox at c2-sized clouds), so S steps of
 extraction + matching cost one host call.
 """
 import torch
