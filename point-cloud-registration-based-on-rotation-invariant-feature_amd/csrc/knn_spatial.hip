@@ -1602,7 +1602,12 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
 // sidx rows, like knn_select_kernel's sorted_emit 1) through an LDS tile, so
 // every store is a whole 256-byte row.
 constexpr int kWselChunk = 2;  // consecutive queries a wave takes at a time
-constexpr int kWselWaves = 8;  // waves per workgroup: one 64-query block
+// waves per workgroup (one 64-query block): 12 rather than 8 -- the
+// compiler then fits the kernel in 81 VGPRs instead of 91 and the waves take
+// ~5 queries each; c2 +1% (seven interleaved rounds on two boxes at 200 and
+// 20 steps, profiles/r06_ab_wsel_waves.log); 10 was slower, 14 and 16 spill
+// SGPRs (-12%)
+constexpr int kWselWaves = 12;
 constexpr int kWselCap = 64;   // keys collected per query (one per lane)
 constexpr int kWselTmax = 0x461C3FFF;  // bits of the largest float below 10000
 
@@ -1733,7 +1738,7 @@ __device__ inline unsigned long long wsel_sort64_exact(unsigned long long x, int
 }
 
 // Appends the keys of the lanes in `m` (a ballot mask) to the wave's LDS
-// rows at slots base, base + 1, ...: d bits to kd, index to kd + 2048 bytes.
+// rows at slots base, base + 1, ...: d bits to kd, index to kd + 256 bytes.
 // exec = m for three VALU (the slot: mbcnt lo / hi; the address) and two
 // ds_write, restored after: no per-lane condition is materialised.
 __device__ inline void wsel_append(unsigned long long m, unsigned addr, unsigned d, int j) {
@@ -1746,7 +1751,7 @@ __device__ inline void wsel_append(unsigned long long m, unsigned addr, unsigned
       "v_mbcnt_hi_u32_b32 %0, %4, %0\n\t"
       "v_lshl_add_u32 %0, %0, 2, %5\n\t"
       "ds_write_b32 %0, %6\n\t"
-      "ds_write_b32 %0, %7 offset:2048\n\t"
+      "ds_write_b32 %0, %7 offset:256\n\t"
       "s_mov_b64 exec, %1"
       : "=&v"(t), "=&s"(save)
       : "s"(m), "s"((unsigned)m), "s"((unsigned)(m >> 32)), "s"(addr), "v"(d), "v"(j)
@@ -1755,13 +1760,13 @@ __device__ inline void wsel_append(unsigned long long m, unsigned addr, unsigned
 
 template <int R>
 __global__ __launch_bounds__(kWselWaves * 64) void knn_wsel_kernel(KnnSet s, int k) {
-  // [0][wave][slot] collected d bits, [1][wave][slot] their sorted positions
-  // (2048 bytes apart: wsel_append's ds_write offset)
-  __shared__ unsigned kbuf_s[2][kWselWaves][kWselCap];
+  // [wave][0][slot] collected d bits, [wave][1][slot] their sorted positions
+  // (256 bytes apart: wsel_append's ds_write offset)
+  __shared__ unsigned kbuf_s[kWselWaves][2][kWselCap];
   __shared__ int tile_s[kBlk][kSortedK + 1];  // output ids [query][slot] (padded: no bank conflicts)
   __shared__ int qnext_s;                     // the next chunk of the block's queries
   __shared__ int cj_s[R * kBlk];              // original index of each sorted position
-  static_assert(sizeof(kbuf_s[0]) == 2048, "wsel_append's offset");
+  static_assert(sizeof(kbuf_s[0][0]) == 256, "wsel_append's offset");
   const int b = blockIdx.y, qblk = blockIdx.x;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -1820,8 +1825,8 @@ __global__ __launch_bounds__(kWselWaves * 64) void knn_wsel_kernel(KnnSet s, int
       if (u < PCR_KNN_UNDEF) tb = (int)__float_as_uint(u);
     }
   }
-  unsigned* kd = kbuf_s[0][wv];
-  int* kj = (int*)kbuf_s[1][wv];
+  unsigned* kd = kbuf_s[wv][0];
+  int* kj = (int*)kbuf_s[wv][1];
   const unsigned kd_addr =  // LDS byte address of the wave's rows
       (unsigned)(uintptr_t)((__attribute__((address_space(3))) unsigned*)kd);
   const float tgt = 0.5f * (float)(k + kWselCap);
