@@ -1601,7 +1601,10 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
 // (knn.cu:24-46).  Written as neighbour ids in sorted query order (KnnSet::
 // sidx rows, like knn_select_kernel's sorted_emit 1) through an LDS tile, so
 // every store is a whole 256-byte row.
-constexpr int kWselChunk = 2;  // consecutive queries a wave takes at a time
+// consecutive queries a wave takes at a time: 1 (with 12 waves) rather than
+// 2, c2 +0.8% over ten interleaved rounds (profiles/r06_ab_wsel_chunk.log);
+// 3 / 4 -2%
+constexpr int kWselChunk = 1;
 // waves per workgroup (one 64-query block): 12 rather than 8 -- the
 // compiler then fits the kernel in 81 VGPRs instead of 91 and the waves take
 // ~5 queries each; c2 +1% (seven interleaved rounds on two boxes at 200 and
