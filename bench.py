@@ -109,9 +109,12 @@ def parse(argv=None):
     ap.add_argument("--c3-cu-split", type=float, default=0.0,
                     help="c3 diagnostic: run the neighbour stream on this fraction of the CUs "
                          "and the caller's chain on the rest (CU-masked HIP streams); 0 = off")
-    ap.add_argument("--steps-per-launch", type=int, default=40,
+    ap.add_argument("--steps-per-launch", type=int, default=200,
                     help="most pipelined steps per native runner call (extract / pairs); "
-                         "--steps and --warmup are split into calls of at most this many")
+                         "--steps and --warmup are split into calls of at most this many "
+                         "(each call ends in a join of the runner's queues, so its pipeline "
+                         "drains: 200 steps as one call 442-447k against 427-431k clouds/s "
+                         "as five of 40, profiles/r06_steps_per_launch.log)")
     ap.add_argument("--batches", type=int, default=None,
                     help="distinct input batches cycled through the timed steps (extract / "
                          "pairs: the runner's batch ring, each batch with its own output set; "
