@@ -1601,16 +1601,17 @@ __global__ __launch_bounds__(NW * 64) void knn_select_kernel(
 // (knn.cu:24-46).  Written as neighbour ids in sorted query order (KnnSet::
 // sidx rows, like knn_select_kernel's sorted_emit 1) through an LDS tile, so
 // every store is a whole 256-byte row.
-// consecutive queries a wave takes at a time: 1 (with 12 waves) rather than
-// 2, c2 +0.8% over ten interleaved rounds (profiles/r06_ab_wsel_chunk.log);
-// 3 / 4 -2%
-constexpr int kWselChunk = 1;
-// waves per workgroup (one 64-query block): 12 rather than 8 -- the
-// compiler then fits the kernel in 81 VGPRs instead of 91 and the waves take
-// ~5 queries each; c2 +1% (seven interleaved rounds on two boxes at 200 and
-// 20 steps, profiles/r06_ab_wsel_waves.log); 10 was slower, 14 and 16 spill
-// SGPRs (-12%)
-constexpr int kWselWaves = 12;
+// Waves per workgroup (one 64-query block), W, and the queries a wave takes
+// from the block's counter at a time, wsel_chunk<W>.  A launch of at most
+// 4096 waves at W = 8 (c2: 32 clouds x 16 blocks) leaves 4 waves per SIMD:
+// there W = 12 (the compiler then fits the kernel in 81 VGPRs instead of 91)
+// taking one query at a time, c2 +1.7% (profiles/r06_ab_wsel_waves.log,
+// r06_ab_wsel_chunk.log, r06_ab_wsel_pairs_waves.log; 10 waves -3%, 14 / 16
+// spill SGPRs, -12%).  Larger launches (pairs: 256 clouds) keep W = 8 with
+// two queries at a time: each wave stages the whole cloud in registers, and
+// 12 waves cost pairs 9% (312-315k against 341-343k clouds/s).
+template <int W>
+constexpr int wsel_chunk() { return W == 8 ? 2 : 1; }
 constexpr int kWselCap = 64;   // keys collected per query (one per lane)
 constexpr int kWselTmax = 0x461C3FFF;  // bits of the largest float below 10000
 
@@ -1761,8 +1762,10 @@ __device__ inline void wsel_append(unsigned long long m, unsigned addr, unsigned
       : "memory");
 }
 
-template <int R>
-__global__ __launch_bounds__(kWselWaves * 64) void knn_wsel_kernel(KnnSet s, int k) {
+template <int R, int W>
+__global__ __launch_bounds__(W * 64) void knn_wsel_kernel(KnnSet s, int k) {
+  constexpr int kWselWaves = W;
+  constexpr int kWselChunk = wsel_chunk<W>();
   // [wave][0][slot] collected d bits, [wave][1][slot] their sorted positions
   // (256 bytes apart: wsel_append's ds_write offset)
   __shared__ unsigned kbuf_s[kWselWaves][2][kWselCap];
@@ -2238,8 +2241,12 @@ pcr_status knn_spatial(const float* xyz1, const float* xyz2, int b, int n, int m
     // registers per coordinate leave 2 waves per SIMD and it lost (928 us
     // against 600 at c3), so those keep the per-lane kernel.
     if (s1.npad <= 16 * kBlk) {
-      hipLaunchKernelGGL((knn_wsel_kernel<16>), dim3(s1.nblk, b), dim3(kWselWaves * 64), 0, st,
-                         s1, k);
+      if ((size_t)s1.nblk * b * 8 <= 4096)
+        hipLaunchKernelGGL((knn_wsel_kernel<16, 12>), dim3(s1.nblk, b), dim3(12 * 64), 0, st, s1,
+                           k);
+      else
+        hipLaunchKernelGGL((knn_wsel_kernel<16, 8>), dim3(s1.nblk, b), dim3(8 * 64), 0, st, s1,
+                           k);
       return PCR_OK;
     }
     return launch_block<false>(s1, c1, b, k, nullptr, idx1, nullptr, nullptr, nullptr, nullptr,
