@@ -1233,13 +1233,15 @@ extern "C" pcr_status pcr_knn_ppf_sorted(const float* xyz, const float* normals,
   PCR_REQUIRE(workspace != nullptr && workspace_bytes >= pcr_knn_workspace_size(b, n, n) &&
                   knn_sorted_views(const_cast<void*>(workspace), b, n, &sidx, &inv, &npad),
               "knn_ppf_sorted: workspace without sorted neighbour rows");
-  // clouds of <= 1024 points: one workgroup per (cloud, 4 slots, 512
-  // points), a thread per point, so a c2 launch has 4096 waves to hide the
-  // staging and the LDS gathers behind each other's arithmetic (13.9 ->
-  // 13.0 us alone).  At 2048 points every workgroup already has 4 points per
-  // thread, and splitting it re-stages the 48 KB cloud per range (c3: 100 ->
-  // 160 us), so those keep one workgroup per (cloud, 4 slots).
-  constexpr int SL = 4;
+  // clouds of <= 1024 points: one workgroup per (cloud, 2 slots, 512
+  // points), 256 threads of four points each (round 6: 2 slots x 256 threads
+  // rather than 4 x 512, twice the workgroups -- c2 +0.5%, pairs +2%, c3
+  // within noise, profiles/r06_ab_ppf_shape.log; 4 slots over 256-point
+  // ranges was slower).  At 2048 points splitting a workgroup's points
+  // re-stages the 48 KB cloud per range (c3: 100 -> 160 us), so those keep
+  // one workgroup per (cloud, 2 slots).
+  constexpr int SL = 2;
+  constexpr int NT = 256;
   const int pr = n <= 1024 ? ceil_div(n, 512) : 1;
   // 16-byte LDS-DMA pieces and output vectors when every row is 16-byte
   // aligned: four points per thread (local_ppf_quad_kernel)
@@ -1249,8 +1251,8 @@ extern "C" pcr_status pcr_knn_ppf_sorted(const float* xyz, const float* normals,
   const dim3 grid(b * ceil_div(k, SL) * pr);
   if (v16) {
     const size_t lds = ppf_lds_layout(n, SL, npad, 16).bytes;
-    allow_big_lds(local_ppf_quad_kernel<SL>, lds);
-    hipLaunchKernelGGL((local_ppf_quad_kernel<SL>), grid, dim3(512), lds, as_stream(stream),
+    allow_big_lds(local_ppf_quad_kernel<SL, NT>, lds);
+    hipLaunchKernelGGL((local_ppf_quad_kernel<SL, NT>), grid, dim3(NT), lds, as_stream(stream),
                        xyz, normals, n, k, relative, ppf, sidx, inv, npad, idx, pr);
   } else {
     const size_t lds = ppf_lds_layout(n, SL, npad, 4).bytes;
