@@ -1091,8 +1091,12 @@ static pcr_status devox_backward(const float* grad_y, const int* inds, const flo
   PCR_REQUIRE(r3l < (1ll << 31) / 64, "devoxelize_backward: resolution too large");
   if (b == 0 || c == 0) return PCR_OK;
   const int r3 = (int)r3l;
-  // hot window: every spherical corner lies below r^2 + 8r + 5
-  int hw = skip_neg ? r * r + 8 * r + 8 : 2048;
+  // hot window: every spherical corner lies below r^2 + 8r + 5.  Rounded up
+  // to 32 voxels, so the zero stream past it starts on a 128-byte line: from
+  // r^2 + 8r + 8 (1288 at r = 32) every 1 KB wave store split a line with the
+  // next one, and the c3 backward took 0.617 ms alone against 0.528 aligned
+  // (c3 step 1.91 -> 1.81-1.85 ms, profiles/r06_ab_devox_bwd_align.log)
+  int hw = skip_neg ? (r * r + 8 * r + 8 + 31) / 32 * 32 : 2048;
   if (hw > r3) hw = r3;
   int G = kBwdMaxG;
   if (!skip_neg && hw < r3 && (size_t)r3 * 4 <= 128 * 1024) {
