@@ -4,6 +4,8 @@ prep (pcr_extractor_voxel_prep), the means launch (pcr_extractor_voxel_means)
 and the grid stream from those means (pcr_extractor_voxel_stream_devox); the
 round-6 grid stream that formed the means itself was timed with it
 (profiles/r06_ab_stream_means.log).
+Clouds past the stream's devox role (c3) time prep, the means + devox launch
+and the grid stream without devox.
 usage: [CFG=BxNxCxR,...] python scripts/voxel_chain_time.py"""
 import os
 import sys
@@ -51,12 +53,27 @@ for b, n, c, r in cfgs:
             b, c, n, r, _ptr(cnt), _ptr(grid), _ptr(devox), _ptr(dwgts), _ptr(desc), _ptr(ws),
             ws.numel(), st), "stream_devox")
 
-    prep()
-    means()
-    stream_devox()
+    def means_devox():
+        cnt, grid, devox, desc = outs[0]
+        _lib.check(lib.pcr_extractor_voxel_means_devox(
+            _ptr(feat), b, c, n, r, _ptr(devox), _ptr(dinds), _ptr(dwgts), _ptr(desc), _ptr(ws),
+            ws.numel(), st), "means_devox")
+
+    def stream():
+        cnt, grid, devox, desc = outs[0]
+        _lib.check(lib.pcr_extractor_voxel_stream(b, c, n, r, _ptr(cnt), _ptr(grid), _ptr(ws),
+                                                  ws.numel(), st), "stream")
+
+    # clouds past the stream's devox role (c3: 2048 points): the means launch
+    # evaluates the devox, the grid stream writes grid + cnt only
+    dv = bool(lib.pcr_extractor_stream_devox_ok(n, c, r))
+    launches = (("prep", prep), ("means", means), ("stream_devox", stream_devox)) if dv else \
+        (("prep", prep), ("means_devox", means_devox), ("stream", stream))
+    for _, f in launches:
+        f()
     torch.cuda.synchronize()
     res = {}
-    for name, f in (("prep", prep), ("means", means), ("stream_devox", stream_devox)):
+    for name, f in launches:
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(30)]
         for e0, e1 in ev:
